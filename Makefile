@@ -1,0 +1,52 @@
+# Build of the MI355X batched SHA-256 library (in-tree, so the .so travels to the GPU box).
+#
+#   make            -> s3client_amd/lib/libs3hash.so  (C-ABI + lib/hash C++ drop-in + kernels)
+#                      oracle/liboracle.so (+ oracle/_ref when /root/reference exists)
+#                      tests/cpp binaries (drop-in link tests)
+HIPCC   ?= /opt/rocm/bin/hipcc
+CXX     ?= g++
+ARCH    ?= gfx950
+LIBDIR  := s3client_amd/lib
+CSRC    := s3client_amd/csrc
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -fno-slp-vectorize
+CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Iinclude
+
+LIB := $(LIBDIR)/libs3hash.so
+
+all: $(LIB) oracle
+
+$(LIBDIR)/capi.o: $(CSRC)/capi.hip $(CSRC)/sha256_kernels.hip $(CSRC)/sha256_device.hpp include/s3hash.h
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIBDIR)/lib_hash.o: $(CSRC)/cpu/lib_hash.cpp include/sha256.h include/utility.h include/s3hash.h
+	@mkdir -p $(LIBDIR)
+	$(CXX) $(CXXFLAGS) -c -o $@ $<
+
+$(LIB): $(LIBDIR)/capi.o $(LIBDIR)/lib_hash.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
+
+oracle:
+	$(MAKE) -C oracle
+
+CPPTESTS := tests/cpp/build/dropin_test tests/cpp/build/sign_test
+cpptests: $(CPPTESTS)
+
+tests/cpp/build/dropin_test: tests/cpp/dropin_test.cpp $(LIB)
+	@mkdir -p tests/cpp/build
+	$(CXX) -O2 -std=c++17 -Iinclude -o $@ $< -L$(LIBDIR) -ls3hash -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)'
+
+tests/cpp/build/sign_test: tests/cpp/sign_test.cpp s3client_amd/host/aws_sign.cpp s3client_amd/host/aws_sign.h $(LIB)
+	@mkdir -p tests/cpp/build
+	$(CXX) -O2 -std=c++17 -Iinclude -Is3client_amd/host -o $@ $< s3client_amd/host/aws_sign.cpp \
+	    -L$(LIBDIR) -ls3hash -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)'
+
+isa: $(CSRC)/capi.hip
+	@mkdir -p build/isa
+	cd build/isa && $(HIPCC) $(HIPFLAGS) -c -save-temps -o capi.o ../../$(CSRC)/capi.hip
+
+clean:
+	rm -rf $(LIBDIR) tests/cpp/build build
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle cpptests isa clean

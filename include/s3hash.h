@@ -1,0 +1,111 @@
+/* include/s3hash.h -- C-ABI of the MI355X batched SHA-256 path (libs3hash.so).
+ *
+ * This is the boundary the S3 client links against for PAYLOAD hashing: plain pointers and
+ * sizes, int status codes, no C++ or HIP types, no exceptions.  It sits beside the C++
+ * drop-in of lib/hash (include/sha256.h, include/utility.h), whose single-message calls stay
+ * on the CPU exactly as in the reference.
+ *
+ * Reference interfaces each entry point serves (paths under /root/reference):
+ *   s3h_sha256_batch_device / s3h_plan_*  -- batched form of sha256::sha256
+ *       (lib/hash/sha256.h:70, lib/hash/sha256.cpp:147-160), applied to the parts that
+ *       lib/src/upload.cpp:89-110 (UploadParts) slices, before each part's digest is passed
+ *       as `payloadHash` to S3Api::UploadFilePart (lib/include/s3-api.h:447-452).
+ *   s3h_sha256_batch_host  -- the same starting and ending in host memory (file chunks
+ *       staged for upload -> 32-byte digests handed back to the SigV4 signer,
+ *       lib/src/aws_sign.cpp:236-237 x-amz-content-sha256).
+ *   s3h_plan_launch_range  -- resumable chaining state: sha256::sha256_stream semantics
+ *       (lib/hash/sha256.h:97, sha256.cpp:84-144) for many parts at once.
+ *
+ * Digest layout (every entry point): 8 uint32 words per part with word i = bswap32(H_i),
+ * exactly lib/hash's `to_little` output (sha256.h:103-106); on little-endian hosts the 32
+ * bytes in memory are the canonical SHA-256 digest, and sha256::hash_to_text prints them.
+ */
+#ifndef S3HASH_H
+#define S3HASH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define S3H_API_VERSION 1
+
+enum s3h_status {
+  S3H_OK = 0,
+  S3H_EINVAL = -1,   /* bad argument (null pointer, bad device, n too large, ...) */
+  S3H_ENODEV = -2,   /* no HIP device visible: the GPU path never falls back to the CPU */
+  S3H_EHIP = -3,     /* HIP runtime error (message in s3h_last_error) */
+  S3H_ENOMEM = -4    /* device or pinned host allocation failed */
+};
+
+enum s3h_kernel {
+  S3H_KERNEL_AUTO = 0, /* choose by part count */
+  S3H_KERNEL_LANE = 1, /* fused: one lane = schedule + rounds of one part */
+  S3H_KERNEL_PC = 2    /* producer/consumer: producer wave stages W+K through LDS */
+};
+
+/* Last error message of the calling thread ("" if none). */
+const char *s3h_last_error(void);
+int s3h_api_version(void);
+/* Number of visible HIP devices; S3H_ENODEV (and *count = 0) when there is none. */
+int s3h_device_count(int *count);
+
+/* ---------------------------------------------------------------- device-resident path
+ * A plan captures the part geometry (byte offsets relative to a base pointer, lengths) of
+ * one batch, sorted on the host by block count and uploaded once to `device`.  Launching it
+ * hashes every part of a device buffer laid out that way; the same plan can be launched on
+ * many buffers with that layout.  `stream` is a hipStream_t (NULL = the null stream). */
+typedef struct s3h_plan_s *s3h_plan_t;
+
+int s3h_plan_create(int device, const uint64_t *offsets, const uint64_t *lengths, uint64_t n,
+                    int kernel, s3h_plan_t *plan);
+int s3h_plan_destroy(s3h_plan_t plan);
+/* Asynchronous on `stream`: d_base and d_digests (n*8 uint32) are device pointers. */
+int s3h_plan_launch(s3h_plan_t plan, const void *d_base, uint32_t *d_digests, void *stream);
+/* Resumable form: process blocks [blk_begin, blk_end) of every part, where part p's block b
+ * lives at d_base + offsets[p] + 64*(b - blk_origin).  Chaining state is kept in the plan
+ * between launches (same stream order required); a part's digest is written by the launch
+ * that processes its final (padding) block. */
+int s3h_plan_launch_range(s3h_plan_t plan, const void *d_base, uint32_t *d_digests,
+                          uint64_t blk_begin, uint64_t blk_end, uint64_t blk_origin,
+                          void *stream);
+/* Introspection: total 64-B compressions, max blocks of any part, chosen kernel, grid size. */
+int s3h_plan_info(s3h_plan_t plan, uint64_t *n, uint64_t *total_blocks, uint64_t *max_blocks,
+                  int *kernel, uint32_t *grid);
+
+/* One-shot convenience: plan + launch + wait.  Returns when d_digests is complete. */
+int s3h_sha256_batch_device(int device, const void *d_base, const uint64_t *offsets,
+                            const uint64_t *lengths, uint64_t n, uint32_t *d_digests,
+                            void *stream);
+
+/* ---------------------------------------------------------------- host-resident path
+ * parts[i] (host memory, pinned or pageable) of lengths[i] bytes -> digests (host, n*8).
+ * Parts are sharded round-robin over `ndevices` GPUs (0 = all visible), part i on device
+ * i % ndevices; each device streams its parts through HBM in slices of `slice_bytes` per
+ * part (0 = default 4 MiB) with copies overlapped with hashing.  Blocking. */
+int s3h_sha256_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
+                          uint32_t *digests, int ndevices, uint64_t slice_bytes);
+
+/* ---------------------------------------------------------------- synthetic inputs
+ * Fill part i (at d_base + offsets[i], 8-B aligned, lengths[i] bytes) with generator
+ * G(seed, part_ids[i], lengths[i]) of SURVEY.md 8(d).  Asynchronous on `stream`. */
+int s3h_generate_parts(int device, void *d_base, const uint64_t *offsets,
+                       const uint64_t *lengths, const uint64_t *part_ids, uint64_t n,
+                       uint64_t seed, void *stream);
+
+/* ---------------------------------------------------------------- CPU drop-in (C view)
+ * C entry points of the lib/hash drop-in that the same library exports in C++ form
+ * (namespace sha256, include/sha256.h).  Single messages: CPU, never the GPU. */
+void s3h_cpu_sha256(const uint8_t *data, uint64_t length, uint32_t hash[8]);
+void s3h_cpu_hmac256(const uint8_t *data, uint64_t length, const uint8_t *key,
+                     uint64_t key_length, uint8_t mac[32]);
+/* lowercase hex of the 32 digest bytes + NUL (sha256::hash_to_text). */
+void s3h_hash_to_text(const uint32_t hash[8], char text[65]);
+/* "sha-ni" or "scalar": which compression the CPU drop-in dispatched to. */
+const char *s3h_cpu_backend(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* S3HASH_H */

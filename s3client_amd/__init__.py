@@ -1,0 +1,13 @@
+"""s3client_amd -- MI355X-native (gfx950) batched SHA-256 for S3 upload-part payload hashing.
+
+Drop-in for uv-cpp/s3client's lib/hash on the payload-hashing path; see DESIGN.md.
+"""
+from .hashing import (Plan, device_count, digests_to_text, generate_parts, hash_to_text,
+                      hmac256, nblocks, sha256, sha256_batch_device, sha256_batch_host,
+                      cpu_backend)
+from .upload import upload_parts_geometry, UploadPart
+from ._native import S3HashError, LIB_PATH
+
+__all__ = ["Plan", "device_count", "digests_to_text", "generate_parts", "hash_to_text",
+           "hmac256", "nblocks", "sha256", "sha256_batch_device", "sha256_batch_host",
+           "cpu_backend", "upload_parts_geometry", "UploadPart", "S3HashError", "LIB_PATH"]

@@ -1,0 +1,95 @@
+"""ctypes binding of libs3hash.so (the C-ABI declared in include/s3hash.h).
+
+The library is built in-tree (``make`` at the repo root, or ``__graft_entry__.build()``) to
+``s3client_amd/lib/libs3hash.so``.  There is no fallback: if the library is missing, every
+entry point raises, and the batched GPU entry points raise when no HIP device is visible.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libs3hash.so")
+
+S3H_OK, S3H_EINVAL, S3H_ENODEV, S3H_EHIP, S3H_ENOMEM = 0, -1, -2, -3, -4
+KERNEL_AUTO, KERNEL_LANE, KERNEL_PC = 0, 1, 2
+KERNEL_NAMES = {KERNEL_AUTO: "auto", KERNEL_LANE: "lane", KERNEL_PC: "pc"}
+
+# every symbol include/s3hash.h declares (tests check the library exports all of them)
+C_ABI_SYMBOLS = (
+    "s3h_last_error", "s3h_api_version", "s3h_device_count",
+    "s3h_plan_create", "s3h_plan_destroy", "s3h_plan_launch", "s3h_plan_launch_range",
+    "s3h_plan_info", "s3h_sha256_batch_device", "s3h_sha256_batch_host",
+    "s3h_generate_parts", "s3h_cpu_sha256", "s3h_cpu_hmac256", "s3h_hash_to_text",
+    "s3h_cpu_backend",
+)
+# the lib/hash drop-in (C++ mangled names identical to the reference's libs3client.a)
+CXX_DROPIN_SYMBOLS = (
+    "_ZN6sha2566sha256EPKhmPj",          # sha256::sha256(const uint8_t*, size_t, uint32_t*)
+    "_ZN6sha25613sha256_streamEPjPKhm",  # sha256::sha256_stream(uint32_t*, const uint8_t*, uint64_t)
+    "_ZN6sha25611sha256_nextEPKhjPjmPh", # sha256::sha256_next(...)
+    "_ZN6sha25610print_hashEPj",         # sha256::print_hash(uint32_t*)
+    "_ZN6sha25611sha256_fileEPKcPj",     # sha256::sha256_file(const char*, uint32_t*)
+    "_Z7hmac256PKhmS0_mPh",              # hmac256(...)
+    "_Z12alloc_paddedmmPmPh",            # alloc_padded(...)
+)
+
+
+class S3HashError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"s3hash error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+_lock = threading.Lock()
+
+u64p = ctypes.POINTER(ctypes.c_uint64)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+
+
+def lib() -> ctypes.CDLL:
+    """Load libs3hash.so once; raise loudly if it has not been built."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise S3HashError(S3H_EINVAL, f"{LIB_PATH} missing: run `make` (or "
+                                  "__graft_entry__.build()) -- there is no fallback path")
+            L = ctypes.CDLL(LIB_PATH)
+            L.s3h_last_error.restype = ctypes.c_char_p
+            L.s3h_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+            L.s3h_plan_create.argtypes = [ctypes.c_int, u64p, u64p, ctypes.c_uint64, ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_void_p)]
+            L.s3h_plan_destroy.argtypes = [ctypes.c_void_p]
+            L.s3h_plan_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p]
+            L.s3h_plan_launch_range.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                ctypes.c_void_p]
+            L.s3h_plan_info.argtypes = [ctypes.c_void_p, u64p, u64p, u64p,
+                                        ctypes.POINTER(ctypes.c_int), u32p]
+            L.s3h_sha256_batch_device.argtypes = [ctypes.c_int, ctypes.c_void_p, u64p, u64p,
+                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+            L.s3h_sha256_batch_host.argtypes = [ctypes.POINTER(ctypes.c_void_p), u64p,
+                                                ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
+                                                ctypes.c_uint64]
+            L.s3h_generate_parts.argtypes = [ctypes.c_int, ctypes.c_void_p, u64p, u64p, u64p,
+                                             ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
+            L.s3h_cpu_sha256.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+            L.s3h_cpu_sha256.restype = None
+            L.s3h_cpu_hmac256.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                          ctypes.c_uint64, ctypes.c_void_p]
+            L.s3h_cpu_hmac256.restype = None
+            L.s3h_hash_to_text.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+            L.s3h_hash_to_text.restype = None
+            L.s3h_cpu_backend.restype = ctypes.c_char_p
+            _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != S3H_OK:
+        raise S3HashError(rc, lib().s3h_last_error().decode(errors="replace"))

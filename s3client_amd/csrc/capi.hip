@@ -1,0 +1,368 @@
+// capi.hip -- host side of the C-ABI in include/s3hash.h.
+//
+// Everything here is plumbing around the kernels of sha256_kernels.hip: plan building
+// (host-side sort by block count), launches, the host-resident streaming path and the
+// multi-GPU sharding.  No entry point ever computes a digest on the CPU for the batched API:
+// with no HIP device every call fails with S3H_ENODEV.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/s3hash.h"
+#include "sha256_kernels.hip"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return fail(e_ == hipErrorOutOfMemory ? S3H_ENOMEM : S3H_EHIP, "%s: %s (%s:%d)",     \
+                  #expr, hipGetErrorString(e_), __FILE__, __LINE__);                       \
+  } while (0)
+
+int check_device(int device) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+    return fail(S3H_ENODEV, "no HIP device visible (the batched SHA-256 path has no CPU fallback)");
+  if (device < 0 || device >= count) return fail(S3H_EINVAL, "device %d out of range [0,%d)", device, count);
+  return S3H_OK;
+}
+
+struct DeviceGuard {  // restores the calling thread's current device
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace
+
+struct s3h_plan_s {
+  int device = 0;
+  int kernel = S3H_KERNEL_PC;
+  uint64_t n = 0;
+  uint64_t total_blocks = 0;
+  uint64_t max_blocks = 0;
+  uint32_t grid = 0;
+  s3h::Slot* d_slots = nullptr;
+  uint32_t* d_out_idx = nullptr;
+  uint32_t* d_state = nullptr;  // n*8 chaining words, allocated on first ranged launch
+};
+
+namespace {
+
+// Above this many parts every SIMD already holds >= 1 consumer+producer pair, and the fused
+// kernel's lower instruction total (no LDS traffic) wins; below it per-chain latency rules.
+constexpr uint64_t kPcMaxParts = 65536;
+constexpr uint64_t kMaxParts = 1ull << 31;
+
+int plan_build(int device, const uint64_t* offsets, const uint64_t* lengths, uint64_t n,
+               int kernel, s3h_plan_s** out) {
+  *out = nullptr;
+  if (!offsets || !lengths || n == 0 || n > kMaxParts)
+    return fail(S3H_EINVAL, "plan: need offsets, lengths and 0 < n <= 2^31 (n=%llu)",
+                (unsigned long long)n);
+  if (int rc = check_device(device)) return rc;
+  if (kernel == S3H_KERNEL_AUTO) kernel = n <= kPcMaxParts ? S3H_KERNEL_PC : S3H_KERNEL_LANE;
+  if (kernel != S3H_KERNEL_PC && kernel != S3H_KERNEL_LANE)
+    return fail(S3H_EINVAL, "plan: unknown kernel %d", kernel);
+
+  std::vector<uint32_t> order(n);
+  std::iota(order.begin(), order.end(), 0u);
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+    return s3h::nblocks(lengths[a]) > s3h::nblocks(lengths[b]);
+  });
+  std::vector<s3h::Slot> slots(n);
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    slots[i] = {offsets[order[i]], lengths[order[i]]};
+    total += s3h::nblocks(lengths[order[i]]);
+  }
+
+  auto* P = new s3h_plan_s();
+  P->device = device;
+  P->kernel = kernel;
+  P->n = n;
+  P->total_blocks = total;
+  P->max_blocks = s3h::nblocks(slots[0].len);
+  P->grid = kernel == S3H_KERNEL_PC ? uint32_t((n + 63) / 64) : uint32_t((n + 255) / 256);
+
+  DeviceGuard g(device);
+  hipError_t e = hipMalloc(&P->d_slots, n * sizeof(s3h::Slot));
+  if (e == hipSuccess) e = hipMalloc(&P->d_out_idx, n * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemcpy(P->d_slots, slots.data(), n * sizeof(s3h::Slot), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(P->d_out_idx, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(P->d_slots);
+    (void)hipFree(P->d_out_idx);
+    delete P;
+    return fail(e == hipErrorOutOfMemory ? S3H_ENOMEM : S3H_EHIP, "plan upload: %s", hipGetErrorString(e));
+  }
+  *out = P;
+  return S3H_OK;
+}
+
+int plan_launch(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint64_t b0, uint64_t b1,
+                uint64_t origin, hipStream_t stream, bool ranged) {
+  if (!P || !d_base || !d_digests) return fail(S3H_EINVAL, "launch: null plan/base/digests");
+  if (b1 <= b0) return S3H_OK;
+  DeviceGuard g(P->device);
+  if (ranged && !P->d_state) HIP_TRY(hipMalloc(&P->d_state, P->n * 8 * sizeof(uint32_t)));
+  s3h::LaunchArgs A;
+  A.base = static_cast<const uint8_t*>(d_base);
+  A.slots = P->d_slots;
+  A.out_idx = P->d_out_idx;
+  A.state = ranged ? P->d_state : nullptr;
+  A.digests = d_digests;
+  A.blk_begin = b0;
+  A.blk_end = b1;
+  A.blk_origin = origin;
+  A.n = uint32_t(P->n);
+  if (P->kernel == S3H_KERNEL_PC)
+    hipLaunchKernelGGL(s3h::sha256_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
+  else
+    hipLaunchKernelGGL(s3h::sha256_lane_kernel, dim3(P->grid), dim3(256), 0, stream, A);
+  HIP_TRY(hipGetLastError());
+  return S3H_OK;
+}
+
+// ------------------------------------------------------------------ host streaming path
+struct HostShard {
+  int device;
+  std::vector<uint64_t> parts;  // global part indices on this device
+};
+
+int run_host_shard(const HostShard& sh, const uint8_t* const* parts, const uint64_t* lengths,
+                   uint32_t* digests, uint64_t slice) {
+  const uint64_t n = sh.parts.size();
+  if (n == 0) return S3H_OK;
+  DeviceGuard g(sh.device);
+  std::vector<uint64_t> offs(n), lens(n);
+  for (uint64_t j = 0; j < n; ++j) {
+    offs[j] = j * slice;
+    lens[j] = lengths[sh.parts[j]];
+  }
+  s3h_plan_s* P = nullptr;
+  if (int rc = plan_build(sh.device, offs.data(), lens.data(), n, S3H_KERNEL_AUTO, &P)) return rc;
+  struct Cleanup {
+    s3h_plan_s* P;
+    ~Cleanup() { s3h_plan_destroy(P); }
+  } cleanup{P};
+
+  constexpr int kRing = 3;
+  uint8_t* ring = nullptr;
+  uint32_t* d_dig = nullptr;
+  hipStream_t copy_s = nullptr, hash_s = nullptr;
+  hipEvent_t copied[kRing], hashed[kRing];
+  HIP_TRY(hipMalloc(&ring, kRing * n * slice));
+  struct Free {
+    void* p;
+    ~Free() { (void)hipFree(p); }
+  } f1{ring};
+  HIP_TRY(hipMalloc(&d_dig, n * 8 * sizeof(uint32_t)));
+  Free f2{d_dig};
+  HIP_TRY(hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&hash_s, hipStreamNonBlocking));
+  for (int r = 0; r < kRing; ++r) {
+    HIP_TRY(hipEventCreateWithFlags(&copied[r], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&hashed[r], hipEventDisableTiming));
+  }
+  const uint64_t bps = slice / 64;  // blocks per slice
+  int rc = S3H_OK;
+  uint64_t k = 0;
+  for (uint64_t b0 = 0; b0 < P->max_blocks; b0 += bps, ++k) {
+    const int r = int(k % kRing);
+    uint8_t* slot_base = ring + uint64_t(r) * n * slice;
+    if (k >= kRing) {
+      hipError_t e = hipStreamWaitEvent(copy_s, hashed[r], 0);
+      if (e != hipSuccess) { rc = fail(S3H_EHIP, "wait: %s", hipGetErrorString(e)); break; }
+    }
+    const uint64_t byte0 = b0 * 64;
+    for (uint64_t j = 0; j < n && rc == S3H_OK; ++j) {
+      const uint64_t len = lens[j];
+      if (byte0 >= len) continue;
+      const uint64_t cnt = std::min(slice, len - byte0);
+      hipError_t e = hipMemcpyAsync(slot_base + j * slice, parts[sh.parts[j]] + byte0, cnt,
+                                    hipMemcpyHostToDevice, copy_s);
+      if (e != hipSuccess) rc = fail(S3H_EHIP, "H2D: %s", hipGetErrorString(e));
+    }
+    if (rc) break;
+    hipError_t e = hipEventRecord(copied[r], copy_s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(hash_s, copied[r], 0);
+    if (e != hipSuccess) { rc = fail(S3H_EHIP, "event: %s", hipGetErrorString(e)); break; }
+    rc = plan_launch(P, slot_base, d_dig, b0, b0 + bps, b0, hash_s, true);
+    if (rc) break;
+    e = hipEventRecord(hashed[r], hash_s);
+    if (e != hipSuccess) { rc = fail(S3H_EHIP, "event: %s", hipGetErrorString(e)); break; }
+  }
+  std::vector<uint32_t> local(n * 8);
+  if (rc == S3H_OK) {
+    hipError_t e = hipMemcpyAsync(local.data(), d_dig, n * 32, hipMemcpyDeviceToHost, hash_s);
+    if (e == hipSuccess) e = hipStreamSynchronize(hash_s);
+    if (e != hipSuccess) rc = fail(S3H_EHIP, "D2H digests: %s", hipGetErrorString(e));
+  }
+  (void)hipStreamSynchronize(copy_s);
+  (void)hipStreamSynchronize(hash_s);
+  for (int r = 0; r < kRing; ++r) {
+    (void)hipEventDestroy(copied[r]);
+    (void)hipEventDestroy(hashed[r]);
+  }
+  (void)hipStreamDestroy(copy_s);
+  (void)hipStreamDestroy(hash_s);
+  if (rc == S3H_OK)
+    for (uint64_t j = 0; j < n; ++j) std::memcpy(digests + 8 * sh.parts[j], &local[8 * j], 32);
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* s3h_last_error(void) { return g_err.c_str(); }
+int s3h_api_version(void) { return S3H_API_VERSION; }
+
+int s3h_device_count(int* count) {
+  if (!count) return fail(S3H_EINVAL, "null count");
+  *count = 0;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess || c <= 0) return fail(S3H_ENODEV, "no HIP device visible");
+  *count = c;
+  return S3H_OK;
+}
+
+int s3h_plan_create(int device, const uint64_t* offsets, const uint64_t* lengths, uint64_t n,
+                    int kernel, s3h_plan_t* plan) {
+  if (!plan) return fail(S3H_EINVAL, "null plan out-pointer");
+  return plan_build(device, offsets, lengths, n, kernel, plan);
+}
+
+int s3h_plan_destroy(s3h_plan_t P) {
+  if (!P) return S3H_OK;
+  DeviceGuard g(P->device);
+  (void)hipFree(P->d_slots);
+  (void)hipFree(P->d_out_idx);
+  (void)hipFree(P->d_state);
+  delete P;
+  return S3H_OK;
+}
+
+int s3h_plan_launch(s3h_plan_t P, const void* d_base, uint32_t* d_digests, void* stream) {
+  if (!P) return fail(S3H_EINVAL, "null plan");
+  return plan_launch(P, d_base, d_digests, 0, P->max_blocks, 0, static_cast<hipStream_t>(stream), false);
+}
+
+int s3h_plan_launch_range(s3h_plan_t P, const void* d_base, uint32_t* d_digests, uint64_t b0,
+                          uint64_t b1, uint64_t origin, void* stream) {
+  if (!P) return fail(S3H_EINVAL, "null plan");
+  if (origin > b0) return fail(S3H_EINVAL, "blk_origin (%llu) > blk_begin (%llu)",
+                               (unsigned long long)origin, (unsigned long long)b0);
+  return plan_launch(P, d_base, d_digests, b0, b1, origin, static_cast<hipStream_t>(stream), true);
+}
+
+int s3h_plan_info(s3h_plan_t P, uint64_t* n, uint64_t* total_blocks, uint64_t* max_blocks,
+                  int* kernel, uint32_t* grid) {
+  if (!P) return fail(S3H_EINVAL, "null plan");
+  if (n) *n = P->n;
+  if (total_blocks) *total_blocks = P->total_blocks;
+  if (max_blocks) *max_blocks = P->max_blocks;
+  if (kernel) *kernel = P->kernel;
+  if (grid) *grid = P->grid;
+  return S3H_OK;
+}
+
+int s3h_sha256_batch_device(int device, const void* d_base, const uint64_t* offsets,
+                            const uint64_t* lengths, uint64_t n, uint32_t* d_digests,
+                            void* stream) {
+  s3h_plan_s* P = nullptr;
+  if (int rc = plan_build(device, offsets, lengths, n, S3H_KERNEL_AUTO, &P)) return rc;
+  int rc = plan_launch(P, d_base, d_digests, 0, P->max_blocks, 0, static_cast<hipStream_t>(stream), false);
+  if (rc == S3H_OK) {
+    DeviceGuard g(device);
+    hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) rc = fail(S3H_EHIP, "batch_device sync: %s", hipGetErrorString(e));
+  }
+  s3h_plan_destroy(P);
+  return rc;
+}
+
+int s3h_sha256_batch_host(const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
+                          uint32_t* digests, int ndevices, uint64_t slice_bytes) {
+  if (!parts || !lengths || !digests || n == 0) return fail(S3H_EINVAL, "batch_host: bad arguments");
+  int count = 0;
+  if (int rc = s3h_device_count(&count)) return rc;
+  if (ndevices <= 0 || ndevices > count) ndevices = count;
+  if (slice_bytes == 0) slice_bytes = 4ull << 20;
+  if (slice_bytes % 64) return fail(S3H_EINVAL, "slice_bytes must be a multiple of 64");
+  for (uint64_t i = 0; i < n; ++i)
+    if (!parts[i] && lengths[i]) return fail(S3H_EINVAL, "batch_host: part %llu is null", (unsigned long long)i);
+  std::vector<HostShard> shards(ndevices);
+  for (int d = 0; d < ndevices; ++d) shards[d].device = d;
+  for (uint64_t i = 0; i < n; ++i) shards[i % ndevices].parts.push_back(i);
+  std::vector<int> rcs(ndevices, S3H_OK);
+  std::vector<std::string> errs(ndevices);
+  std::vector<std::thread> pool;
+  for (int d = 0; d < ndevices; ++d)
+    pool.emplace_back([&, d] {
+      rcs[d] = run_host_shard(shards[d], parts, lengths, digests, slice_bytes);
+      if (rcs[d]) errs[d] = g_err;
+    });
+  for (auto& t : pool) t.join();
+  for (int d = 0; d < ndevices; ++d)
+    if (rcs[d]) return fail(rcs[d], "device %d: %s", d, errs[d].c_str());
+  return S3H_OK;
+}
+
+int s3h_generate_parts(int device, void* d_base, const uint64_t* offsets, const uint64_t* lengths,
+                       const uint64_t* part_ids, uint64_t n, uint64_t seed, void* stream) {
+  if (!d_base || !offsets || !lengths || !part_ids || n == 0 || n > 65535)
+    return fail(S3H_EINVAL, "generate: bad arguments (n must be in [1, 65535] per call)");
+  if (int rc = check_device(device)) return rc;
+  std::vector<s3h::GenPart> g(n);
+  uint64_t maxlen = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (offsets[i] % 8) return fail(S3H_EINVAL, "generate: offsets must be 8-byte aligned");
+    g[i] = {offsets[i], lengths[i], part_ids[i]};
+    maxlen = std::max(maxlen, lengths[i]);
+  }
+  DeviceGuard dg(device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  s3h::GenPart* d_g = nullptr;
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&d_g), n * sizeof(s3h::GenPart), s));
+  HIP_TRY(hipMemcpyAsync(d_g, g.data(), n * sizeof(s3h::GenPart), hipMemcpyHostToDevice, s));
+  const uint64_t words = (maxlen + 7) / 8;
+  const uint32_t gx = uint32_t(std::min<uint64_t>(std::max<uint64_t>((words + 255) / 256, 1), 256));
+  hipLaunchKernelGGL(s3h::generate_kernel, dim3(gx, uint32_t(n)), dim3(256), 0, s,
+                     static_cast<uint8_t*>(d_base), d_g, seed);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipFreeAsync(d_g, s));
+  // the host vector `g` must outlive the async copy
+  HIP_TRY(hipStreamSynchronize(s));
+  return S3H_OK;
+}
+
+}  // extern "C"

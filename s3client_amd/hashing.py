@@ -1,0 +1,187 @@
+"""Python view of the MI355X batched SHA-256 path (over the C-ABI, include/s3hash.h).
+
+Mirrors lib/hash's interface (/root/reference/lib/hash/sha256.h):
+  * ``sha256(data)``        -> 8 digest words, ``hash[i] = bswap32(H_i)`` (sha256.h:70, CPU)
+  * ``hmac256(data, key)``  -> 32-byte MAC (hmac256.cpp:60-95, CPU)
+  * ``hash_to_text(words)`` -> 64 lowercase hex chars (sha256.h:113-119)
+and adds the batched GPU entry points that the parallel upload uses for per-part payload
+hashes (lib/src/upload.cpp:89-110 -> S3Api::UploadFilePart(..., payloadHash)):
+  * ``Plan`` / ``sha256_batch_device``  -- parts already resident in HBM (torch tensors)
+  * ``sha256_batch_host``               -- parts in host memory, sharded over GPUs
+
+Device memory, streams and events come from PyTorch (plumbing only); all hashing is done by
+the HIP kernels in s3client_amd/csrc.  Nothing here falls back to the CPU for a batch.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from . import _native
+from ._native import check, lib
+
+DIGEST_WORDS = 8
+
+
+def _u64(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint64))
+
+
+def _p64(a: np.ndarray):
+    return a.ctypes.data_as(_native.u64p)
+
+
+def device_count() -> int:
+    c = ctypes.c_int(0)
+    rc = lib().s3h_device_count(ctypes.byref(c))
+    return c.value if rc == 0 else 0
+
+
+def nblocks(length: int) -> int:
+    """64-byte compressions SHA-256 performs on a message of ``length`` bytes."""
+    return (int(length) + 72) // 64
+
+
+def _stream_handle(stream) -> int | None:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    return getattr(stream, "cuda_stream", stream)
+
+
+class Plan:
+    """Geometry of one batch of parts, uploaded once (s3h_plan_create)."""
+
+    def __init__(self, offsets: Sequence[int], lengths: Sequence[int], device: int = 0,
+                 kernel: str | int = "auto"):
+        k = kernel if isinstance(kernel, int) else {"auto": 0, "lane": 1, "pc": 2}[kernel]
+        self.offsets, self.lengths = _u64(offsets), _u64(lengths)
+        if self.offsets.shape != self.lengths.shape or self.offsets.ndim != 1:
+            raise ValueError("offsets and lengths must be 1-D and of equal length")
+        self.n = int(self.lengths.size)
+        self.device = device
+        h = ctypes.c_void_p()
+        check(lib().s3h_plan_create(device, _p64(self.offsets), _p64(self.lengths), self.n, k,
+                                    ctypes.byref(h)))
+        self._h = h
+
+    def info(self) -> dict:
+        n, tb, mb = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        k, g = ctypes.c_int(), ctypes.c_uint32()
+        check(lib().s3h_plan_info(self._h, ctypes.byref(n), ctypes.byref(tb), ctypes.byref(mb),
+                                  ctypes.byref(k), ctypes.byref(g)))
+        return {"n": n.value, "total_blocks": tb.value, "max_blocks": mb.value,
+                "kernel": _native.KERNEL_NAMES[k.value], "grid": g.value}
+
+    def _check_buffers(self, data, digests):
+        import torch
+        if not (data.is_cuda and digests.is_cuda):
+            raise ValueError("data and digests must be device tensors")
+        if digests.numel() * digests.element_size() < 32 * self.n:
+            raise ValueError("digests buffer too small (need n*32 bytes)")
+        end = int((self.offsets + self.lengths).max()) if self.n else 0
+        if data.numel() * data.element_size() < end:
+            raise ValueError(f"data buffer ({data.numel() * data.element_size()} B) smaller "
+                             f"than the plan's extent ({end} B)")
+        del torch
+
+    def launch(self, data, digests, stream=None) -> None:
+        """Hash every part of ``data`` (device tensor) into ``digests`` (n*8 words)."""
+        self._check_buffers(data, digests)
+        check(lib().s3h_plan_launch(self._h, ctypes.c_void_p(data.data_ptr()),
+                                    ctypes.c_void_p(digests.data_ptr()),
+                                    ctypes.c_void_p(_stream_handle(stream))))
+
+    def launch_range(self, data_ptr: int, digests, blk_begin: int, blk_end: int,
+                     blk_origin: int, stream=None) -> None:
+        check(lib().s3h_plan_launch_range(self._h, ctypes.c_void_p(data_ptr),
+                                          ctypes.c_void_p(digests.data_ptr()), blk_begin,
+                                          blk_end, blk_origin,
+                                          ctypes.c_void_p(_stream_handle(stream))))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().s3h_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def sha256_batch_device(data, offsets, lengths, device: int | None = None, kernel="auto",
+                        stream=None):
+    """Digest every part [offsets[i], offsets[i]+lengths[i]) of the device tensor ``data``.
+
+    Returns an (n, 8) int32 device tensor holding the uint32 digest words (lib/hash layout)."""
+    import torch
+    dev = data.device.index if device is None else device
+    with Plan(offsets, lengths, device=dev, kernel=kernel) as plan:
+        out = torch.empty((plan.n, DIGEST_WORDS), dtype=torch.int32, device=data.device)
+        plan.launch(data, out, stream)
+        torch.cuda.current_stream(data.device).synchronize() if stream is None else stream.synchronize()
+    return out
+
+
+def sha256_batch_host(parts: Sequence, ndevices: int = 0, slice_bytes: int = 0) -> np.ndarray:
+    """Digest host-resident parts (bytes / numpy uint8 arrays) on the GPUs: (n, 8) uint32."""
+    arrs = [np.frombuffer(p, dtype=np.uint8) if isinstance(p, (bytes, bytearray, memoryview))
+            else np.ascontiguousarray(p, dtype=np.uint8).reshape(-1) for p in parts]
+    n = len(arrs)
+    ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data if a.size else 0 for a in arrs])
+    lens = _u64([a.size for a in arrs])
+    out = np.zeros((n, DIGEST_WORDS), dtype=np.uint32)
+    check(lib().s3h_sha256_batch_host(ptrs, _p64(lens), n, out.ctypes.data, ndevices,
+                                      slice_bytes))
+    return out
+
+
+def generate_parts(data, offsets, lengths, part_ids, seed: int, stream=None) -> None:
+    """Fill parts of device tensor ``data`` with generator G(seed, part_id, length)."""
+    offs, lens, ids = _u64(offsets), _u64(lengths), _u64(part_ids)
+    dev = data.device.index
+    for s in range(0, offs.size, 65535):
+        e = min(offs.size, s + 65535)
+        check(lib().s3h_generate_parts(dev, ctypes.c_void_p(data.data_ptr()), _p64(offs[s:e]),
+                                       _p64(lens[s:e]), _p64(ids[s:e]), e - s, seed,
+                                       ctypes.c_void_p(_stream_handle(stream))))
+
+
+# ------------------------------------------------------------------ CPU drop-in (lib/hash)
+def sha256(data: bytes) -> np.ndarray:
+    """lib/hash sha256::sha256 (CPU, single message): 8 words, hash[i] = bswap32(H_i)."""
+    b = bytes(data)
+    out = np.zeros(DIGEST_WORDS, dtype=np.uint32)
+    lib().s3h_cpu_sha256(b, len(b), out.ctypes.data)
+    return out
+
+
+def hmac256(data: bytes, key: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    d, k = bytes(data), bytes(key)
+    lib().s3h_cpu_hmac256(d, len(d), k, len(k), out)
+    return out.raw
+
+
+def hash_to_text(words) -> str:
+    """sha256::hash_to_text: lowercase hex of the 32 digest bytes as laid out in memory."""
+    return np.ascontiguousarray(words, dtype=np.uint32).reshape(8).tobytes().hex()
+
+
+def digests_to_text(words) -> list[str]:
+    w = np.ascontiguousarray(words).view(np.uint32).reshape(-1, DIGEST_WORDS)
+    return [row.tobytes().hex() for row in w]
+
+
+def cpu_backend() -> str:
+    return lib().s3h_cpu_backend().decode()

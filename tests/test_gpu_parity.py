@@ -1,0 +1,180 @@
+"""GPU parity: the HIP kernels (through the C-ABI) against the oracle and the golden vectors.
+
+Bar: bit-exact digests (integer work).  Sizes are chosen so the CPU oracle finishes in
+seconds; the full C2 batch (1024 x 8 MiB) is checked part-by-part against the oracle too."""
+import numpy as np
+import pytest
+
+import s3client_amd as s3
+
+pytestmark = pytest.mark.gpu
+SEED = 20241008
+KERNELS = ["pc", "lane"]
+
+
+def _dev_buffer(torch, host: np.ndarray):
+    t = torch.empty(max(host.size, 1), dtype=torch.uint8, device="cuda")
+    if host.size:
+        t.copy_(torch.from_numpy(host))
+    return t
+
+
+def _run(torch, host_buf, offs, lens, kernel):
+    data = _dev_buffer(torch, host_buf)
+    out = s3.sha256_batch_device(data, offs, lens, kernel=kernel)
+    return out.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_length_edges_all_alignments(torch_cuda, oracle, golden, kernel):
+    """Every golden edge length, placed at byte misalignments 0..3 and 13 (v_perm decode)."""
+    edges = [e for e in golden["edge"] if e["L"] <= (1 << 20) + 13]
+    big = np.frombuffer(oracle.generate(7, max(e["L"] for e in edges)), dtype=np.uint8)
+    offs, lens, want, chunks, pos = [], [], [], [], 0
+    for mis in (0, 1, 2, 3, 13):
+        for e in edges:
+            pos += (-pos) % 64 + mis
+            offs.append(pos)
+            lens.append(e["L"])
+            want.append(e["digest"])
+            chunks.append((pos, big[:e["L"]]))
+            pos += e["L"]
+    host = np.zeros(pos + 64, dtype=np.uint8)
+    for o, c in chunks:
+        host[o:o + c.size] = c
+    got = s3.digests_to_text(_run(torch_cuda, host, offs, lens, kernel))
+    bad = [(lens[i], offs[i] % 4) for i in range(len(want)) if got[i] != want[i]]
+    assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_random_ragged_vs_oracle(torch_cuda, oracle, kernel):
+    rng = np.random.default_rng(2024)
+    n = 777
+    lens = rng.integers(0, 20000, n)
+    lens[:5] = [0, 0, 55, 56, 64]  # empty parts and padding edges
+    gaps = rng.integers(0, 100, n)
+    offs = np.cumsum(gaps + np.concatenate([[0], lens[:-1]]))
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 8, dtype=np.uint8)
+    got = _run(torch_cuda, host, offs, lens, kernel)
+    want = oracle.batch(host, offs, lens)
+    assert np.array_equal(got, want)
+
+
+def test_kernels_agree_on_many_small_parts(torch_cuda, oracle):
+    """n > 65536 exercises the AUTO switch to the fused kernel; overlapping parts allowed."""
+    rng = np.random.default_rng(7)
+    n = 70000
+    lens = rng.integers(0, 200, n)
+    offs = rng.integers(0, 1 << 20, n)
+    host = rng.integers(0, 256, (1 << 20) + 256, dtype=np.uint8)
+    data = _dev_buffer(torch_cuda, host)
+    a = s3.sha256_batch_device(data, offs, lens, kernel="auto").cpu().numpy().view(np.uint32)
+    b = s3.sha256_batch_device(data, offs, lens, kernel="pc").cpu().numpy().view(np.uint32)
+    assert np.array_equal(a, b)
+    idx = rng.choice(n, 500, replace=False)
+    want = oracle.batch(host, offs[idx], lens[idx])
+    assert np.array_equal(a[idx], want)
+
+
+def test_device_generator_matches_oracle(torch_cuda, oracle):
+    lens = [0, 1, 7, 8, 9, 1000, 4097, 65536 + 3]
+    offs = np.concatenate([[0], np.cumsum([(L + 255) // 256 * 256 for L in lens])[:-1]])
+    ids = [5, 6, 7, 8, 9, 10, 11, 1023]
+    data = torch_cuda.zeros(int(offs[-1] + lens[-1]) + 256, dtype=torch_cuda.uint8, device="cuda")
+    s3.generate_parts(data, offs, lens, ids, SEED)
+    host = data.cpu().numpy()
+    for o, L, p in zip(offs, lens, ids):
+        assert host[o:o + L].tobytes() == oracle.generate(p, L), (p, L)
+
+
+def _c2(torch, nparts):
+    L = 8 << 20
+    offs = np.arange(nparts, dtype=np.uint64) * L
+    lens = np.full(nparts, L, dtype=np.uint64)
+    data = torch.empty(nparts * L, dtype=torch.uint8, device="cuda")
+    s3.generate_parts(data, offs, lens, np.arange(nparts), SEED)
+    return data, offs, lens
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_c2_full_batch_bit_exact(torch_cuda, oracle, golden, kernel):
+    """BASELINE config 2: 1024 x 8 MiB in HBM; fixtures p in {0..15, 511, 1022, 1023} and all
+    1024 digests against the oracle on the same bytes."""
+    data, offs, lens = _c2(torch_cuda, 1024)
+    out = s3.sha256_batch_device(data, offs, lens, kernel=kernel).cpu().numpy().view(np.uint32)
+    txt = s3.digests_to_text(out)
+    for e in golden["c2_parts"]:
+        assert txt[e["p"]] == e["digest"], e["p"]
+    if kernel == "pc":
+        host = data.cpu().numpy()
+        want = oracle.batch(host, offs, lens, threads=16)
+        assert np.array_equal(out, want)
+
+
+def test_resumable_ranges_match_single_launch(torch_cuda, oracle):
+    rng = np.random.default_rng(11)
+    n = 200
+    lens = rng.integers(0, 300000, n)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    host = rng.integers(0, 256, int(lens.sum()) + 64, dtype=np.uint8)
+    data = _dev_buffer(torch_cuda, host)
+    for kernel in KERNELS:
+        plan = s3.Plan(offs, lens, kernel=kernel)
+        one = torch_cuda.zeros((n, 8), dtype=torch_cuda.int32, device="cuda")
+        plan.launch(data, one)
+        many = torch_cuda.zeros((n, 8), dtype=torch_cuda.int32, device="cuda")
+        mb = plan.info()["max_blocks"]
+        step = 977
+        for b0 in range(0, mb, step):
+            plan.launch_range(data.data_ptr(), many, b0, b0 + step, 0)
+        torch_cuda.cuda.synchronize()
+        assert torch_cuda.equal(one, many), kernel
+        assert np.array_equal(one.cpu().numpy().view(np.uint32), oracle.batch(host, offs, lens))
+        plan.close()
+
+
+def test_host_path_transfer_geometry(torch_cuda, golden):
+    """test/parallel-file-transfer-test.cpp data sliced by lib/src/upload.cpp geometry, hashed
+    from HOST memory (H2D included), against the reference's digests."""
+    t = golden["transfer"]
+    data = (np.arange(t["size"], dtype=np.uint64) % 128).astype(np.uint8)
+    parts = s3.upload_parts_geometry(t["size"], t["jobs"], t["parts_per_job"])
+    assert [(p.offset, p.size) for p in parts] == [(q["offset"], q["size"]) for q in t["parts"]]
+    from s3client_amd.upload import payload_hashes
+    assert payload_hashes(data, parts) == [q["digest"] for q in t["parts"]]
+
+
+def test_host_path_multipart_and_small_slices(torch_cuda, golden):
+    mp = golden["multipart"]
+    data = (np.arange(mp["size"], dtype=np.uint64) % 256).astype(np.uint8)
+    views = [data[p["offset"]:p["offset"] + p["size"]] for p in mp["parts"]]
+    for sl in (0, 64, 4096 * 3, 1 << 20):
+        got = s3.digests_to_text(s3.sha256_batch_host(views, slice_bytes=sl))
+        assert got == [p["digest"] for p in mp["parts"]], sl
+
+
+def test_c3_parts_ragged(torch_cuda, oracle, golden):
+    """Two whole BASELINE config-3 parts (50.5 MiB and 8.7 MiB, not multiples of 64) plus a
+    ragged batch of 64 C3-distributed lengths scaled down 64x, packed at 256-B offsets."""
+    lens = [e["L"] for e in golden["c3_parts"]]
+    offs = [0, (lens[0] + 255) // 256 * 256]
+    data = torch_cuda.empty(offs[1] + lens[1] + 256, dtype=torch_cuda.uint8, device="cuda")
+    s3.generate_parts(data, offs, lens, [e["p"] for e in golden["c3_parts"]], SEED)
+    got = s3.digests_to_text(s3.sha256_batch_device(data, offs, lens).cpu().numpy())
+    assert got == [e["digest"] for e in golden["c3_parts"]]
+    small = [L // 64 + 3 for L in golden["c3_lengths"]]
+    so = np.concatenate([[0], np.cumsum([(L + 255) // 256 * 256 for L in small])[:-1]])
+    d2 = torch_cuda.empty(int(so[-1]) + small[-1] + 256, dtype=torch_cuda.uint8, device="cuda")
+    s3.generate_parts(d2, so, small, range(64), SEED)
+    for k in KERNELS:
+        g2 = s3.sha256_batch_device(d2, so, small, kernel=k).cpu().numpy().view(np.uint32)
+        assert np.array_equal(g2, oracle.batch(d2.cpu().numpy(), so, small)), k
+
+
+def test_plan_rejects_undersized_buffers(torch_cuda):
+    data = torch_cuda.empty(100, dtype=torch_cuda.uint8, device="cuda")
+    dig = torch_cuda.empty((1, 8), dtype=torch_cuda.int32, device="cuda")
+    plan = s3.Plan([50], [60])
+    with pytest.raises(ValueError):
+        plan.launch(data, dig)

@@ -1,0 +1,71 @@
+"""The oracle (oracle/sha256_oracle.c) pinned against the reference's golden vectors.
+
+tests/golden/sha256_golden.json was produced by tests/golden/gen_golden.py from the REAL
+lib/hash compiled from /root/reference (and cross-checked there with hashlib)."""
+import hashlib
+import hmac as pyhmac
+
+import numpy as np
+import pytest
+
+
+def test_reference_kats(oracle, golden):
+    # lib/hash/sha256.cpp:248-249, 284-285, 331-332 (+ empty, "abc")
+    for k in golden["kat"]:
+        assert oracle.hex(k["ascii"].encode()) == k["digest"], k["name"]
+
+
+def test_kat_literals_from_reference_source(oracle):
+    assert oracle.hex(b"12345678" * 6) == \
+        "dd7f20ca4910f937c3e560427de36fea7c37eed94899b3a9bf286905860d17ae"
+    assert oracle.hex(b"12345678" * 14 + b"1234567") == \
+        "0c65765f1b9fff74bb831fa24c63d9ab0513c881fc7b4919b43f72f5487a24fd"
+    assert oracle.hex(b"12345678" * 15) == \
+        "979e3016a670a5b1308dba2d715f75201eebcef0adc4a1ac99877fad91ce3ff6"
+
+
+def test_length_edges(oracle, golden):
+    big = oracle.generate(7, max(e["L"] for e in golden["edge"]))
+    for e in golden["edge"]:
+        assert oracle.hex(big[:e["L"]]) == e["digest"], e["L"]
+
+
+def test_generator_matches_c2_fixtures(oracle, golden):
+    for e in golden["c2_parts"][:3]:
+        assert oracle.hex(oracle.generate(e["p"], e["L"])) == e["digest"], e["p"]
+
+
+def test_c3_lengths(oracle, golden):
+    assert [oracle.c3_length(p) for p in range(64)] == golden["c3_lengths"]
+    assert golden["c3_lengths"][:4] == [52996377, 9123323, 20283550, 58275873]
+
+
+def test_transfer_parts(oracle, golden):
+    t = golden["transfer"]
+    data = (np.arange(t["size"], dtype=np.uint64) % 128).astype(np.uint8).tobytes()
+    for p in t["parts"]:
+        assert oracle.hex(data[p["offset"]:p["offset"] + p["size"]]) == p["digest"]
+
+
+def test_hmac(oracle, golden):
+    for h in golden["hmac"]:
+        assert oracle.hmac(bytes.fromhex(h["msg"]), bytes.fromhex(h["key"])).hex() == h["mac"]
+
+
+def test_stream_state(oracle, golden):
+    big = oracle.generate(7, 1000)
+    iv = [0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+          0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19]
+    for s in golden["stream"]:
+        assert list(oracle.stream(iv, big[:s["L"]])) == s["state"], s["L"]
+
+
+def test_batch_threads(oracle):
+    rng = np.random.default_rng(1)
+    lens = rng.integers(0, 5000, 40)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    base = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
+    got = oracle.batch(base, offs, lens, threads=4)
+    for i in range(40):
+        want = hashlib.sha256(base[offs[i]:offs[i] + lens[i]].tobytes()).digest()
+        assert got[i].tobytes() == want
