@@ -77,6 +77,19 @@ def workload(cfg: str, rank: int, world: int, ppg: int):
     return ids, lens, offs, name
 
 
+def pmc_traffic(cfg: str, kernel: str, algo_bytes: float):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary of this config+kernel
+    (profiles/rNN_<cfg>_<kernel>_pmc.json, FETCH_SIZE x2 + WRITE_SIZE), scaled per launch."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{cfg}_{kernel}_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        s = json.load(f)
+    ratio = s["traffic_bytes_per_launch"] / s["algorithmic_bytes_per_launch"]
+    return int(round(ratio * algo_bytes)), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(host: np.ndarray, offs, lens, gpu_digests: np.ndarray, nsample: int):
     """lib/hash timed on this host's cores over a bounded sample of the same parts."""
     from tests.oracle_lib import REF_SO, ORACLE_SO, u64p
@@ -185,8 +198,10 @@ def main():
     algo_bytes = part_bytes + 32 * len(lens)           # read once + digests written
     achieved = algo_bytes / (kern_ms / 1e3) / 1e9      # GB/s, this rank's kernel
     compressions = info["total_blocks"]
-    # per-chain ceiling: the longest part's blocks, one VALU per 4 cycles at 2.4 GHz
-    chain_ceiling = None
+    traffic, traffic_src = pmc_traffic(args.config, info["kernel"], algo_bytes)
+    # one part = one sequential chain on one lane: report what one chain sustains and how
+    # many of the chip's 256 CU x 4 SIMD x 64 = 65,536 lanes the batch can occupy
+    chain_gbps = float(lens.max()) / (kern_ms / 1e3) / 1e9
 
     if rank == 0:
         line = {
@@ -202,11 +217,14 @@ def main():
             "parity": {"fixtures_checked": checked, "mismatches": int(bad)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": None, "kernel_ms": round(kern_ms, 3),
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel_ms": round(kern_ms, 3),
                          "kernel_ms_max_rank": round(kern_ms_max, 3),
                          "bytes_per_launch": int(algo_bytes),
                          "compressions_per_launch": int(compressions),
-                         "compressions_per_s": round(compressions / (kern_ms / 1e3), 1)},
+                         "compressions_per_s": round(compressions / (kern_ms / 1e3), 1),
+                         "per_chain_GBps": round(chain_gbps, 4),
+                         "lanes_occupied_frac": round(min(len(lens), 65536) / 65536, 5)},
         }
         if world == 1 and not args.no_cpu_baseline:
             n = min(args.cpu_sample_parts, len(lens))
