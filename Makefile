@@ -13,7 +13,7 @@ CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Iinclude
 
 LIB := $(LIBDIR)/libs3hash.so
 
-all: $(LIB) oracle
+all: $(LIB) oracle cpptests
 
 $(LIBDIR)/capi.o: $(CSRC)/capi.hip $(CSRC)/sha256_kernels.hip $(CSRC)/sha256_device.hpp include/s3hash.h
 	@mkdir -p $(LIBDIR)
@@ -30,7 +30,12 @@ oracle:
 	$(MAKE) -C oracle
 
 CPPTESTS := tests/cpp/build/dropin_test tests/cpp/build/sign_test
-cpptests: $(CPPTESTS)
+cpptests: $(CPPTESTS) apps/build/s3-upload-hash
+
+apps/build/s3-upload-hash: apps/s3_upload_hash.cpp s3client_amd/host/aws_sign.cpp s3client_amd/host/aws_sign.h include/s3hash_batch.hpp $(LIB)
+	@mkdir -p apps/build
+	$(CXX) -O2 -std=c++17 -pthread -Iinclude -Is3client_amd/host -o $@ $< s3client_amd/host/aws_sign.cpp \
+	    -L$(LIBDIR) -ls3hash -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
 tests/cpp/build/dropin_test: tests/cpp/dropin_test.cpp $(LIB)
 	@mkdir -p tests/cpp/build
@@ -46,7 +51,7 @@ isa: $(CSRC)/capi.hip
 	cd build/isa && $(HIPCC) $(HIPFLAGS) -c -save-temps -o capi.o ../../$(CSRC)/capi.hip
 
 clean:
-	rm -rf $(LIBDIR) tests/cpp/build build
+	rm -rf $(LIBDIR) tests/cpp/build apps/build build
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle cpptests isa clean

@@ -1,0 +1,178 @@
+// apps/s3_upload_hash.cpp -- parallel-upload counterpart with payload signing (config 5).
+//
+// The reference's s3-upload (apps/parallel_upload.cpp:55-167 -> sss::Upload ->
+// lib/src/upload.cpp:113-149 UploadFile) slices a file into cfg.jobs x cfg.partsPerJob parts
+// (upload.cpp:98-107, 133) and PUTs each with x-amz-content-sha256: UNSIGNED-PAYLOAD
+// (upload.cpp:60 passes no payloadHash).  This tool computes the same part geometry, hashes
+// every part in ONE batched GPU call (libs3hash.so, host-resident path: H2D included), and
+// emits the signed UploadPart headers each part would carry, with the real digest in
+// x-amz-content-sha256.  No network I/O (libcurl headers, Lyra and MinIO are not available
+// in this environment): `--print-headers` shows what would be sent.
+//
+//   s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--cpu] [--verify] [--print-headers]
+//                  [--endpoint URL --bucket B --key K --access A --secret S --upload-id ID]
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "aws_sign.h"
+#include "s3hash_batch.hpp"
+#include "sha256.h"
+
+namespace {
+
+struct Part {
+  int job, number;
+  uint64_t offset, size;
+};
+
+// lib/src/upload.cpp:98-107 + :133, 136-140 (jobs x partsPerJob)
+std::vector<Part> geometry(uint64_t size, int jobs, int parts_per_job) {
+  std::vector<Part> out;
+  const uint64_t per_job = (size + jobs - 1) / jobs;
+  for (int j = 0; j < jobs; ++j) {
+    uint64_t off = uint64_t(j) * per_job;
+    if (off >= size) break;
+    const uint64_t chunk = std::min(per_job, size - off);
+    const uint64_t psz = (chunk + parts_per_job - 1) / parts_per_job;
+    for (int k = 0; k < parts_per_job; ++k) {
+      if (uint64_t(k) * psz >= chunk) break;
+      const uint64_t s = std::min(psz, chunk - uint64_t(k) * psz);
+      out.push_back({j, j * parts_per_job + k, off, s});
+      off += s;
+    }
+  }
+  return out;
+}
+
+double now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void usage() {
+  std::fprintf(stderr,
+               "usage: s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--cpu] [--verify]\n"
+               "       [--print-headers] [--endpoint URL --bucket B --key K --access A\n"
+               "        --secret S --upload-id ID] [--devices N]\n");
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::string file, endpoint = "http://127.0.0.1:9000", bucket = "bucket1", key = "key1";
+  std::string access = "ACCESS", secret = "SECRET", upload_id = "UPLOAD-ID";
+  int jobs = 1, ppj = 1, devices = 0;
+  bool cpu = false, verify = false, print_headers = false;
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    auto next = [&]() -> std::string {
+      if (i + 1 >= argc) { usage(); std::exit(2); }
+      return argv[++i];
+    };
+    if (a == "-f") file = next();
+    else if (a == "-j") jobs = std::atoi(next().c_str());
+    else if (a == "-n") ppj = std::atoi(next().c_str());
+    else if (a == "--cpu") cpu = true;
+    else if (a == "--verify") verify = true;
+    else if (a == "--print-headers") print_headers = true;
+    else if (a == "--endpoint") endpoint = next();
+    else if (a == "--bucket") bucket = next();
+    else if (a == "--key") key = next();
+    else if (a == "--access") access = next();
+    else if (a == "--secret") secret = next();
+    else if (a == "--upload-id") upload_id = next();
+    else if (a == "--devices") devices = std::atoi(next().c_str());
+    else { usage(); return 2; }
+  }
+  if (file.empty() || jobs < 1 || ppj < 1) { usage(); return 2; }
+
+  const int fd = open(file.c_str(), O_RDONLY);
+  if (fd < 0) { std::perror(file.c_str()); return 1; }
+  struct stat st {};
+  fstat(fd, &st);
+  const uint64_t size = uint64_t(st.st_size);
+  if (size == 0) { std::fprintf(stderr, "empty file\n"); return 1; }
+  auto* data = static_cast<const uint8_t*>(mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0));
+  if (data == MAP_FAILED) { std::perror("mmap"); return 1; }
+
+  const std::vector<Part> parts = geometry(size, jobs, ppj);
+  std::vector<const uint8_t*> ptrs;
+  std::vector<uint64_t> lens;
+  for (const auto& p : parts) {
+    ptrs.push_back(data + p.offset);
+    lens.push_back(p.size);
+  }
+
+  std::vector<std::string> hex(parts.size());
+  double t0 = now();
+  if (cpu) {  // lib/hash drop-in on the host cores, one std::thread per job as upload.cpp does
+    std::vector<std::thread> pool;
+    for (int j = 0; j < jobs; ++j)
+      pool.emplace_back([&, j] {
+        for (size_t i = 0; i < parts.size(); ++i)
+          if (parts[i].job == j) {
+            uint32_t h[8];
+            sha256::sha256(ptrs[i], lens[i], h);
+            char t[65];
+            sha256::hash_to_text(h, t);
+            hex[i] = t;
+          }
+      });
+    for (auto& t : pool) t.join();
+  } else {
+    try {
+      hex = sha256::payload_hashes(ptrs, lens, devices);
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "%s\n", e.what());
+      return 1;
+    }
+  }
+  const double dt = now() - t0;
+
+  int mismatches = 0;
+  if (verify)
+    for (size_t i = 0; i < parts.size(); ++i) {
+      uint32_t h[8];
+      sha256::sha256(ptrs[i], lens[i], h);
+      char t[65];
+      sha256::hash_to_text(h, t);
+      mismatches += hex[i] != t;
+    }
+
+  std::printf("part,job,offset,size,sha256\n");
+  for (size_t i = 0; i < parts.size(); ++i)
+    std::printf("%d,%d,%llu,%llu,%s\n", parts[i].number, parts[i].job,
+                (unsigned long long)parts[i].offset, (unsigned long long)parts[i].size,
+                hex[i].c_str());
+  if (print_headers)
+    for (size_t i = 0; i < parts.size(); ++i) {
+      s3h::sigv4::SignConfig c;
+      c.access = access;
+      c.secret = secret;
+      c.endpoint = endpoint;
+      c.method = "PUT";
+      c.bucket = bucket;
+      c.key = key;
+      c.payloadHash = hex[i];  // instead of UNSIGNED-PAYLOAD (aws_sign.cpp:236-237)
+      c.parameters = {{"partNumber", std::to_string(parts[i].number)}, {"uploadId", upload_id}};
+      c.headers = {{"content-length", std::to_string(parts[i].size)}};
+      for (const auto& kv : s3h::sigv4::SignHeaders(c))
+        std::printf("# part %d %s: %s\n", parts[i].number, kv.first.c_str(), kv.second.c_str());
+    }
+  std::fprintf(stderr, "%s: %zu parts, %.3f GiB in %.3f s = %.3f GiB/s%s\n",
+               cpu ? "cpu lib/hash drop-in" : "gpu batch (H2D included)", parts.size(),
+               double(size) / (1 << 30), dt, double(size) / (1 << 30) / dt,
+               verify ? (mismatches ? ", VERIFY FAILED" : ", verified vs CPU") : "");
+  munmap(const_cast<uint8_t*>(data), size);
+  close(fd);
+  return mismatches ? 1 : 0;
+}

@@ -29,10 +29,6 @@ sys.path.insert(0, ROOT)
 SEED = 20241008
 MIB = 1 << 20
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# VALU issue roof for this path: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 ops/s divided by
-# the VALU instructions one 64-B block costs in the fused kernel's ISA (schedule + rounds).
-VALU_OPS_PER_S = 256 * 4 * 32 * 2.4e9
-CHAIN_ISSUE_CYCLES = 4          # one wave alone issues one VALU per 4 cycles (microarch guide)
 
 
 def parse():
@@ -60,21 +56,20 @@ def c3_length(p: int) -> int:
 
 
 def workload(cfg: str, rank: int, world: int, ppg: int):
-    """Global part ids, lengths and packed offsets of this rank's shard."""
+    """Global part ids, lengths and packed offsets of this rank's shard (s3client_amd.shard)."""
+    from s3client_amd.shard import pack_offsets, shard_ids
     if cfg == "c3":
         n_total = ppg * world if ppg else 4096
-        ids = np.arange(rank, n_total, world, dtype=np.uint64)
+        ids = shard_ids(n_total, rank, world)
         lens = np.array([c3_length(int(p)) for p in ids], dtype=np.uint64)
         name = f"C3: {n_total} parts x U[5,64] MiB (ragged)"
     else:
         per = ppg or (8192 if cfg == "c4" else 1024)
-        ids = np.arange(per, dtype=np.uint64) * world + rank
+        ids = shard_ids(per * world, rank, world)
         lens = np.full(per, 8 * MIB, dtype=np.uint64)
         name = (f"C2: 1024 parts x 8 MiB per GPU" if cfg == "c2" and not ppg
                 else f"{per} parts x 8 MiB per GPU")
-    padded = (lens + 255) // 256 * 256
-    offs = np.concatenate([[0], np.cumsum(padded)[:-1]]).astype(np.uint64)
-    return ids, lens, offs, name
+    return ids, lens, pack_offsets(lens), name
 
 
 def pmc_traffic(cfg: str, kernel: str, algo_bytes: float):
@@ -158,20 +153,6 @@ def main():
         plan.launch(data, digests, stream)
     torch.cuda.synchronize(dev)
 
-    # parity spot-check of this run's digests against the reference fixtures
-    gd = digests.cpu().numpy().view(np.uint32)
-    with open(os.path.join(ROOT, "tests", "golden", "sha256_golden.json")) as f:
-        gold = json.load(f)
-    fixtures = {e["p"]: e["digest"] for e in gold["c2_parts"]}
-    if args.config == "c3":
-        fixtures = {e["p"]: e["digest"] for e in gold["c3_parts"]}
-    checked = bad = 0
-    for slot, p in enumerate(ids):
-        want = fixtures.get(int(p))
-        if want is not None:
-            checked += 1
-            bad += s3.hash_to_text(gd[slot]) != want
-
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
     if world > 1:
@@ -191,6 +172,20 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall, kern_ms_max = float(t[0]), float(t[1])
+
+    # parity spot-check of the last timed step's digests against the reference fixtures
+    gd = digests.cpu().numpy().view(np.uint32)
+    with open(os.path.join(ROOT, "tests", "golden", "sha256_golden.json")) as f:
+        gold = json.load(f)
+    fixtures = {e["p"]: e["digest"] for e in gold["c2_parts"]}
+    if args.config == "c3":
+        fixtures = {e["p"]: e["digest"] for e in gold["c3_parts"]}
+    checked = bad = 0
+    for slot, p in enumerate(ids):
+        want = fixtures.get(int(p))
+        if want is not None:
+            checked += 1
+            bad += s3.hash_to_text(gd[slot]) != want
 
     part_bytes = float(lens.sum())
     total_bytes = part_bytes * world * args.steps

@@ -1,0 +1,62 @@
+// include/s3hash_batch.hpp -- C++ convenience layer over the C-ABI (include/s3hash.h) in the
+// same `namespace sha256` as the lib/hash drop-in, for C++ callers such as the parallel
+// upload (the reference's lib/src/upload.cpp:89-110 insertion point).  Header-only; every
+// call goes to the GPU through libs3hash.so and throws on error (no CPU fallback).
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "s3hash.h"
+#include "sha256.h"
+
+namespace sha256 {
+
+struct batch_error : std::runtime_error {
+  int code;
+  batch_error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+inline void batch_check(int rc) {
+  if (rc != S3H_OK) throw batch_error(rc, std::string("s3hash: ") + s3h_last_error());
+}
+
+// Digests of host-resident parts on the GPUs (0 = all visible devices), one uint32_t[8] per
+// part in lib/hash's layout (hash[i] = bswap32(H_i)).
+inline std::vector<uint32_t> sha256_batch(const std::vector<const uint8_t*>& parts,
+                                          const std::vector<uint64_t>& lengths,
+                                          int ndevices = 0, uint64_t slice_bytes = 0) {
+  if (parts.size() != lengths.size()) throw std::invalid_argument("parts/lengths size mismatch");
+  std::vector<uint32_t> out(8 * parts.size());
+  if (!parts.empty())
+    batch_check(s3h_sha256_batch_host(parts.data(), lengths.data(), parts.size(), out.data(),
+                                      ndevices, slice_bytes));
+  return out;
+}
+
+// Parts already in device memory at d_base + offsets[i]; digests written to d_digests.
+inline void sha256_batch_device(int device, const void* d_base,
+                                const std::vector<uint64_t>& offsets,
+                                const std::vector<uint64_t>& lengths, uint32_t* d_digests,
+                                void* stream = nullptr) {
+  batch_check(s3h_sha256_batch_device(device, d_base, offsets.data(), lengths.data(),
+                                      offsets.size(), d_digests, stream));
+}
+
+// 64-char lowercase hex per part: the `payloadHash` strings S3Api::UploadFilePart takes
+// (lib/include/s3-api.h:447-452).
+inline std::vector<std::string> payload_hashes(const std::vector<const uint8_t*>& parts,
+                                               const std::vector<uint64_t>& lengths,
+                                               int ndevices = 0) {
+  const std::vector<uint32_t> d = sha256_batch(parts, lengths, ndevices);
+  std::vector<std::string> out(parts.size());
+  for (size_t i = 0; i < parts.size(); ++i) {
+    char t[65];
+    hash_to_text(const_cast<uint32_t*>(&d[8 * i]), t);
+    out[i] = t;
+  }
+  return out;
+}
+
+}  // namespace sha256

@@ -1,0 +1,113 @@
+// tests/cpp/dropin_test.cpp -- the lib/hash drop-in linked exactly as the reference's callers
+// link lib/hash: only include/sha256.h + utility.h and libs3hash.so.  Mirrors the reference's
+// in-file known-answer tests (lib/hash/sha256.cpp:236-399, which do not compile upstream) and
+// exercises every exported symbol.  `--gpu` also runs the batched C++ API on the GPU.
+// Output: CSV "Hash,<action>,0|1," like the reference tests (test/utility.cpp:87-95).
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "s3hash_batch.hpp"
+#include "sha256.h"
+
+static int fails = 0;
+static void report(const char* action, bool ok) {
+  std::printf("Hash,%s,%d,\n", action, int(ok));
+  fails += !ok;
+}
+
+static std::string text(uint32_t h[8]) {
+  char t[65];
+  sha256::hash_to_text(h, t);
+  return t;
+}
+
+static std::string digest(const std::string& s) {
+  uint32_t h[8];
+  sha256::sha256(reinterpret_cast<const uint8_t*>(s.data()), s.size(), h);
+  return text(h);
+}
+
+int main(int argc, char** argv) {
+  std::string s6, s14, s15;
+  for (int i = 0; i < 15; ++i) {
+    if (i < 6) s6 += "12345678";
+    if (i < 14) s14 += "12345678";
+    s15 += "12345678";
+  }
+  s14 += "1234567";
+  // KATs of lib/hash/sha256.cpp:248-249, 284-285, 331-332
+  report("sha256 48 bytes", digest(s6) == "dd7f20ca4910f937c3e560427de36fea7c37eed94899b3a9bf286905860d17ae");
+  report("sha256 119 bytes", digest(s14) == "0c65765f1b9fff74bb831fa24c63d9ab0513c881fc7b4919b43f72f5487a24fd");
+  report("sha256 120 bytes", digest(s15) == "979e3016a670a5b1308dba2d715f75201eebcef0adc4a1ac99877fad91ce3ff6");
+  report("sha256 empty", digest("") == "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855");
+
+  // sha256_stream over an alloc_padded buffer == sha256 (sha256.cpp:147-160 composition)
+  {
+    size_t sz = 0;
+    uint8_t* buf = alloc_padded(s15.size(), s15.size(), &sz, nullptr);
+    std::memcpy(buf, s15.data(), s15.size());
+    uint32_t h[8];
+    sha256::init_hash(h);
+    sha256::sha256_stream(h, buf, sz);
+    sha256::to_little(h);
+    std::free(buf);
+    report("alloc_padded+stream", sz == 192 && text(h) == digest(s15));
+  }
+  // chunked: whole blocks with total_length 0, then the final chunk with the total length
+  {
+    std::string big(1000, 'x');
+    for (size_t i = 0; i < big.size(); ++i) big[i] = char(i * 7 + 3);
+    uint32_t h[8];
+    sha256::init_hash(h);
+    sha256::sha256_next(reinterpret_cast<const uint8_t*>(big.data()), 640, h, 0, nullptr);
+    std::vector<uint8_t> tmp(512);
+    sha256::sha256_next(reinterpret_cast<const uint8_t*>(big.data()) + 640, 360, h, 1000, tmp.data());
+    sha256::to_little(h);
+    report("sha256_next chunked", text(h) == digest(big));
+  }
+  // sha256_file == sha256 of the same bytes (incl. exactly 16 MiB, the reference buffer size)
+  for (size_t n : {size_t(0), size_t(1), size_t(100000), size_t(16) << 20}) {
+    std::string path = "/tmp/s3h_dropin_" + std::to_string(n);
+    std::vector<uint8_t> v(n);
+    for (size_t i = 0; i < n; ++i) v[i] = uint8_t(i * 31 + 7);
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (n) std::fwrite(v.data(), 1, n, f);
+    std::fclose(f);
+    uint32_t a[8], b[8];
+    sha256::sha256_file(path.c_str(), a);
+    sha256::sha256(v.data(), n, b);
+    std::remove(path.c_str());
+    report(("sha256_file " + std::to_string(n)).c_str(), std::memcmp(a, b, 32) == 0);
+  }
+  // hmac256 RFC 4231 test case 2 ("Jefe")
+  {
+    const std::string key = "Jefe", msg = "what do ya want for nothing?";
+    uint8_t mac[32];
+    hmac256(reinterpret_cast<const uint8_t*>(msg.data()), msg.size(),
+            reinterpret_cast<const uint8_t*>(key.data()), key.size(), mac);
+    char t[65];
+    for (int i = 0; i < 32; ++i) std::snprintf(t + 2 * i, 3, "%02x", mac[i]);
+    report("hmac256 rfc4231", std::string(t) == "5bdcc146bf60754e6a042426089575c75a003f089d2739839dec58b964ec3843");
+  }
+  // utility.h helpers
+  report("utility", to_big_endian(0x0102030405060708ull) == 0x0807060504030201ull &&
+                        to_little_endian(0x11223344u) == 0x44332211u &&
+                        next_div_by(129, 64) == 192 && next_div_by(128, 64) == 128 &&
+                        right_rotate(1u, 1) == 0x80000000u && lshift(0xff, 8) == 0xff00u);
+  if (argc > 1 && std::string(argv[1]) == "--gpu") {
+    std::vector<std::string> msgs = {s6, s14, s15, "", std::string(5 << 20, 'q')};
+    std::vector<const uint8_t*> ptrs;
+    std::vector<uint64_t> lens;
+    for (auto& m : msgs) {
+      ptrs.push_back(reinterpret_cast<const uint8_t*>(m.data()));
+      lens.push_back(m.size());
+    }
+    const auto hex = sha256::payload_hashes(ptrs, lens);
+    bool ok = true;
+    for (size_t i = 0; i < msgs.size(); ++i) ok &= hex[i] == digest(msgs[i]);
+    report("gpu batch payload_hashes", ok);
+  }
+  return fails ? 1 : 0;
+}

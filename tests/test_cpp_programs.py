@@ -1,0 +1,78 @@
+"""C++ programs linked against libs3hash.so the way the reference's callers link lib/hash:
+the signer KATs of config 1 (test/sign-test.cpp, test/presign-url-test.cpp) through the
+drop-in, and the lib/hash drop-in known-answer tests.  `--gpu` adds the batched C++ API."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BUILD = os.path.join(ROOT, "tests", "cpp", "build")
+
+
+@pytest.fixture(scope="module")
+def programs():
+    subprocess.run(["make", "-C", ROOT, "cpptests"], check=True, capture_output=True)
+    return BUILD
+
+
+def _run(path, *args):
+    r = subprocess.run([path, *args], capture_output=True, text=True, timeout=300)
+    rows = [l.split(",") for l in r.stdout.strip().splitlines()]
+    return r.returncode, rows
+
+
+def test_sign_kats(programs):
+    rc, rows = _run(os.path.join(programs, "sign_test"))
+    assert rc == 0 and rows and all(r[2] == "1" for r in rows), rows
+    assert {r[1] for r in rows} >= {"Sign request", "Presign URL", "Sign payload request"}
+
+
+def test_dropin_kats(programs):
+    rc, rows = _run(os.path.join(programs, "dropin_test"))
+    assert rc == 0 and len(rows) >= 12 and all(r[2] == "1" for r in rows), rows
+
+
+@pytest.mark.gpu
+def test_dropin_gpu_batch(programs):
+    rc, rows = _run(os.path.join(programs, "dropin_test"), "--gpu")
+    assert rc == 0 and rows[-1][1] == "gpu batch payload_hashes" and rows[-1][2] == "1", rows
+
+
+def _xfer_file(tmp_path, golden):
+    import numpy as np
+    t = golden["transfer"]
+    p = tmp_path / "xfer.bin"
+    (np.arange(t["size"], dtype=np.uint64) % 128).astype(np.uint8).tofile(p)
+    return str(p), t
+
+
+def _parse_parts(stdout):
+    lines = [l for l in stdout.splitlines() if l and not l.startswith("#")]
+    assert lines[0] == "part,job,offset,size,sha256"
+    return [l.split(",") for l in lines[1:]]
+
+
+def test_upload_counterpart_cpu(programs, tmp_path, golden):
+    """apps/s3_upload_hash.cpp with the CPU drop-in: the transfer test's 3 jobs x 2 parts."""
+    path, t = _xfer_file(tmp_path, golden)
+    app = os.path.join(ROOT, "apps", "build", "s3-upload-hash")
+    r = subprocess.run([app, "-f", path, "-j", "3", "-n", "2", "--cpu", "--print-headers"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    rows = _parse_parts(r.stdout)
+    assert [(int(x[2]), int(x[3]), x[4]) for x in rows] == \
+        [(p["offset"], p["size"], p["digest"]) for p in t["parts"]]
+    heads = [l for l in r.stdout.splitlines() if "x-amz-content-sha256" in l]
+    assert len(heads) == 6 and "UNSIGNED-PAYLOAD" not in r.stdout
+
+
+@pytest.mark.gpu
+def test_upload_counterpart_gpu(programs, tmp_path, golden):
+    path, t = _xfer_file(tmp_path, golden)
+    app = os.path.join(ROOT, "apps", "build", "s3-upload-hash")
+    r = subprocess.run([app, "-f", path, "-j", "3", "-n", "2", "--verify"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    rows = _parse_parts(r.stdout)
+    assert [x[4] for x in rows] == [p["digest"] for p in t["parts"]]

@@ -1,0 +1,78 @@
+"""Multi-rank sharding on CPU with the gloo backend, world_size 2.
+
+Each rank takes parts p % world == rank, digests them locally (CPU drop-in here; the GPU
+path on the box), and the digest table is reassembled only for verification.  Checks: the
+shards partition the batch, the reassembled table equals the oracle's, and bench.py's
+workload() uses the same partition."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from s3client_amd.shard import gather_digests, pack_offsets, shard_ids
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, n_total, lens, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import s3client_amd as s3
+    from tests.oracle_lib import Oracle
+    orc = Oracle()
+    ids = shard_ids(n_total, rank, world)
+    local = np.stack([s3.sha256(orc.generate(int(p), int(lens[int(p)]))) for p in ids])
+    t = __import__("torch").tensor([float(rank + 1)])
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)          # bench.py's max-over-ranks timing
+    full = gather_digests(local, ids, n_total)
+    if rank == 0:
+        q.put((full, float(t)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_round_robin_shards_reassemble_to_oracle(oracle, world):
+    n_total = 37
+    lens = np.random.default_rng(world).integers(0, 3000, n_total)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, lens, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    full, tmax = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert tmax == float(world)
+    want = np.stack([oracle.sha256(oracle.generate(p, int(lens[p]))) for p in range(n_total)])
+    assert np.array_equal(full, want)
+
+
+def test_shards_partition_and_bench_workload_matches():
+    import bench
+    for world in (1, 2, 4, 8):
+        allids = np.concatenate([shard_ids(1000, r, world) for r in range(world)])
+        assert sorted(allids.tolist()) == list(range(1000))
+        for r in range(world):
+            ids, lens, offs, _ = bench.workload("c2", r, world, 0)
+            assert np.array_equal(ids, shard_ids(1024 * world, r, world))
+            assert np.all(offs % 256 == 0) and np.all(lens == 8 << 20)
+    ids, lens, offs, _ = bench.workload("c3", 1, 2, 0)
+    assert ids.size == 2048 and int(ids[0]) == 1
+
+
+def test_pack_offsets_alignment():
+    offs = pack_offsets([0, 1, 255, 256, 257])
+    assert offs.tolist() == [0, 0, 256, 512, 768]

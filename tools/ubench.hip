@@ -1,7 +1,8 @@
 // tools/ubench.hip -- microbenchmarks that pin down the VALU issue model the SHA-256
 // kernels are designed against (DESIGN.md "Issue model").  Standalone HIP program:
 //   hipcc --offload-arch=gfx950 -O3 -o tools/ubench tools/ubench.hip && tools/ubench
-// Every kernel runs a straight line of 2048 instructions (512 x a 4-instruction asm group)
+// Every kernel loops 256 times over a 128-instruction body (32 x a 4-instruction asm group,
+// small enough to stay in the instruction cache)
 // and reports shader cycles per instruction per wave from s_memtime, plus the in-kernel
 // clock from s_memrealtime (100 MHz).  Workgroups of 64 / 256 / 512 / 1024 threads put
 // 1 / 1 / 2 / 4 waves on each SIMD of one CU (dispatch order 0->2->1->3).
@@ -12,7 +13,7 @@
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
   printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
-constexpr int N = 2048;
+constexpr int N = 2048 * 16;  // 256 trips of a 128-instruction body (i-cache resident)
 
 __device__ __forceinline__ uint64_t stamp() {
   uint64_t t;
@@ -31,8 +32,10 @@ __device__ __forceinline__ uint64_t rstamp() {
     float fa = float(a), fb = 1.0001f, fc = 0.5f;                                         \
     const uint64_t r0 = rstamp();                                                         \
     const uint64_t t0 = stamp();                                                          \
-    _Pragma("unroll") for (int i = 0; i < N / 4; ++i) {                                   \
-      asm volatile(ASM : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(fa) : "v"(fb), "v"(fc)); \
+    _Pragma("unroll 1") for (int o = 0; o < N / 128; ++o) {                               \
+      _Pragma("unroll") for (int i = 0; i < 32; ++i) {                                    \
+        asm volatile(ASM : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(fa) : "v"(fb), "v"(fc)); \
+      }                                                                                   \
     }                                                                                     \
     const uint64_t t1 = stamp();                                                          \
     const uint64_t r1 = rstamp();                                                         \
