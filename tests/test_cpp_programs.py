@@ -63,7 +63,7 @@ def test_upload_counterpart_cpu(programs, tmp_path, golden):
     rows = _parse_parts(r.stdout)
     assert [(int(x[2]), int(x[3]), x[4]) for x in rows] == \
         [(p["offset"], p["size"], p["digest"]) for p in t["parts"]]
-    heads = [l for l in r.stdout.splitlines() if "x-amz-content-sha256" in l]
+    heads = [l for l in r.stdout.splitlines() if " x-amz-content-sha256: " in l]
     assert len(heads) == 6 and "UNSIGNED-PAYLOAD" not in r.stdout
 
 
