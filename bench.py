@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4"])
     ap.add_argument("--parts-per-gpu", type=int, default=0, help="override batch size")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "pc", "lane"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "pair", "pc", "lane"])
     ap.add_argument("--cpu-sample-parts", type=int, default=384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="device", choices=["device", "host"],

@@ -88,8 +88,8 @@ int plan_build(int device, const uint64_t* offsets, const uint64_t* lengths, uin
     return fail(S3H_EINVAL, "plan: need offsets, lengths and 0 < n <= 2^31 (n=%llu)",
                 (unsigned long long)n);
   if (int rc = check_device(device)) return rc;
-  if (kernel == S3H_KERNEL_AUTO) kernel = n <= kPcMaxParts ? S3H_KERNEL_PC : S3H_KERNEL_LANE;
-  if (kernel != S3H_KERNEL_PC && kernel != S3H_KERNEL_LANE)
+  if (kernel == S3H_KERNEL_AUTO) kernel = n <= kPcMaxParts ? S3H_KERNEL_PAIR : S3H_KERNEL_LANE;
+  if (kernel != S3H_KERNEL_PC && kernel != S3H_KERNEL_LANE && kernel != S3H_KERNEL_PAIR)
     return fail(S3H_EINVAL, "plan: unknown kernel %d", kernel);
 
   std::vector<uint32_t> order(n);
@@ -110,7 +110,9 @@ int plan_build(int device, const uint64_t* offsets, const uint64_t* lengths, uin
   P->n = n;
   P->total_blocks = total;
   P->max_blocks = s3h::nblocks(slots[0].len);
-  P->grid = kernel == S3H_KERNEL_PC ? uint32_t((n + 63) / 64) : uint32_t((n + 255) / 256);
+  P->grid = kernel == S3H_KERNEL_PC     ? uint32_t((n + 63) / 64)
+            : kernel == S3H_KERNEL_PAIR ? uint32_t((n + s3h::kPairParts - 1) / s3h::kPairParts)
+                                        : uint32_t((n + 255) / 256);
 
   DeviceGuard g(device);
   hipError_t e = hipMalloc(&P->d_slots, n * sizeof(s3h::Slot));
@@ -145,6 +147,8 @@ int plan_launch(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint64_t
   A.n = uint32_t(P->n);
   if (P->kernel == S3H_KERNEL_PC)
     hipLaunchKernelGGL(s3h::sha256_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_PAIR)
+    hipLaunchKernelGGL(s3h::sha256_pair_kernel, dim3(P->grid), dim3(s3h::kPairThreads), 0, stream, A);
   else
     hipLaunchKernelGGL(s3h::sha256_lane_kernel, dim3(P->grid), dim3(256), 0, stream, A);
   HIP_TRY(hipGetLastError());

@@ -101,8 +101,9 @@ __global__ __launch_bounds__(256) void sha256_lane_kernel(LaunchArgs A) {
 
 // ------------------------------------------------------------- producer/consumer kernel
 // Decode + pad + schedule one block and store W[t]+K[t] as 16 x 16 B rows of LDS.
+template <int kRow>
 __device__ __forceinline__ void produce_block(const RawBlock& r, uint32_t sel, const uint8_t* bp,
-                                              uint64_t len, uint64_t blk, uint4 (*buf)[64],
+                                              uint64_t len, uint64_t blk, uint4 (*buf)[kRow],
                                               uint32_t lane) {
   uint32_t w[16], wk[64];
   make_block(r, sel, bp, len, blk, w);
@@ -186,6 +187,155 @@ __global__ __launch_bounds__(kPcThreads) void sha256_pc_kernel(LaunchArgs A) {
       __syncthreads();
     }
     if (valid && nb > A.blk_begin) store_result(A, slot, nb, st);
+  }
+}
+
+// ------------------------------------------------------------- lane-pair kernel
+// Each part's 64-round chain is split over a PAIR of lanes: the "e-half" (lanes in DPP banks
+// 0 and 2 of every 16-lane row) holds e,f,g,h and computes T1 = h + W+K + Sigma1(e) + Ch;
+// the "a-half" (banks 1 and 3, partner = lane + 4) holds a,b,c,d and computes
+// T2 = Sigma0(a) + Maj(a,b,c) with the SAME instruction stream (per-lane rotate amounts,
+// Ch and Maj unified as one bfi over a per-lane selector).  Two bank-masked DPP adds finish
+// the round: e' = d(partner) + T1 on the e-half, a' = T1(partner) + T2 on the a-half.
+// A round is 10 VALU instead of 14, and since a lone wave issues ~1 VALU per 5 cycles
+// whatever the op (profiles/r01_ubench_valu_issue.txt), each chain runs ~1.35x faster.
+// Workgroup = 128 threads: wave 0 consumes 32 parts (64 lanes), wave 1 produces W+K for
+// those 32 parts, two blocks per step (lanes 0-31 even blocks, 32-63 odd blocks).
+constexpr int kPairThreads = 128;
+constexpr int kPairParts = 32;
+
+__device__ __forceinline__ uint32_t pair_chain(uint32_t lane) {
+  return (lane >> 4) * 8u + ((lane >> 3) & 1u) * 4u + (lane & 3u);
+}
+__device__ __forceinline__ bool pair_is_ahalf(uint32_t lane) { return (lane >> 2) & 1u; }
+
+// One round on the pair, as asm text over named operands: the new value lands in d (in
+// place), x is this round's h+W+K on the e-half (0 on the a-half) and xn receives the next
+// round's (c + wn) on the e-half.  Hazards: the a-half DPP reads q3 two instructions after it
+// is written (the two wait states a DPP read of a fresh VALU result needs); every other DPP
+// source was written >= 2 rounds earlier.
+#define S3H_PAIR_TXT(a, b, c, d, x, xn, wn)                                                   \
+  "v_alignbit_b32 %[q1], %[" #a "], %[" #a "], %[h1]\n\t"                                     \
+  "v_alignbit_b32 %[q2], %[" #a "], %[" #a "], %[h2]\n\t"                                     \
+  "v_alignbit_b32 %[q3], %[" #a "], %[" #a "], %[h3]\n\t"                                     \
+  "v_bitop3_b32 %[q4], %[" #a "], %[" #b "], %[m] bitop3:0xd2\n\t"                            \
+  "v_bitop3_b32 %[q1], %[q1], %[q2], %[q3] bitop3:0x96\n\t"                                   \
+  "v_bfi_b32 %[q2], %[q4], %[" #b "], %[" #c "]\n\t"                                          \
+  "v_add3_u32 %[q3], %[" #x "], %[q1], %[q2]\n\t"                                             \
+  "v_add_u32_dpp %[" #xn "], %[" #c "], %[" #wn "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5\n\t" \
+  "v_add_u32_dpp %[" #d "], %[" #d "], %[q3] row_shl:4 row_mask:0xf bank_mask:0x5\n\t"       \
+  "v_add_u32_dpp %[" #d "], %[q3], %[q3] row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+
+// Four rounds (one full rotation of the state names) in one asm statement, so the compiler
+// pads only once per four rounds.
+#define S3H_PAIR_4RND(W1, W2, W3, W4)                                                          \
+  asm volatile(S3H_PAIR_TXT(s0, s1, s2, s3, xa, xb, w1) S3H_PAIR_TXT(s3, s0, s1, s2, xb, xa, w2) \
+               S3H_PAIR_TXT(s2, s3, s0, s1, xa, xb, w3) S3H_PAIR_TXT(s1, s2, s3, s0, xb, xa, w4) \
+               : [s0] "+v"(s0), [s1] "+v"(s1), [s2] "+v"(s2), [s3] "+v"(s3), [xa] "+v"(xa),    \
+                 [xb] "+v"(xb), [q1] "=&v"(q1), [q2] "=&v"(q2), [q3] "=&v"(q3), [q4] "=&v"(q4)  \
+               : [w1] "v"(W1), [w2] "v"(W2), [w3] "v"(W3), [w4] "v"(W4), [h1] "v"(sh1),         \
+                 [h2] "v"(sh2), [h3] "v"(sh3), [m] "v"(msk))
+
+__global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A) {
+  __shared__ uint4 lds_wk[2][2][16][kPairParts];  // [buffer][block in step][round group][part]
+
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t slot0 = blockIdx.x * kPairParts;
+  const uint64_t b0 = A.blk_begin;
+  const uint64_t wg_nb = nblocks(A.slots[slot0].len);
+  const uint64_t wg_end = wg_nb < A.blk_end ? wg_nb : A.blk_end;
+  if (wg_end <= b0) return;
+  const uint64_t iters = wg_end - b0;          // blocks this launch, uniform in the workgroup
+  const uint64_t steps = (iters + 1) >> 1;     // two blocks per producer step
+
+  if (wave == 1) {
+    // ---------------------------------------------------------------- producer
+    const uint32_t part = lane & 31u, half = lane >> 5;
+    const uint32_t slot = slot0 + part;
+    Slot s = {0, 0};
+    if (slot < A.n) s = A.slots[slot];
+    const uint8_t* p = A.base + s.off + 64ull * (b0 + half - A.blk_origin);
+    const uint32_t sel = be_selector(uint32_t(reinterpret_cast<uintptr_t>(A.base + s.off) & 3));
+    const uint64_t nfull = s.len >> 6;
+    const uint64_t bh = b0 + half;  // this lane's first block
+    RawBlock ra, rb;
+    if (bh < nfull) fetch_full(p, ra);
+    if (bh + 2 < nfull) fetch_full(p + 128, rb);
+    produce_block(ra, sel, p, s.len, bh, lds_wk[0][half], part);
+    __syncthreads();
+    for (uint64_t k = 1; k <= steps; k += 2) {
+      if (k < steps) {
+        if (bh + 2 * (k + 1) < nfull) fetch_full(p + 128 * (k + 1), ra);
+        produce_block(rb, sel, p + 128 * k, s.len, bh + 2 * k, lds_wk[1][half], part);
+      }
+      __syncthreads();
+      if (k + 1 > steps) break;
+      if (k + 1 < steps) {
+        if (bh + 2 * (k + 2) < nfull) fetch_full(p + 128 * (k + 2), rb);
+        produce_block(ra, sel, p + 128 * (k + 1), s.len, bh + 2 * (k + 1), lds_wk[0][half], part);
+      }
+      __syncthreads();
+    }
+  } else {
+    // ---------------------------------------------------------------- consumer
+    const uint32_t part = pair_chain(lane);
+    const bool ahalf = pair_is_ahalf(lane);
+    const uint32_t slot = slot0 + part;
+    const bool valid = slot < A.n;
+    const uint64_t nb = valid ? nblocks(A.slots[slot].len) : 0;
+    const uint32_t sh1 = ahalf ? 2u : 6u, sh2 = ahalf ? 13u : 11u, sh3 = ahalf ? 22u : 25u;
+    const uint32_t msk = ahalf ? 0xffffffffu : 0u;
+    const uint32_t w0 = ahalf ? 0u : 4u;  // which half of the chaining state this lane holds
+    uint32_t s0, s1, s2, s3;
+    if (valid && b0 > 0 && A.state) {
+      const uint4 v = reinterpret_cast<const uint4*>(A.state + 8ull * slot + w0)[0];
+      s0 = v.x; s1 = v.y; s2 = v.z; s3 = v.w;
+    } else {
+      s0 = ahalf ? 0x6a09e667u : 0x510e527fu;
+      s1 = ahalf ? 0xbb67ae85u : 0x9b05688cu;
+      s2 = ahalf ? 0x3c6ef372u : 0x1f83d9abu;
+      s3 = ahalf ? 0xa54ff53au : 0x5be0cd19u;
+    }
+    uint32_t xa = 0, xb = 0;  // a-half lanes are never written: their X stays 0
+    uint32_t q1, q2, q3, q4;
+    __syncthreads();
+    for (uint64_t j = 0; j < steps; ++j) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint64_t i = 2 * j + h;
+        if (i < iters) {
+          uint32_t wk[64];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const uint4 v = lds_wk[j & 1][h][q][part];
+            wk[4 * q] = v.x; wk[4 * q + 1] = v.y; wk[4 * q + 2] = v.z; wk[4 * q + 3] = v.w;
+          }
+          const uint32_t t0 = s0, t1 = s1, t2 = s2, t3 = s3;
+          asm volatile(
+              "s_nop 1\n\t"
+              "v_add_u32_dpp %0, %1, %2 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5"
+              : "+v"(xa) : "v"(s3), "v"(wk[0]));
+#pragma unroll
+          for (int t = 0; t < 64; t += 4)
+            S3H_PAIR_4RND(wk[(t + 1) & 63], wk[(t + 2) & 63], wk[(t + 3) & 63], wk[(t + 4) & 63]);
+          const bool live = (b0 + i) < nb;
+          s0 = live ? s0 + t0 : t0;
+          s1 = live ? s1 + t1 : t1;
+          s2 = live ? s2 + t2 : t2;
+          s3 = live ? s3 + t3 : t3;
+        }
+      }
+      __syncthreads();
+    }
+    if (valid && nb > b0) {
+      if (nb <= A.blk_end) {
+        uint4* o = reinterpret_cast<uint4*>(A.digests + 8ull * A.out_idx[slot] + w0);
+        o[0] = make_uint4(bswap(s0), bswap(s1), bswap(s2), bswap(s3));
+      } else if (A.state) {
+        reinterpret_cast<uint4*>(A.state + 8ull * slot + w0)[0] = make_uint4(s0, s1, s2, s3);
+      }
+    }
   }
 }
 

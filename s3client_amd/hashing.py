@@ -56,7 +56,7 @@ class Plan:
 
     def __init__(self, offsets: Sequence[int], lengths: Sequence[int], device: int = 0,
                  kernel: str | int = "auto"):
-        k = kernel if isinstance(kernel, int) else {"auto": 0, "lane": 1, "pc": 2}[kernel]
+        k = kernel if isinstance(kernel, int) else _native.KERNEL_IDS[kernel]
         self.offsets, self.lengths = _u64(offsets), _u64(lengths)
         if self.offsets.shape != self.lengths.shape or self.offsets.ndim != 1:
             raise ValueError("offsets and lengths must be 1-D and of equal length")

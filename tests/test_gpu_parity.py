@@ -9,7 +9,7 @@ import s3client_amd as s3
 
 pytestmark = pytest.mark.gpu
 SEED = 20241008
-KERNELS = ["pc", "lane"]
+KERNELS = ["pair", "pc", "lane"]
 
 
 def _dev_buffer(torch, host: np.ndarray):
@@ -70,8 +70,9 @@ def test_kernels_agree_on_many_small_parts(torch_cuda, oracle):
     host = rng.integers(0, 256, (1 << 20) + 256, dtype=np.uint8)
     data = _dev_buffer(torch_cuda, host)
     a = s3.sha256_batch_device(data, offs, lens, kernel="auto").cpu().numpy().view(np.uint32)
-    b = s3.sha256_batch_device(data, offs, lens, kernel="pc").cpu().numpy().view(np.uint32)
-    assert np.array_equal(a, b)
+    for k in ("pc", "pair"):
+        b = s3.sha256_batch_device(data, offs, lens, kernel=k).cpu().numpy().view(np.uint32)
+        assert np.array_equal(a, b), k
     idx = rng.choice(n, 500, replace=False)
     want = oracle.batch(host, offs[idx], lens[idx])
     assert np.array_equal(a[idx], want)
@@ -106,7 +107,7 @@ def test_c2_full_batch_bit_exact(torch_cuda, oracle, golden, kernel):
     txt = s3.digests_to_text(out)
     for e in golden["c2_parts"]:
         assert txt[e["p"]] == e["digest"], e["p"]
-    if kernel == "pc":
+    if kernel == "pair":
         host = data.cpu().numpy()
         want = oracle.batch(host, offs, lens, threads=16)
         assert np.array_equal(out, want)
