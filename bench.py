@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4"])
     ap.add_argument("--parts-per-gpu", type=int, default=0, help="override batch size")
+    ap.add_argument("--part-bytes", type=int, default=0, help="override part size (sweeps)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "pair", "pc", "lane"])
     ap.add_argument("--cpu-sample-parts", type=int, default=384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -55,7 +56,7 @@ def c3_length(p: int) -> int:
     return 5 * MIB + z % (59 * MIB + 1)
 
 
-def workload(cfg: str, rank: int, world: int, ppg: int):
+def workload(cfg: str, rank: int, world: int, ppg: int, part_bytes: int = 0):
     """Global part ids, lengths and packed offsets of this rank's shard (s3client_amd.shard)."""
     from s3client_amd.shard import pack_offsets, shard_ids
     if cfg == "c3":
@@ -66,9 +67,10 @@ def workload(cfg: str, rank: int, world: int, ppg: int):
     else:
         per = ppg or (8192 if cfg == "c4" else 1024)
         ids = shard_ids(per * world, rank, world)
-        lens = np.full(per, 8 * MIB, dtype=np.uint64)
-        name = (f"C2: 1024 parts x 8 MiB per GPU" if cfg == "c2" and not ppg
-                else f"{per} parts x 8 MiB per GPU")
+        pb = part_bytes or 8 * MIB
+        lens = np.full(per, pb, dtype=np.uint64)
+        name = (f"C2: 1024 parts x 8 MiB per GPU" if cfg == "c2" and not ppg and not part_bytes
+                else f"{per} parts x {pb} B per GPU")
     return ids, lens, pack_offsets(lens), name
 
 
@@ -137,7 +139,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    ids, lens, offs, name = workload(args.config, rank, world, args.parts_per_gpu)
+    ids, lens, offs, name = workload(args.config, rank, world, args.parts_per_gpu,
+                                    args.part_bytes)
     nbytes = int(offs[-1] + lens[-1]) + 256
     data = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     s3.generate_parts(data, offs, lens, ids, SEED)

@@ -76,8 +76,11 @@ struct s3h_plan_s {
 
 namespace {
 
-// Above this many parts every SIMD already holds >= 1 consumer+producer pair, and the fused
-// kernel's lower instruction total (no LDS traffic) wins; below it per-chain latency rules.
+// Kernel choice by part count (profiles/r01_sweep_parts_256KiB.jsonl): while parts are
+// scarcer than SIMDs x 32, per-chain latency rules and the lane-pair kernel (10 VALU/round per
+// wave) wins; once consumer+producer waves fill every SIMD the total instruction count rules:
+// producer/consumer up to 64K parts, then the fused one-lane-per-part kernel.
+constexpr uint64_t kPairMaxParts = 32768;
 constexpr uint64_t kPcMaxParts = 65536;
 constexpr uint64_t kMaxParts = 1ull << 31;
 
@@ -88,7 +91,8 @@ int plan_build(int device, const uint64_t* offsets, const uint64_t* lengths, uin
     return fail(S3H_EINVAL, "plan: need offsets, lengths and 0 < n <= 2^31 (n=%llu)",
                 (unsigned long long)n);
   if (int rc = check_device(device)) return rc;
-  if (kernel == S3H_KERNEL_AUTO) kernel = n <= kPcMaxParts ? S3H_KERNEL_PAIR : S3H_KERNEL_LANE;
+  if (kernel == S3H_KERNEL_AUTO)
+    kernel = n <= kPairMaxParts ? S3H_KERNEL_PAIR : n <= kPcMaxParts ? S3H_KERNEL_PC : S3H_KERNEL_LANE;
   if (kernel != S3H_KERNEL_PC && kernel != S3H_KERNEL_LANE && kernel != S3H_KERNEL_PAIR)
     return fail(S3H_EINVAL, "plan: unknown kernel %d", kernel);
 

@@ -279,6 +279,7 @@ __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A)
     }
   } else {
     // ---------------------------------------------------------------- consumer
+    __builtin_amdgcn_s_setprio(3);  // wins VALU arbitration if a producer shares the SIMD
     const uint32_t part = pair_chain(lane);
     const bool ahalf = pair_is_ahalf(lane);
     const uint32_t slot = slot0 + part;

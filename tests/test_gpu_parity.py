@@ -63,6 +63,9 @@ def test_random_ragged_vs_oracle(torch_cuda, oracle, kernel):
 
 def test_kernels_agree_on_many_small_parts(torch_cuda, oracle):
     """n > 65536 exercises the AUTO switch to the fused kernel; overlapping parts allowed."""
+    assert s3.Plan([0] * 70000, [1] * 70000).info()["kernel"] == "lane"
+    assert s3.Plan([0] * 40000, [1] * 40000).info()["kernel"] == "pc"
+    assert s3.Plan([0] * 1024, [1] * 1024).info()["kernel"] == "pair"
     rng = np.random.default_rng(7)
     n = 70000
     lens = rng.integers(0, 200, n)
