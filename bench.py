@@ -116,7 +116,7 @@ def cpu_baseline(host: np.ndarray, offs, lens, gpu_digests: np.ndarray, nsample:
         pass
     gib = float(ln.sum()) / 2**30
     return {"value": round(gib / dt, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "sample": f"{n} of the bench's 8 MiB parts ({gib:.2f} GiB) with lib/hash "
+            "sample": f"{n} of the bench's parts ({gib:.2f} GiB) with lib/hash "
                       f"sha256::sha256 on {threads} threads, round-robin; same bytes as the GPU",
             "single_thread_GiBps": round(float(ln[:n1].sum()) / 2**30 / dt1, 3),
             "cpu_model": cpu_model, "digests_match_gpu": parity}
