@@ -29,6 +29,12 @@ sys.path.insert(0, ROOT)
 SEED = 20241008
 MIB = 1 << 20
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+CLOCK_GHZ = 2.4                 # in-kernel clock measured by tools/ubench (2.39-2.40 GHz)
+# Instructions one chain's wave issues per 64-B block (ISA audit: `make isa`, consumer loop;
+# pair = 640 round VALU + state/X bookkeeping + 16 ds_read_b128).  A lone wave issues about
+# one instruction per 5 cycles (profiles/r01_ubench_valu_issue.txt): this, not HBM, bounds
+# each part's chain.
+CHAIN_INSTR_PER_BLOCK = {"pair": 672, "pc": 923, "lane": 1425}
 
 
 def parse():
@@ -134,10 +140,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local)
+    # One process per GPU.  S3H_BENCH_SHARE_GPU=1 (rehearsal on a 1-GPU box only) maps ranks
+    # onto the visible devices modulo their count and uses gloo for the timing collectives.
+    share = os.environ.get("S3H_BENCH_SHARE_GPU") == "1"
+    gpu = local % torch.cuda.device_count() if share else local
+    torch.cuda.set_device(gpu)
+    backend = "gloo" if share else "nccl"
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+    dev = torch.device("cuda", gpu)
+    local = gpu
 
     ids, lens, offs, name = workload(args.config, rank, world, args.parts_per_gpu,
                                     args.part_bytes)
@@ -171,9 +186,10 @@ def main():
         dist.barrier()
     wall = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64,
+                     device=dev if backend == "nccl" else "cpu")
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # max over ranks: the slowest GPU sets the time
     wall, kern_ms_max = float(t[0]), float(t[1])
 
     # parity spot-check of the last timed step's digests against the reference fixtures
@@ -200,6 +216,12 @@ def main():
     # one part = one sequential chain on one lane: report what one chain sustains and how
     # many of the chip's 256 CU x 4 SIMD x 64 = 65,536 lanes the batch can occupy
     chain_gbps = float(lens.max()) / (kern_ms / 1e3) / 1e9
+    cyc_per_block = kern_ms / 1e3 * CLOCK_GHZ * 1e9 / info["max_blocks"]
+    issue = {"bound": "per-wave instruction issue of each part's sequential chain",
+             "chain_instr_per_block": CHAIN_INSTR_PER_BLOCK[info["kernel"]],
+             "cycles_per_block": round(cyc_per_block, 1),
+             "cycles_per_instr": round(cyc_per_block / CHAIN_INSTR_PER_BLOCK[info["kernel"]], 3),
+             "lone_wave_issue_cycles_measured": 5.1, "clock_GHz_assumed": CLOCK_GHZ}
 
     if rank == 0:
         line = {
@@ -223,6 +245,7 @@ def main():
                          "compressions_per_s": round(compressions / (kern_ms / 1e3), 1),
                          "per_chain_GBps": round(chain_gbps, 4),
                          "lanes_occupied_frac": round(min(len(lens), 65536) / 65536, 5)},
+            "issue": issue,
         }
         if world == 1 and not args.no_cpu_baseline:
             n = min(args.cpu_sample_parts, len(lens))
