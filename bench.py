@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--kernel", default="auto", choices=["auto", "pair", "pc", "lane"])
     ap.add_argument("--cpu-sample-parts", type=int, default=384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--slice-bytes", type=int, default=0, help="host mode: bytes per part per slice")
     ap.add_argument("--mode", default="device", choices=["device", "host"],
                     help="host: H2D-inclusive rate from pinned host memory (not the metric)")
     return ap.parse_args()
@@ -267,11 +268,11 @@ def host_mode(args, s3, torch, dist, data, ids, lens, offs, world, rank, name):
     torch.cuda.empty_cache()
     h = host.numpy()
     views = [h[int(o):int(o) + int(L)] for o, L in zip(offs, lens)]
-    out = s3.sha256_batch_host(views, ndevices=1)
+    out = s3.sha256_batch_host(views, ndevices=1, slice_bytes=args.slice_bytes)
     times = []
     for _ in range(max(1, args.steps)):
         t0 = time.perf_counter()
-        out = s3.sha256_batch_host(views, ndevices=1)
+        out = s3.sha256_batch_host(views, ndevices=1, slice_bytes=args.slice_bytes)
         times.append(time.perf_counter() - t0)
     wall = float(np.mean(times))
     with open(os.path.join(ROOT, "tests", "golden", "sha256_golden.json")) as f:
@@ -282,7 +283,8 @@ def host_mode(args, s3, torch, dist, data, ids, lens, offs, world, rank, name):
     if rank == 0:
         print(json.dumps({"metric": "host-resident (H2D-inclusive) SHA-256 GiB/s", "value":
                           round(float(lens.sum()) / 2**30 / wall, 3), "unit": "GiB/s",
-                          "n_gpus": 1, "steps": args.steps, "config": {"workload": name},
+                          "n_gpus": 1, "steps": args.steps,
+                          "config": {"workload": name, "slice_bytes": args.slice_bytes or "auto"},
                           "fixture_mismatches": int(bad), "ms_per_batch": round(wall * 1e3, 2)}))
     return 0
 

@@ -84,7 +84,9 @@ int s3h_sha256_batch_device(int device, const void *d_base, const uint64_t *offs
  * parts[i] (host memory, pinned or pageable) of lengths[i] bytes -> digests (host, n*8).
  * Parts are sharded round-robin over `ndevices` GPUs (0 = all visible), part i on device
  * i % ndevices; each device streams its parts through HBM in slices of `slice_bytes` per
- * part (0 = default 4 MiB) with copies overlapped with hashing.  Blocking. */
+ * part (0 = auto: 256 KiB when the parts are equal-length chunks at a constant host stride,
+ * copied with one 2-D copy per slice; 2 MiB otherwise) with copies overlapped with hashing.
+ * Blocking. */
 int s3h_sha256_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                           uint32_t *digests, int ndevices, uint64_t slice_bytes);
 

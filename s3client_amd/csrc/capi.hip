@@ -171,10 +171,23 @@ int run_host_shard(const HostShard& sh, const uint8_t* const* parts, const uint6
   if (n == 0) return S3H_OK;
   DeviceGuard g(sh.device);
   std::vector<uint64_t> offs(n), lens(n);
-  for (uint64_t j = 0; j < n; ++j) {
-    offs[j] = j * slice;
-    lens[j] = lengths[sh.parts[j]];
-  }
+  for (uint64_t j = 0; j < n; ++j) lens[j] = lengths[sh.parts[j]];
+  // Fast path: all parts of this shard have one length and sit at a constant positive host
+  // stride (a file's chunks); then each slice is ONE hipMemcpy2DAsync instead of n copies,
+  // and small slices (short pipeline fill) pay off.  Otherwise per-part copies cost ~10 us
+  // each, so slices are larger (profiles/r01_host_slices.jsonl).
+  bool uniform = n > 1;
+  const intptr_t stride = n > 1 ? parts[sh.parts[1]] - parts[sh.parts[0]] : 0;
+  for (uint64_t j = 1; j < n && uniform; ++j)
+    uniform = lens[j] == lens[0] && parts[sh.parts[j]] - parts[sh.parts[j - 1]] == stride;
+  uniform = uniform && stride >= intptr_t(lens[0]) && lens[0] > 0;
+  if (slice == 0) slice = uniform ? (256ull << 10) : (2ull << 20);
+  // The 3-slot ring holds 3*n*slice bytes: keep it within min(16 GiB, free/4) of HBM.
+  size_t free_b = 0, total_b = 0;
+  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  const uint64_t budget = std::min<uint64_t>(16ull << 30, free_b / 4);
+  if (3 * n * slice > budget) slice = std::max<uint64_t>(64, budget / (3 * n) / 64 * 64);
+  for (uint64_t j = 0; j < n; ++j) offs[j] = j * slice;
   s3h_plan_s* P = nullptr;
   if (int rc = plan_build(sh.device, offs.data(), lens.data(), n, S3H_KERNEL_AUTO, &P)) return rc;
   struct Cleanup {
@@ -211,13 +224,23 @@ int run_host_shard(const HostShard& sh, const uint8_t* const* parts, const uint6
       if (e != hipSuccess) { rc = fail(S3H_EHIP, "wait: %s", hipGetErrorString(e)); break; }
     }
     const uint64_t byte0 = b0 * 64;
-    for (uint64_t j = 0; j < n && rc == S3H_OK; ++j) {
-      const uint64_t len = lens[j];
-      if (byte0 >= len) continue;
-      const uint64_t cnt = std::min(slice, len - byte0);
-      hipError_t e = hipMemcpyAsync(slot_base + j * slice, parts[sh.parts[j]] + byte0, cnt,
-                                    hipMemcpyHostToDevice, copy_s);
-      if (e != hipSuccess) rc = fail(S3H_EHIP, "H2D: %s", hipGetErrorString(e));
+    if (uniform) {
+      // equal-length parts at a constant host stride (file chunks): one 2-D copy per slice
+      if (byte0 < lens[0]) {
+        const uint64_t cnt = std::min(slice, lens[0] - byte0);
+        hipError_t e = hipMemcpy2DAsync(slot_base, slice, parts[sh.parts[0]] + byte0, stride, cnt,
+                                        n, hipMemcpyHostToDevice, copy_s);
+        if (e != hipSuccess) rc = fail(S3H_EHIP, "H2D 2D: %s", hipGetErrorString(e));
+      }
+    } else {
+      for (uint64_t j = 0; j < n && rc == S3H_OK; ++j) {
+        const uint64_t len = lens[j];
+        if (byte0 >= len) continue;
+        const uint64_t cnt = std::min(slice, len - byte0);
+        hipError_t e = hipMemcpyAsync(slot_base + j * slice, parts[sh.parts[j]] + byte0, cnt,
+                                      hipMemcpyHostToDevice, copy_s);
+        if (e != hipSuccess) rc = fail(S3H_EHIP, "H2D: %s", hipGetErrorString(e));
+      }
     }
     if (rc) break;
     hipError_t e = hipEventRecord(copied[r], copy_s);
@@ -324,7 +347,6 @@ int s3h_sha256_batch_host(const uint8_t* const* parts, const uint64_t* lengths, 
   int count = 0;
   if (int rc = s3h_device_count(&count)) return rc;
   if (ndevices <= 0 || ndevices > count) ndevices = count;
-  if (slice_bytes == 0) slice_bytes = 4ull << 20;
   if (slice_bytes % 64) return fail(S3H_EINVAL, "slice_bytes must be a multiple of 64");
   for (uint64_t i = 0; i < n; ++i)
     if (!parts[i] && lengths[i]) return fail(S3H_EINVAL, "batch_host: part %llu is null", (unsigned long long)i);

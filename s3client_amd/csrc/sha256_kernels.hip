@@ -59,11 +59,27 @@ __device__ __forceinline__ void store_result(const LaunchArgs& A, uint32_t slot,
   }
 }
 
+// First block index that may NOT be loaded with fetch_full: the part's first partial block
+// or the end of the launch's range, whichever comes first.
+__device__ __forceinline__ uint64_t fetch_end(uint64_t len, uint64_t blk_end) {
+  const uint64_t nfull = len >> 6;
+  return nfull < blk_end ? nfull : blk_end;
+}
+
 // Decode block `blk` of the part whose bytes for that block start at `p`.
+// Blocks at or past `limit` (the launch's blk_end) are never consumed; they are zero-filled
+// without touching memory (the pair producer's odd lanes can step one block past the range).
 __device__ __forceinline__ void make_block(const RawBlock& r, uint32_t sel, const uint8_t* p,
-                                           uint64_t len, uint64_t blk, uint32_t w[16]) {
-  if (blk < (len >> 6)) decode_full(r, sel, w);
-  else build_tail(p, len, blk, w);
+                                           uint64_t len, uint64_t blk, uint64_t limit,
+                                           uint32_t w[16]) {
+  if (blk >= limit) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = 0;
+  } else if (blk < (len >> 6)) {
+    decode_full(r, sel, w);
+  } else {
+    build_tail(p, len, blk, w);
+  }
 }
 
 // ------------------------------------------------------------------ fused lane kernel
@@ -78,14 +94,16 @@ __global__ __launch_bounds__(256) void sha256_lane_kernel(LaunchArgs A) {
   load_state(A, slot, st);
   const uint8_t* p = A.base + s.off + 64ull * (A.blk_begin - A.blk_origin);
   const uint32_t sel = be_selector(uint32_t(reinterpret_cast<uintptr_t>(p) & 3));
-  const uint64_t nfull = s.len >> 6;
+  // Only whole blocks inside both the part and this launch's range are ever loaded: a ranged
+  // launch's base may hold nothing beyond blk_end (host streaming ring).
+  const uint64_t fend = fetch_end(s.len, A.blk_end);
   RawBlock cur;
-  if (A.blk_begin < nfull) fetch_full(p, cur);
+  if (A.blk_begin < fend) fetch_full(p, cur);
   for (uint64_t b = A.blk_begin; b < end; ++b) {
     RawBlock nxt;
-    if (b + 1 < nfull) fetch_full(p + 64, nxt);  // prefetch one block ahead
+    if (b + 1 < fend) fetch_full(p + 64, nxt);  // prefetch one block ahead
     uint32_t w[16], wk[64];
-    make_block(cur, sel, p, s.len, b, w);
+    make_block(cur, sel, p, s.len, b, A.blk_end, w);
     schedule_wk(w, wk);
     uint32_t t[8];
 #pragma unroll
@@ -103,10 +121,10 @@ __global__ __launch_bounds__(256) void sha256_lane_kernel(LaunchArgs A) {
 // Decode + pad + schedule one block and store W[t]+K[t] as 16 x 16 B rows of LDS.
 template <int kRow>
 __device__ __forceinline__ void produce_block(const RawBlock& r, uint32_t sel, const uint8_t* bp,
-                                              uint64_t len, uint64_t blk, uint4 (*buf)[kRow],
-                                              uint32_t lane) {
+                                              uint64_t len, uint64_t blk, uint64_t limit,
+                                              uint4 (*buf)[kRow], uint32_t lane) {
   uint32_t w[16], wk[64];
-  make_block(r, sel, bp, len, blk, w);
+  make_block(r, sel, bp, len, blk, limit, w);
   schedule_wk(w, wk);
 #pragma unroll
   for (int q = 0; q < 16; ++q)
@@ -141,24 +159,24 @@ __global__ __launch_bounds__(kPcThreads) void sha256_pc_kernel(LaunchArgs A) {
     const uint64_t b0 = A.blk_begin;
     const uint8_t* p = A.base + s.off + 64ull * (b0 - A.blk_origin);
     const uint32_t sel = be_selector(uint32_t(reinterpret_cast<uintptr_t>(p) & 3));
-    const uint64_t nfull = s.len >> 6;
+    const uint64_t fend = fetch_end(s.len, A.blk_end);
     RawBlock ra, rb;
-    if (b0 < nfull) fetch_full(p, ra);
-    if (b0 + 1 < nfull) fetch_full(p + 64, rb);
-    produce_block(ra, sel, p, s.len, b0, lds_wk[0], lane);
+    if (b0 < fend) fetch_full(p, ra);
+    if (b0 + 1 < fend) fetch_full(p + 64, rb);
+    produce_block(ra, sel, p, s.len, b0, A.blk_end, lds_wk[0], lane);
     __syncthreads();
     for (uint64_t k = 1; k <= iters; k += 2) {
       // odd step: block b0+k from rb into buffer 1; refill ra with block b0+k+1
       if (k < iters) {
-        if (b0 + k + 1 < nfull) fetch_full(p + 64 * (k + 1), ra);
-        produce_block(rb, sel, p + 64 * k, s.len, b0 + k, lds_wk[1], lane);
+        if (b0 + k + 1 < fend) fetch_full(p + 64 * (k + 1), ra);
+        produce_block(rb, sel, p + 64 * k, s.len, b0 + k, A.blk_end, lds_wk[1], lane);
       }
       __syncthreads();
       if (k + 1 > iters) break;
       // even step: block b0+k+1 from ra into buffer 0; refill rb with block b0+k+2
       if (k + 1 < iters) {
-        if (b0 + k + 2 < nfull) fetch_full(p + 64 * (k + 2), rb);
-        produce_block(ra, sel, p + 64 * (k + 1), s.len, b0 + k + 1, lds_wk[0], lane);
+        if (b0 + k + 2 < fend) fetch_full(p + 64 * (k + 2), rb);
+        produce_block(ra, sel, p + 64 * (k + 1), s.len, b0 + k + 1, A.blk_end, lds_wk[0], lane);
       }
       __syncthreads();
     }
@@ -257,23 +275,23 @@ __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A)
     if (slot < A.n) s = A.slots[slot];
     const uint8_t* p = A.base + s.off + 64ull * (b0 + half - A.blk_origin);
     const uint32_t sel = be_selector(uint32_t(reinterpret_cast<uintptr_t>(A.base + s.off) & 3));
-    const uint64_t nfull = s.len >> 6;
+    const uint64_t fend = fetch_end(s.len, A.blk_end);
     const uint64_t bh = b0 + half;  // this lane's first block
     RawBlock ra, rb;
-    if (bh < nfull) fetch_full(p, ra);
-    if (bh + 2 < nfull) fetch_full(p + 128, rb);
-    produce_block(ra, sel, p, s.len, bh, lds_wk[0][half], part);
+    if (bh < fend) fetch_full(p, ra);
+    if (bh + 2 < fend) fetch_full(p + 128, rb);
+    produce_block(ra, sel, p, s.len, bh, A.blk_end, lds_wk[0][half], part);
     __syncthreads();
     for (uint64_t k = 1; k <= steps; k += 2) {
       if (k < steps) {
-        if (bh + 2 * (k + 1) < nfull) fetch_full(p + 128 * (k + 1), ra);
-        produce_block(rb, sel, p + 128 * k, s.len, bh + 2 * k, lds_wk[1][half], part);
+        if (bh + 2 * (k + 1) < fend) fetch_full(p + 128 * (k + 1), ra);
+        produce_block(rb, sel, p + 128 * k, s.len, bh + 2 * k, A.blk_end, lds_wk[1][half], part);
       }
       __syncthreads();
       if (k + 1 > steps) break;
       if (k + 1 < steps) {
-        if (bh + 2 * (k + 2) < nfull) fetch_full(p + 128 * (k + 2), rb);
-        produce_block(ra, sel, p + 128 * (k + 1), s.len, bh + 2 * (k + 1), lds_wk[0][half], part);
+        if (bh + 2 * (k + 2) < fend) fetch_full(p + 128 * (k + 2), rb);
+        produce_block(ra, sel, p + 128 * (k + 1), s.len, bh + 2 * (k + 1), A.blk_end, lds_wk[0][half], part);
       }
       __syncthreads();
     }

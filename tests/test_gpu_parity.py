@@ -182,3 +182,25 @@ def test_plan_rejects_undersized_buffers(torch_cuda):
     plan = s3.Plan([50], [60])
     with pytest.raises(ValueError):
         plan.launch(data, dig)
+
+
+def test_host_path_small_slices_large_batch(torch_cuda, oracle):
+    """Host streaming with many slices per part: every ranged launch must load only bytes of
+    its own slice (regression: prefetches once ran one block past the ring slot)."""
+    rng = np.random.default_rng(3)
+    lens = [2 << 20, (2 << 20) + 13, 1 << 20, 777777, 0, 64, 300000] * 20
+    parts = [rng.integers(0, 256, L, dtype=np.uint8) for L in lens]
+    want = np.stack([oracle.sha256(p.tobytes()) for p in parts])
+    for sl in (256 << 10, 64 << 10):
+        assert np.array_equal(s3.sha256_batch_host(parts, slice_bytes=sl), want), sl
+
+
+def test_host_path_uniform_stride_2d_copies(torch_cuda, oracle):
+    """Equal-length parts at a constant host stride take the one-2D-copy-per-slice path."""
+    rng = np.random.default_rng(4)
+    L, stride, n = (1 << 20) + 7, (1 << 20) + 64, 64
+    buf = rng.integers(0, 256, stride * n, dtype=np.uint8)
+    views = [buf[i * stride:i * stride + L] for i in range(n)]
+    want = oracle.batch(buf, np.arange(n) * stride, np.full(n, L))
+    for sl in (64 << 10, 256 << 10, 0):
+        assert np.array_equal(s3.sha256_batch_host(views, slice_bytes=sl), want), sl
