@@ -23,7 +23,11 @@ $(LIBDIR)/lib_hash.o: $(CSRC)/cpu/lib_hash.cpp include/sha256.h include/utility.
 	@mkdir -p $(LIBDIR)
 	$(CXX) $(CXXFLAGS) -c -o $@ $<
 
-$(LIB): $(LIBDIR)/capi.o $(LIBDIR)/lib_hash.o
+$(LIBDIR)/lib_md5.o: $(CSRC)/cpu/lib_md5.cpp include/md5.h include/utility.h include/s3hash.h
+	@mkdir -p $(LIBDIR)
+	$(CXX) $(CXXFLAGS) -c -o $@ $<
+
+$(LIB): $(LIBDIR)/capi.o $(LIBDIR)/lib_hash.o $(LIBDIR)/lib_md5.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 
 oracle:

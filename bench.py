@@ -34,7 +34,7 @@ CLOCK_GHZ = 2.4                 # in-kernel clock measured by tools/ubench (2.39
 # pair = 640 round VALU + state/X bookkeeping + 16 ds_read_b128).  A lone wave issues about
 # one instruction per 5 cycles (profiles/r01_ubench_valu_issue.txt): this, not HBM, bounds
 # each part's chain.
-CHAIN_INSTR_PER_BLOCK = {"pair": 672, "pc": 923, "lane": 1425}
+CHAIN_INSTR_PER_BLOCK = {"pair": 672, "pc": 923, "lane": 1425, "md5-pc": 280}
 
 
 def parse():
@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--parts-per-gpu", type=int, default=0, help="override batch size")
     ap.add_argument("--part-bytes", type=int, default=0, help="override part size (sweeps)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "pair", "pc", "lane"])
+    ap.add_argument("--algo", default="sha256", choices=["sha256", "md5"],
+                    help="md5: the SURVEY 8(f) Content-MD5/ETag kernel (not the metric)")
     ap.add_argument("--cpu-sample-parts", type=int, default=384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--slice-bytes", type=int, default=0, help="host mode: bytes per part per slice")
@@ -94,23 +96,29 @@ def pmc_traffic(cfg: str, kernel: str, algo_bytes: float):
     return int(round(ratio * algo_bytes)), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(host: np.ndarray, offs, lens, gpu_digests: np.ndarray, nsample: int):
-    """lib/hash timed on this host's cores over a bounded sample of the same parts."""
+def cpu_baseline(host: np.ndarray, offs, lens, gpu_digests: np.ndarray, nsample: int,
+                 algo: str = "sha256"):
+    """lib/hash timed on this host's cores over a bounded sample of the same parts.  MD5: the
+    reference has no padded in-memory md5 (md5.cpp:119-122), so the oracle port is timed."""
     from tests.oracle_lib import REF_SO, ORACLE_SO, u64p
-    kind = "reference" if os.path.exists(REF_SO) else "port"
+    kind = "reference" if os.path.exists(REF_SO) and algo == "sha256" else "port"
     L = ctypes.CDLL(REF_SO if kind == "reference" else ORACLE_SO)
-    fn = L.ref_sha256_batch if kind == "reference" else L.oracle_sha256_batch
+    if algo == "md5":
+        fn = L.oracle_md5_batch
+    else:
+        fn = L.ref_sha256_batch if kind == "reference" else L.oracle_sha256_batch
+    words = 4 if algo == "md5" else 8
     fn.argtypes = [ctypes.c_void_p, u64p, u64p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
     threads = int(os.environ.get("S3H_CPU_THREADS", min(16, os.cpu_count() or 1)))
     n = min(nsample, len(lens))
     o = np.ascontiguousarray(offs[:n], dtype=np.uint64)
     ln = np.ascontiguousarray(lens[:n], dtype=np.uint64)
-    out = np.zeros((n, 8), dtype=np.uint32)
+    out = np.zeros((n, words), dtype=np.uint32)
     t0 = time.perf_counter()
     fn(host.ctypes.data, o.ctypes.data_as(u64p), ln.ctypes.data_as(u64p), n, out.ctypes.data, threads)
     dt = time.perf_counter() - t0
     n1 = min(8, n)
-    out1 = np.zeros((n1, 8), dtype=np.uint32)
+    out1 = np.zeros((n1, words), dtype=np.uint32)
     t1 = time.perf_counter()
     fn(host.ctypes.data, o.ctypes.data_as(u64p), ln.ctypes.data_as(u64p), n1, out1.ctypes.data, 1)
     dt1 = time.perf_counter() - t1
@@ -123,8 +131,9 @@ def cpu_baseline(host: np.ndarray, offs, lens, gpu_digests: np.ndarray, nsample:
         pass
     gib = float(ln.sum()) / 2**30
     return {"value": round(gib / dt, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "sample": f"{n} of the bench's parts ({gib:.2f} GiB) with lib/hash "
-                      f"sha256::sha256 on {threads} threads, round-robin; same bytes as the GPU",
+            "sample": f"{n} of the bench's parts ({gib:.2f} GiB) with "
+                      f"{'lib/hash sha256::sha256' if kind == 'reference' else 'the oracle port (' + algo + ')'}"
+                      f" on {threads} threads, round-robin; same bytes as the GPU",
             "single_thread_GiBps": round(float(ln[:n1].sum()) / 2**30 / dt1, 3),
             "cpu_model": cpu_model, "digests_match_gpu": parity}
 
@@ -160,10 +169,11 @@ def main():
     nbytes = int(offs[-1] + lens[-1]) + 256
     data = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     s3.generate_parts(data, offs, lens, ids, SEED)
-    digests = torch.zeros((len(lens), 8), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
-    plan = s3.Plan(offs, lens, device=local, kernel=args.kernel)
+    plan = s3.Plan(offs, lens, device=local, kernel=args.kernel, algo=args.algo)
+    digests = torch.zeros((len(lens), plan.words), dtype=torch.int32, device=dev)
     info = plan.info()
+    kname = "md5-pc" if args.algo == "md5" else info["kernel"]
 
     if args.mode == "host":
         return host_mode(args, s3, torch, dist, data, ids, lens, offs, world, rank, name)
@@ -200,6 +210,10 @@ def main():
     fixtures = {e["p"]: e["digest"] for e in gold["c2_parts"]}
     if args.config == "c3":
         fixtures = {e["p"]: e["digest"] for e in gold["c3_parts"]}
+    if args.algo == "md5":
+        fixtures = {e["p"]: e["digest"] for e in gold["md5"]["c2_parts"]} if args.config != "c3" else {}
+    if args.part_bytes:
+        fixtures = {}
     checked = bad = 0
     for slot, p in enumerate(ids):
         want = fixtures.get(int(p))
@@ -210,30 +224,32 @@ def main():
     part_bytes = float(lens.sum())
     total_bytes = part_bytes * world * args.steps
     value = total_bytes / 2**30 / wall
-    algo_bytes = part_bytes + 32 * len(lens)           # read once + digests written
+    algo_bytes = part_bytes + 4 * plan.words * len(lens)  # read once + digests written
     achieved = algo_bytes / (kern_ms / 1e3) / 1e9      # GB/s, this rank's kernel
     compressions = info["total_blocks"]
-    traffic, traffic_src = pmc_traffic(args.config, info["kernel"], algo_bytes)
+    traffic, traffic_src = pmc_traffic(args.config, kname, algo_bytes)
     # one part = one sequential chain on one lane: report what one chain sustains and how
     # many of the chip's 256 CU x 4 SIMD x 64 = 65,536 lanes the batch can occupy
     chain_gbps = float(lens.max()) / (kern_ms / 1e3) / 1e9
     cyc_per_block = kern_ms / 1e3 * CLOCK_GHZ * 1e9 / info["max_blocks"]
     issue = {"bound": "per-wave instruction issue of each part's sequential chain",
-             "chain_instr_per_block": CHAIN_INSTR_PER_BLOCK[info["kernel"]],
+             "chain_instr_per_block": CHAIN_INSTR_PER_BLOCK[kname],
              "cycles_per_block": round(cyc_per_block, 1),
-             "cycles_per_instr": round(cyc_per_block / CHAIN_INSTR_PER_BLOCK[info["kernel"]], 3),
+             "cycles_per_instr": round(cyc_per_block / CHAIN_INSTR_PER_BLOCK[kname], 3),
              "lone_wave_issue_cycles_measured": 5.1, "clock_GHz_assumed": CLOCK_GHZ}
 
     if rank == 0:
         line = {
-            "metric": "device-resident SHA-256 GiB/s over 8 MiB parts; bit-exact digests vs lib/hash",
+            "metric": ("device-resident SHA-256 GiB/s over 8 MiB parts; bit-exact digests vs lib/hash"
+                       if args.algo == "sha256" else
+                       "device-resident MD5 GiB/s over 8 MiB parts (SURVEY 8(f); not the metric)"),
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic: generator G(seed=20241008) written in HBM by a HIP kernel",
             "config": {"workload": name, "parts_per_gpu": int(len(lens)),
                        "part_bytes": int(lens[0]) if args.config != "c3" else "5-64 MiB",
-                       "kernel": info["kernel"], "grid": info["grid"],
+                       "kernel": kname, "grid": info["grid"],
                        "parallelism": f"parts sharded round-robin over {world} GPU(s), no collective"},
             "parity": {"fixtures_checked": checked, "mismatches": int(bad)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -252,7 +268,7 @@ def main():
             n = min(args.cpu_sample_parts, len(lens))
             end = int(offs[n - 1] + lens[n - 1])
             host = data[:end].cpu().numpy()
-            line["cpu_baseline"] = cpu_baseline(host, offs, lens, gd, n)
+            line["cpu_baseline"] = cpu_baseline(host, offs, lens, gd, n, args.algo)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

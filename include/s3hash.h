@@ -46,6 +46,11 @@ enum s3h_kernel {
   S3H_KERNEL_PAIR = 3  /* producer/consumer with each chain split over a lane pair (DPP) */
 };
 
+enum s3h_algo {
+  S3H_ALGO_SHA256 = 0, /* payload SHA-256 (x-amz-content-sha256), digests n x 8 words */
+  S3H_ALGO_MD5 = 1     /* MD5 (Content-MD5, multipart ETags), digests n x 4 words */
+};
+
 /* Last error message of the calling thread ("" if none). */
 const char *s3h_last_error(void);
 int s3h_api_version(void);
@@ -61,6 +66,10 @@ typedef struct s3h_plan_s *s3h_plan_t;
 
 int s3h_plan_create(int device, const uint64_t *offsets, const uint64_t *lengths, uint64_t n,
                     int kernel, s3h_plan_t *plan);
+/* Same for any algorithm (s3h_algo); digests are 8 (SHA-256) or 4 (MD5) words per part. */
+int s3h_plan_create_ex(int device, int algo, const uint64_t *offsets, const uint64_t *lengths,
+                       uint64_t n, int kernel, s3h_plan_t *plan);
+int s3h_plan_algo(s3h_plan_t plan);
 int s3h_plan_destroy(s3h_plan_t plan);
 /* Asynchronous on `stream`: d_base and d_digests (n*8 uint32) are device pointers. */
 int s3h_plan_launch(s3h_plan_t plan, const void *d_base, uint32_t *d_digests, void *stream);
@@ -80,6 +89,11 @@ int s3h_sha256_batch_device(int device, const void *d_base, const uint64_t *offs
                             const uint64_t *lengths, uint64_t n, uint32_t *d_digests,
                             void *stream);
 
+/* Batched MD5 (lib/hash/md5.cpp semantics with md5_file's padding): n x 4 words, the
+ * digest bytes in memory order (md5::hash_to_text prints them). */
+int s3h_md5_batch_device(int device, const void *d_base, const uint64_t *offsets,
+                         const uint64_t *lengths, uint64_t n, uint32_t *d_digests, void *stream);
+
 /* ---------------------------------------------------------------- host-resident path
  * parts[i] (host memory, pinned or pageable) of lengths[i] bytes -> digests (host, n*8).
  * Parts are sharded round-robin over `ndevices` GPUs (0 = all visible), part i on device
@@ -89,6 +103,9 @@ int s3h_sha256_batch_device(int device, const void *d_base, const uint64_t *offs
  * Blocking. */
 int s3h_sha256_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                           uint32_t *digests, int ndevices, uint64_t slice_bytes);
+
+int s3h_md5_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
+                       uint32_t *digests, int ndevices, uint64_t slice_bytes);
 
 /* ---------------------------------------------------------------- synthetic inputs
  * Fill part i (at d_base + offsets[i], 8-B aligned, lengths[i] bytes) with generator
@@ -103,6 +120,8 @@ int s3h_generate_parts(int device, void *d_base, const uint64_t *offsets,
 void s3h_cpu_sha256(const uint8_t *data, uint64_t length, uint32_t hash[8]);
 void s3h_cpu_hmac256(const uint8_t *data, uint64_t length, const uint8_t *key,
                      uint64_t key_length, uint8_t mac[32]);
+/* MD5 drop-in (md5::md5, include/md5.h): hash[0..3], digest bytes = words in LE order. */
+void s3h_cpu_md5(const uint8_t *data, uint64_t length, uint32_t hash[4]);
 /* lowercase hex of the 32 digest bytes + NUL (sha256::hash_to_text). */
 void s3h_hash_to_text(const uint32_t hash[8], char text[65]);
 /* "sha-ni" or "scalar": which compression the CPU drop-in dispatched to. */

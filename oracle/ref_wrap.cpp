@@ -10,7 +10,12 @@
 #include <thread>
 #include <vector>
 
+#include "md5.h"     // /root/reference/lib/hash/md5.h (via -I)
 #include "sha256.h"  // /root/reference/lib/hash/sha256.h (via -I)
+
+namespace md5 {
+void md5_file(const char *fname, uint32_t hash[4]);  // md5.cpp:132 (no header declaration)
+}
 
 void hmac256(const uint8_t *data, size_t length, const uint8_t *key, size_t key_length,
              uint8_t hmac_hash[32]);  // declared ad hoc like lib/src/aws_sign.cpp:54-55
@@ -29,6 +34,13 @@ void ref_hmac256(const uint8_t *data, uint64_t len, const uint8_t *key, uint64_t
                  uint8_t out[32]) {
   hmac256(data, (size_t)len, key, (size_t)klen, out);
 }
+
+void ref_md5_stream(uint32_t h[4], const uint8_t *data, uint64_t len) {
+  md5::md5_stream(h, data, len);
+}
+
+// md5_file is the reference's only correctly padded MD5 entry point (md5.cpp:132-180).
+void ref_md5_file(const char *path, uint32_t out[4]) { md5::md5_file(path, out); }
 
 // lib/hash's sha256() over n parts with `threads` std::threads, parts round-robin
 // (BASELINE.md "CPU baseline plan").

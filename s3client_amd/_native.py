@@ -24,8 +24,12 @@ C_ABI_SYMBOLS = (
     "s3h_plan_create", "s3h_plan_destroy", "s3h_plan_launch", "s3h_plan_launch_range",
     "s3h_plan_info", "s3h_sha256_batch_device", "s3h_sha256_batch_host",
     "s3h_generate_parts", "s3h_cpu_sha256", "s3h_cpu_hmac256", "s3h_hash_to_text",
-    "s3h_cpu_backend",
+    "s3h_cpu_backend", "s3h_cpu_md5", "s3h_plan_create_ex", "s3h_plan_algo",
+    "s3h_md5_batch_device", "s3h_md5_batch_host",
 )
+ALGO_SHA256, ALGO_MD5 = 0, 1
+ALGO_IDS = {"sha256": ALGO_SHA256, "md5": ALGO_MD5}
+DIGEST_WORDS = {ALGO_SHA256: 8, ALGO_MD5: 4}
 # the lib/hash drop-in (C++ mangled names identical to the reference's libs3client.a)
 CXX_DROPIN_SYMBOLS = (
     "_ZN6sha2566sha256EPKhmPj",          # sha256::sha256(const uint8_t*, size_t, uint32_t*)
@@ -35,6 +39,10 @@ CXX_DROPIN_SYMBOLS = (
     "_ZN6sha25611sha256_fileEPKcPj",     # sha256::sha256_file(const char*, uint32_t*)
     "_Z7hmac256PKhmS0_mPh",              # hmac256(...)
     "_Z12alloc_paddedmmPmPh",            # alloc_padded(...)
+    "_ZN3md510md5_streamEPjPKhm",        # md5::md5_stream(uint32_t*, const uint8_t*, uint64_t)
+    "_ZN3md53md5EPKhmPj",                # md5::md5(const uint8_t*, size_t, uint32_t*)
+    "_ZN3md510print_hashEPj",            # md5::print_hash(uint32_t*)
+    "_ZN3md58md5_fileEPKcPj",            # md5::md5_file(const char*, uint32_t*)
 )
 
 
@@ -64,6 +72,10 @@ def lib() -> ctypes.CDLL:
             L.s3h_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
             L.s3h_plan_create.argtypes = [ctypes.c_int, u64p, u64p, ctypes.c_uint64, ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_void_p)]
+            L.s3h_plan_create_ex.argtypes = [ctypes.c_int, ctypes.c_int, u64p, u64p,
+                                             ctypes.c_uint64, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_void_p)]
+            L.s3h_plan_algo.argtypes = [ctypes.c_void_p]
             L.s3h_plan_destroy.argtypes = [ctypes.c_void_p]
             L.s3h_plan_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p]
@@ -74,9 +86,12 @@ def lib() -> ctypes.CDLL:
                                         ctypes.POINTER(ctypes.c_int), u32p]
             L.s3h_sha256_batch_device.argtypes = [ctypes.c_int, ctypes.c_void_p, u64p, u64p,
                                                   ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
-            L.s3h_sha256_batch_host.argtypes = [ctypes.POINTER(ctypes.c_void_p), u64p,
-                                                ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
-                                                ctypes.c_uint64]
+            for name in ("s3h_sha256_batch_host", "s3h_md5_batch_host"):
+                getattr(L, name).argtypes = [ctypes.POINTER(ctypes.c_void_p), u64p,
+                                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
+                                             ctypes.c_uint64]
+            L.s3h_md5_batch_device.argtypes = [ctypes.c_int, ctypes.c_void_p, u64p, u64p,
+                                               ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
             L.s3h_generate_parts.argtypes = [ctypes.c_int, ctypes.c_void_p, u64p, u64p, u64p,
                                              ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
             L.s3h_cpu_sha256.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
@@ -87,6 +102,8 @@ def lib() -> ctypes.CDLL:
             L.s3h_hash_to_text.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
             L.s3h_hash_to_text.restype = None
             L.s3h_cpu_backend.restype = ctypes.c_char_p
+            L.s3h_cpu_md5.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+            L.s3h_cpu_md5.restype = None
             _lib = L
     return _lib
 

@@ -64,6 +64,7 @@ struct DeviceGuard {  // restores the calling thread's current device
 
 struct s3h_plan_s {
   int device = 0;
+  int algo = S3H_ALGO_SHA256;
   int kernel = S3H_KERNEL_PC;
   uint64_t n = 0;
   uint64_t total_blocks = 0;
@@ -84,13 +85,23 @@ constexpr uint64_t kPairMaxParts = 32768;
 constexpr uint64_t kPcMaxParts = 65536;
 constexpr uint64_t kMaxParts = 1ull << 31;
 
-int plan_build(int device, const uint64_t* offsets, const uint64_t* lengths, uint64_t n,
+uint32_t digest_words(int algo) { return algo == S3H_ALGO_MD5 ? 4u : 8u; }
+
+int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* lengths, uint64_t n,
                int kernel, s3h_plan_s** out) {
   *out = nullptr;
+  if (algo != S3H_ALGO_SHA256 && algo != S3H_ALGO_MD5)
+    return fail(S3H_EINVAL, "plan: unknown algorithm %d", algo);
   if (!offsets || !lengths || n == 0 || n > kMaxParts)
     return fail(S3H_EINVAL, "plan: need offsets, lengths and 0 < n <= 2^31 (n=%llu)",
                 (unsigned long long)n);
   if (int rc = check_device(device)) return rc;
+  if (algo == S3H_ALGO_MD5) {
+    // MD5 has one kernel (producer/consumer, 4 VALU per step on the chain)
+    if (kernel != S3H_KERNEL_AUTO && kernel != S3H_KERNEL_PC)
+      return fail(S3H_EINVAL, "plan: MD5 supports only the producer/consumer kernel");
+    kernel = S3H_KERNEL_PC;
+  }
   if (kernel == S3H_KERNEL_AUTO)
     kernel = n <= kPairMaxParts ? S3H_KERNEL_PAIR : n <= kPcMaxParts ? S3H_KERNEL_PC : S3H_KERNEL_LANE;
   if (kernel != S3H_KERNEL_PC && kernel != S3H_KERNEL_LANE && kernel != S3H_KERNEL_PAIR)
@@ -110,6 +121,7 @@ int plan_build(int device, const uint64_t* offsets, const uint64_t* lengths, uin
 
   auto* P = new s3h_plan_s();
   P->device = device;
+  P->algo = algo;
   P->kernel = kernel;
   P->n = n;
   P->total_blocks = total;
@@ -149,7 +161,9 @@ int plan_launch(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint64_t
   A.blk_end = b1;
   A.blk_origin = origin;
   A.n = uint32_t(P->n);
-  if (P->kernel == S3H_KERNEL_PC)
+  if (P->algo == S3H_ALGO_MD5)
+    hipLaunchKernelGGL(s3h::md5_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_PC)
     hipLaunchKernelGGL(s3h::sha256_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_PAIR)
     hipLaunchKernelGGL(s3h::sha256_pair_kernel, dim3(P->grid), dim3(s3h::kPairThreads), 0, stream, A);
@@ -165,8 +179,9 @@ struct HostShard {
   std::vector<uint64_t> parts;  // global part indices on this device
 };
 
-int run_host_shard(const HostShard& sh, const uint8_t* const* parts, const uint64_t* lengths,
-                   uint32_t* digests, uint64_t slice) {
+int run_host_shard(const HostShard& sh, int algo, const uint8_t* const* parts,
+                   const uint64_t* lengths, uint32_t* digests, uint64_t slice) {
+  const uint32_t dw = digest_words(algo);
   const uint64_t n = sh.parts.size();
   if (n == 0) return S3H_OK;
   DeviceGuard g(sh.device);
@@ -189,7 +204,7 @@ int run_host_shard(const HostShard& sh, const uint8_t* const* parts, const uint6
   if (3 * n * slice > budget) slice = std::max<uint64_t>(64, budget / (3 * n) / 64 * 64);
   for (uint64_t j = 0; j < n; ++j) offs[j] = j * slice;
   s3h_plan_s* P = nullptr;
-  if (int rc = plan_build(sh.device, offs.data(), lens.data(), n, S3H_KERNEL_AUTO, &P)) return rc;
+  if (int rc = plan_build(sh.device, algo, offs.data(), lens.data(), n, S3H_KERNEL_AUTO, &P)) return rc;
   struct Cleanup {
     s3h_plan_s* P;
     ~Cleanup() { s3h_plan_destroy(P); }
@@ -205,7 +220,7 @@ int run_host_shard(const HostShard& sh, const uint8_t* const* parts, const uint6
     void* p;
     ~Free() { (void)hipFree(p); }
   } f1{ring};
-  HIP_TRY(hipMalloc(&d_dig, n * 8 * sizeof(uint32_t)));
+  HIP_TRY(hipMalloc(&d_dig, n * dw * sizeof(uint32_t)));
   Free f2{d_dig};
   HIP_TRY(hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&hash_s, hipStreamNonBlocking));
@@ -251,9 +266,9 @@ int run_host_shard(const HostShard& sh, const uint8_t* const* parts, const uint6
     e = hipEventRecord(hashed[r], hash_s);
     if (e != hipSuccess) { rc = fail(S3H_EHIP, "event: %s", hipGetErrorString(e)); break; }
   }
-  std::vector<uint32_t> local(n * 8);
+  std::vector<uint32_t> local(n * dw);
   if (rc == S3H_OK) {
-    hipError_t e = hipMemcpyAsync(local.data(), d_dig, n * 32, hipMemcpyDeviceToHost, hash_s);
+    hipError_t e = hipMemcpyAsync(local.data(), d_dig, n * dw * 4, hipMemcpyDeviceToHost, hash_s);
     if (e == hipSuccess) e = hipStreamSynchronize(hash_s);
     if (e != hipSuccess) rc = fail(S3H_EHIP, "D2H digests: %s", hipGetErrorString(e));
   }
@@ -266,7 +281,8 @@ int run_host_shard(const HostShard& sh, const uint8_t* const* parts, const uint6
   (void)hipStreamDestroy(copy_s);
   (void)hipStreamDestroy(hash_s);
   if (rc == S3H_OK)
-    for (uint64_t j = 0; j < n; ++j) std::memcpy(digests + 8 * sh.parts[j], &local[8 * j], 32);
+    for (uint64_t j = 0; j < n; ++j)
+      std::memcpy(digests + dw * sh.parts[j], &local[dw * j], dw * 4);
   return rc;
 }
 
@@ -289,8 +305,16 @@ int s3h_device_count(int* count) {
 int s3h_plan_create(int device, const uint64_t* offsets, const uint64_t* lengths, uint64_t n,
                     int kernel, s3h_plan_t* plan) {
   if (!plan) return fail(S3H_EINVAL, "null plan out-pointer");
-  return plan_build(device, offsets, lengths, n, kernel, plan);
+  return plan_build(device, S3H_ALGO_SHA256, offsets, lengths, n, kernel, plan);
 }
+
+int s3h_plan_create_ex(int device, int algo, const uint64_t* offsets, const uint64_t* lengths,
+                       uint64_t n, int kernel, s3h_plan_t* plan) {
+  if (!plan) return fail(S3H_EINVAL, "null plan out-pointer");
+  return plan_build(device, algo, offsets, lengths, n, kernel, plan);
+}
+
+int s3h_plan_algo(s3h_plan_t P) { return P ? P->algo : S3H_EINVAL; }
 
 int s3h_plan_destroy(s3h_plan_t P) {
   if (!P) return S3H_OK;
@@ -326,11 +350,10 @@ int s3h_plan_info(s3h_plan_t P, uint64_t* n, uint64_t* total_blocks, uint64_t* m
   return S3H_OK;
 }
 
-int s3h_sha256_batch_device(int device, const void* d_base, const uint64_t* offsets,
-                            const uint64_t* lengths, uint64_t n, uint32_t* d_digests,
-                            void* stream) {
+static int batch_device(int device, int algo, const void* d_base, const uint64_t* offsets,
+                        const uint64_t* lengths, uint64_t n, uint32_t* d_digests, void* stream) {
   s3h_plan_s* P = nullptr;
-  if (int rc = plan_build(device, offsets, lengths, n, S3H_KERNEL_AUTO, &P)) return rc;
+  if (int rc = plan_build(device, algo, offsets, lengths, n, S3H_KERNEL_AUTO, &P)) return rc;
   int rc = plan_launch(P, d_base, d_digests, 0, P->max_blocks, 0, static_cast<hipStream_t>(stream), false);
   if (rc == S3H_OK) {
     DeviceGuard g(device);
@@ -341,8 +364,19 @@ int s3h_sha256_batch_device(int device, const void* d_base, const uint64_t* offs
   return rc;
 }
 
-int s3h_sha256_batch_host(const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
-                          uint32_t* digests, int ndevices, uint64_t slice_bytes) {
+int s3h_sha256_batch_device(int device, const void* d_base, const uint64_t* offsets,
+                            const uint64_t* lengths, uint64_t n, uint32_t* d_digests,
+                            void* stream) {
+  return batch_device(device, S3H_ALGO_SHA256, d_base, offsets, lengths, n, d_digests, stream);
+}
+
+int s3h_md5_batch_device(int device, const void* d_base, const uint64_t* offsets,
+                         const uint64_t* lengths, uint64_t n, uint32_t* d_digests, void* stream) {
+  return batch_device(device, S3H_ALGO_MD5, d_base, offsets, lengths, n, d_digests, stream);
+}
+
+static int batch_host(int algo, const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
+                      uint32_t* digests, int ndevices, uint64_t slice_bytes) {
   if (!parts || !lengths || !digests || n == 0) return fail(S3H_EINVAL, "batch_host: bad arguments");
   int count = 0;
   if (int rc = s3h_device_count(&count)) return rc;
@@ -358,13 +392,23 @@ int s3h_sha256_batch_host(const uint8_t* const* parts, const uint64_t* lengths, 
   std::vector<std::thread> pool;
   for (int d = 0; d < ndevices; ++d)
     pool.emplace_back([&, d] {
-      rcs[d] = run_host_shard(shards[d], parts, lengths, digests, slice_bytes);
+      rcs[d] = run_host_shard(shards[d], algo, parts, lengths, digests, slice_bytes);
       if (rcs[d]) errs[d] = g_err;
     });
   for (auto& t : pool) t.join();
   for (int d = 0; d < ndevices; ++d)
     if (rcs[d]) return fail(rcs[d], "device %d: %s", d, errs[d].c_str());
   return S3H_OK;
+}
+
+int s3h_sha256_batch_host(const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
+                          uint32_t* digests, int ndevices, uint64_t slice_bytes) {
+  return batch_host(S3H_ALGO_SHA256, parts, lengths, n, digests, ndevices, slice_bytes);
+}
+
+int s3h_md5_batch_host(const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
+                       uint32_t* digests, int ndevices, uint64_t slice_bytes) {
+  return batch_host(S3H_ALGO_MD5, parts, lengths, n, digests, ndevices, slice_bytes);
 }
 
 int s3h_generate_parts(int device, void* d_base, const uint64_t* offsets, const uint64_t* lengths,

@@ -358,6 +358,190 @@ __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A)
   }
 }
 
+// ------------------------------------------------------------- MD5 (producer/consumer)
+// Batched MD5 for Content-MD5 / multipart-ETag verification (reference
+// lib/hash/md5.cpp:71-116 for the step function, :158-172 for the padding).  Same
+// workgroup shape as sha256_pc_kernel: the producer decodes little-endian words (one v_perm
+// handles alignment), pads (64-bit LITTLE-endian bit length) and writes M[g(i)] + K[i] for
+// the 64 steps to LDS; the consumer runs the chain: per step one bitop3 (F/G/H/I), one add3,
+// one alignbit (rotate left) and one add.  State words are the digest words (no byte swap).
+__device__ __forceinline__ uint32_t le_selector(uint32_t sh) {
+  return ((sh + 3) << 24) | ((sh + 2) << 16) | ((sh + 1) << 8) | sh;
+}
+
+__device__ __forceinline__ void md5_tail(const uint8_t* p, uint64_t len, uint64_t blk,
+                                         uint32_t w[16]) {
+  const uint64_t nfull = len >> 6;
+  const int rem = (blk == nfull) ? int(len & 63) : -1;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = 4 * j + k;
+      uint32_t byte = 0;
+      if (i < rem) byte = p[i];
+      else if (i == rem) byte = 0x80u;
+      x |= byte << (8 * k);
+    }
+    w[j] = x;
+  }
+  if (blk == nblocks(len) - 1) {
+    const uint64_t bits = len << 3;
+    w[14] = uint32_t(bits);
+    w[15] = uint32_t(bits >> 32);
+  }
+}
+
+#define S3H_MD5_K(i) ((uint32_t)(                                                              \
+  (i)==0?0xd76aa478u:(i)==1?0xe8c7b756u:(i)==2?0x242070dbu:(i)==3?0xc1bdceeeu:(i)==4?0xf57c0fafu: \
+  (i)==5?0x4787c62au:(i)==6?0xa8304613u:(i)==7?0xfd469501u:(i)==8?0x698098d8u:(i)==9?0x8b44f7afu: \
+  (i)==10?0xffff5bb1u:(i)==11?0x895cd7beu:(i)==12?0x6b901122u:(i)==13?0xfd987193u:              \
+  (i)==14?0xa679438eu:(i)==15?0x49b40821u:(i)==16?0xf61e2562u:(i)==17?0xc040b340u:              \
+  (i)==18?0x265e5a51u:(i)==19?0xe9b6c7aau:(i)==20?0xd62f105du:(i)==21?0x02441453u:              \
+  (i)==22?0xd8a1e681u:(i)==23?0xe7d3fbc8u:(i)==24?0x21e1cde6u:(i)==25?0xc33707d6u:              \
+  (i)==26?0xf4d50d87u:(i)==27?0x455a14edu:(i)==28?0xa9e3e905u:(i)==29?0xfcefa3f8u:              \
+  (i)==30?0x676f02d9u:(i)==31?0x8d2a4c8au:(i)==32?0xfffa3942u:(i)==33?0x8771f681u:              \
+  (i)==34?0x6d9d6122u:(i)==35?0xfde5380cu:(i)==36?0xa4beea44u:(i)==37?0x4bdecfa9u:              \
+  (i)==38?0xf6bb4b60u:(i)==39?0xbebfbc70u:(i)==40?0x289b7ec6u:(i)==41?0xeaa127fau:              \
+  (i)==42?0xd4ef3085u:(i)==43?0x04881d05u:(i)==44?0xd9d4d039u:(i)==45?0xe6db99e5u:              \
+  (i)==46?0x1fa27cf8u:(i)==47?0xc4ac5665u:(i)==48?0xf4292244u:(i)==49?0x432aff97u:              \
+  (i)==50?0xab9423a7u:(i)==51?0xfc93a039u:(i)==52?0x655b59c3u:(i)==53?0x8f0ccc92u:              \
+  (i)==54?0xffeff47du:(i)==55?0x85845dd1u:(i)==56?0x6fa87e4fu:(i)==57?0xfe2ce6e0u:              \
+  (i)==58?0xa3014314u:(i)==59?0x4e0811a1u:(i)==60?0xf7537e82u:(i)==61?0xbd3af235u:              \
+  (i)==62?0x2ad7d2bbu:0xeb86d391u))
+
+__device__ __forceinline__ constexpr int md5_g(int i) {
+  return i < 16 ? i : i < 32 ? (5 * i + 1) & 15 : i < 48 ? (3 * i + 5) & 15 : (7 * i) & 15;
+}
+__device__ __forceinline__ constexpr int md5_s(int i) {
+  return i < 16 ? (i % 4 == 0 ? 7 : i % 4 == 1 ? 12 : i % 4 == 2 ? 17 : 22)
+       : i < 32 ? (i % 4 == 0 ? 5 : i % 4 == 1 ? 9 : i % 4 == 2 ? 14 : 20)
+       : i < 48 ? (i % 4 == 0 ? 4 : i % 4 == 1 ? 11 : i % 4 == 2 ? 16 : 23)
+                : (i % 4 == 0 ? 6 : i % 4 == 1 ? 10 : i % 4 == 2 ? 15 : 21);
+}
+
+// F, G, H, I as single v_bitop3_b32 (truth table index = b<<2 | c<<1 | d): F = b?c:d (0xCA),
+// G = d?b:c (0xE4), H = b^c^d (0x96), I = c^(b|~d) (0x39).  Written as builtins because the
+// compiler otherwise splits F/G into disjoint and+add terms (one extra VALU per step).
+template <int I>
+__device__ __forceinline__ uint32_t md5_f(uint32_t b, uint32_t c, uint32_t d) {
+  if constexpr (I < 16) return __builtin_amdgcn_bitop3_b32(b, c, d, 0xCA);
+  else if constexpr (I < 32) return __builtin_amdgcn_bitop3_b32(b, c, d, 0xE4);
+  else if constexpr (I < 48) return __builtin_amdgcn_bitop3_b32(b, c, d, 0x96);
+  else return __builtin_amdgcn_bitop3_b32(b, c, d, 0x39);
+}
+
+// One MD5 step in rotating names: the new b lands in `a` (a is dead after the add3).
+template <int I>
+__device__ __forceinline__ void md5_step(uint32_t& a, uint32_t b, uint32_t c, uint32_t d,
+                                         uint32_t km) {
+  const uint32_t t = a + md5_f<I>(b, c, d) + km;
+  a = b + __builtin_amdgcn_alignbit(t, t, 32 - md5_s(I));
+}
+
+template <int I>
+__device__ __forceinline__ void md5_steps(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d,
+                                          const uint32_t km[64]) {
+  if constexpr (I < 64) {
+    md5_step<I>(a, b, c, d, km[I]);      // (a,b,c,d) -> (d, a', b, c)
+    md5_steps<I + 1>(d, a, b, c, km);
+  }
+}
+
+__device__ __forceinline__ void md5_produce(const RawBlock& r, uint32_t sel, const uint8_t* bp,
+                                            uint64_t len, uint64_t blk, uint64_t limit,
+                                            uint4 (*buf)[64], uint32_t lane) {
+  uint32_t w[16];
+  if (blk >= limit) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = 0;
+  } else if (blk < (len >> 6)) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_perm(r.d[j + 1], r.d[j], sel);
+  } else {
+    md5_tail(bp, len, blk, w);
+  }
+  uint32_t km[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) km[i] = w[md5_g(i)] + S3H_MD5_K(i);
+#pragma unroll
+  for (int q = 0; q < 16; ++q)
+    buf[q][lane] = make_uint4(km[4 * q], km[4 * q + 1], km[4 * q + 2], km[4 * q + 3]);
+}
+
+__global__ __launch_bounds__(kPcThreads) void md5_pc_kernel(LaunchArgs A) {
+  __shared__ uint4 lds_km[2][16][64];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t slot0 = blockIdx.x * 64u;
+  const uint32_t slot = slot0 + lane;
+  const bool valid = slot < A.n;
+  Slot s = {0, 0};
+  if (valid) s = A.slots[slot];
+  const uint64_t nb = valid ? nblocks(s.len) : 0;
+  const uint64_t wg_nb = nblocks(A.slots[slot0].len);
+  const uint64_t wg_end = wg_nb < A.blk_end ? wg_nb : A.blk_end;
+  if (wg_end <= A.blk_begin) return;
+  const uint64_t iters = wg_end - A.blk_begin;
+
+  if (wave == 1) {
+    const uint64_t b0 = A.blk_begin;
+    const uint8_t* p = A.base + s.off + 64ull * (b0 - A.blk_origin);
+    const uint32_t sel = le_selector(uint32_t(reinterpret_cast<uintptr_t>(p) & 3));
+    const uint64_t fend = fetch_end(s.len, A.blk_end);
+    RawBlock ra, rb;
+    if (b0 < fend) fetch_full(p, ra);
+    if (b0 + 1 < fend) fetch_full(p + 64, rb);
+    md5_produce(ra, sel, p, s.len, b0, A.blk_end, lds_km[0], lane);
+    __syncthreads();
+    for (uint64_t k = 1; k <= iters; k += 2) {
+      if (k < iters) {
+        if (b0 + k + 1 < fend) fetch_full(p + 64 * (k + 1), ra);
+        md5_produce(rb, sel, p + 64 * k, s.len, b0 + k, A.blk_end, lds_km[1], lane);
+      }
+      __syncthreads();
+      if (k + 1 > iters) break;
+      if (k + 1 < iters) {
+        if (b0 + k + 2 < fend) fetch_full(p + 64 * (k + 2), rb);
+        md5_produce(ra, sel, p + 64 * (k + 1), s.len, b0 + k + 1, A.blk_end, lds_km[0], lane);
+      }
+      __syncthreads();
+    }
+  } else {
+    __builtin_amdgcn_s_setprio(3);
+    uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    if (valid && A.blk_begin > 0 && A.state) {
+      const uint4 v = reinterpret_cast<const uint4*>(A.state + 8ull * slot)[0];
+      st[0] = v.x; st[1] = v.y; st[2] = v.z; st[3] = v.w;
+    }
+    __syncthreads();
+    for (uint64_t i = 0; i < iters; ++i) {
+      uint32_t km[64];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const uint4 v = lds_km[i & 1][q][lane];
+        km[4 * q] = v.x; km[4 * q + 1] = v.y; km[4 * q + 2] = v.z; km[4 * q + 3] = v.w;
+      }
+      uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+      md5_steps<0>(a, b, c, d, km);
+      const bool live = (A.blk_begin + i) < nb;
+      st[0] = live ? st[0] + a : st[0];
+      st[1] = live ? st[1] + b : st[1];
+      st[2] = live ? st[2] + c : st[2];
+      st[3] = live ? st[3] + d : st[3];
+      __syncthreads();
+    }
+    if (valid && nb > A.blk_begin) {
+      if (nb <= A.blk_end)
+        reinterpret_cast<uint4*>(A.digests + 4ull * A.out_idx[slot])[0] =
+            make_uint4(st[0], st[1], st[2], st[3]);
+      else if (A.state)
+        reinterpret_cast<uint4*>(A.state + 8ull * slot)[0] = make_uint4(st[0], st[1], st[2], st[3]);
+    }
+  }
+}
+
 // ------------------------------------------------------------- synthetic input generator
 // G(seed, p, L) of SURVEY.md 8(d): word j of part p is splitmix64(x0 + (j+1)*golden),
 // x0 = seed ^ p*0xD1B54A32D192ED03, serialised little-endian.  Parts must start 8-B aligned.

@@ -55,16 +55,18 @@ class Plan:
     """Geometry of one batch of parts, uploaded once (s3h_plan_create)."""
 
     def __init__(self, offsets: Sequence[int], lengths: Sequence[int], device: int = 0,
-                 kernel: str | int = "auto"):
+                 kernel: str | int = "auto", algo: str = "sha256"):
         k = kernel if isinstance(kernel, int) else _native.KERNEL_IDS[kernel]
+        self.algo = _native.ALGO_IDS[algo]
+        self.words = _native.DIGEST_WORDS[self.algo]
         self.offsets, self.lengths = _u64(offsets), _u64(lengths)
         if self.offsets.shape != self.lengths.shape or self.offsets.ndim != 1:
             raise ValueError("offsets and lengths must be 1-D and of equal length")
         self.n = int(self.lengths.size)
         self.device = device
         h = ctypes.c_void_p()
-        check(lib().s3h_plan_create(device, _p64(self.offsets), _p64(self.lengths), self.n, k,
-                                    ctypes.byref(h)))
+        check(lib().s3h_plan_create_ex(device, self.algo, _p64(self.offsets), _p64(self.lengths),
+                                       self.n, k, ctypes.byref(h)))
         self._h = h
 
     def info(self) -> dict:
@@ -79,8 +81,8 @@ class Plan:
         import torch
         if not (data.is_cuda and digests.is_cuda):
             raise ValueError("data and digests must be device tensors")
-        if digests.numel() * digests.element_size() < 32 * self.n:
-            raise ValueError("digests buffer too small (need n*32 bytes)")
+        if digests.numel() * digests.element_size() < 4 * self.words * self.n:
+            raise ValueError(f"digests buffer too small (need n*{4 * self.words} bytes)")
         end = int((self.offsets + self.lengths).max()) if self.n else 0
         if data.numel() * data.element_size() < end:
             raise ValueError(f"data buffer ({data.numel() * data.element_size()} B) smaller "
@@ -120,30 +122,51 @@ class Plan:
 
 
 def sha256_batch_device(data, offsets, lengths, device: int | None = None, kernel="auto",
-                        stream=None):
+                        stream=None, algo: str = "sha256"):
     """Digest every part [offsets[i], offsets[i]+lengths[i]) of the device tensor ``data``.
 
-    Returns an (n, 8) int32 device tensor holding the uint32 digest words (lib/hash layout)."""
+    Returns an (n, 8) int32 device tensor holding the uint32 digest words (lib/hash layout);
+    (n, 4) for algo="md5"."""
     import torch
     dev = data.device.index if device is None else device
-    with Plan(offsets, lengths, device=dev, kernel=kernel) as plan:
-        out = torch.empty((plan.n, DIGEST_WORDS), dtype=torch.int32, device=data.device)
+    with Plan(offsets, lengths, device=dev, kernel=kernel, algo=algo) as plan:
+        out = torch.empty((plan.n, plan.words), dtype=torch.int32, device=data.device)
         plan.launch(data, out, stream)
         torch.cuda.current_stream(data.device).synchronize() if stream is None else stream.synchronize()
     return out
 
 
-def sha256_batch_host(parts: Sequence, ndevices: int = 0, slice_bytes: int = 0) -> np.ndarray:
-    """Digest host-resident parts (bytes / numpy uint8 arrays) on the GPUs: (n, 8) uint32."""
+def md5_batch_device(data, offsets, lengths, device: int | None = None, stream=None):
+    """Batched MD5 of device-resident parts: (n, 4) int32 device tensor (LE digest words)."""
+    return sha256_batch_device(data, offsets, lengths, device, "auto", stream, algo="md5")
+
+
+def _host_batch(fn, words, parts, ndevices, slice_bytes):
     arrs = [np.frombuffer(p, dtype=np.uint8) if isinstance(p, (bytes, bytearray, memoryview))
             else np.ascontiguousarray(p, dtype=np.uint8).reshape(-1) for p in parts]
     n = len(arrs)
     ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data if a.size else 0 for a in arrs])
     lens = _u64([a.size for a in arrs])
-    out = np.zeros((n, DIGEST_WORDS), dtype=np.uint32)
-    check(lib().s3h_sha256_batch_host(ptrs, _p64(lens), n, out.ctypes.data, ndevices,
-                                      slice_bytes))
+    out = np.zeros((n, words), dtype=np.uint32)
+    check(fn(ptrs, _p64(lens), n, out.ctypes.data, ndevices, slice_bytes))
     return out
+
+
+def md5_batch_host(parts: Sequence, ndevices: int = 0, slice_bytes: int = 0) -> np.ndarray:
+    """Batched MD5 of host-resident parts on the GPUs: (n, 4) uint32."""
+    return _host_batch(lib().s3h_md5_batch_host, 4, parts, ndevices, slice_bytes)
+
+
+def multipart_etag(part_md5s) -> str:
+    """S3 multipart ETag: hex(MD5(concatenated binary part MD5s)) + "-" + part count."""
+    import hashlib
+    w = np.ascontiguousarray(part_md5s, dtype=np.uint32).reshape(-1, 4)
+    return hashlib.md5(w.tobytes()).hexdigest() + f"-{w.shape[0]}"
+
+
+def sha256_batch_host(parts: Sequence, ndevices: int = 0, slice_bytes: int = 0) -> np.ndarray:
+    """Digest host-resident parts (bytes / numpy uint8 arrays) on the GPUs: (n, 8) uint32."""
+    return _host_batch(lib().s3h_sha256_batch_host, DIGEST_WORDS, parts, ndevices, slice_bytes)
 
 
 def generate_parts(data, offsets, lengths, part_ids, seed: int, stream=None) -> None:
@@ -166,6 +189,14 @@ def sha256(data: bytes) -> np.ndarray:
     return out
 
 
+def md5(data: bytes) -> np.ndarray:
+    """lib/hash md5 drop-in (CPU, single message, padded): 4 words, LE digest bytes."""
+    b = bytes(data)
+    out = np.zeros(4, dtype=np.uint32)
+    lib().s3h_cpu_md5(b, len(b), out.ctypes.data)
+    return out
+
+
 def hmac256(data: bytes, key: bytes) -> bytes:
     out = ctypes.create_string_buffer(32)
     d, k = bytes(data), bytes(key)
@@ -174,12 +205,12 @@ def hmac256(data: bytes, key: bytes) -> bytes:
 
 
 def hash_to_text(words) -> str:
-    """sha256::hash_to_text: lowercase hex of the 32 digest bytes as laid out in memory."""
-    return np.ascontiguousarray(words, dtype=np.uint32).reshape(8).tobytes().hex()
+    """sha256::hash_to_text / md5::hash_to_text: lowercase hex of the digest bytes in memory."""
+    return np.ascontiguousarray(words, dtype=np.uint32).reshape(-1).tobytes().hex()
 
 
-def digests_to_text(words) -> list[str]:
-    w = np.ascontiguousarray(words).view(np.uint32).reshape(-1, DIGEST_WORDS)
+def digests_to_text(words, nwords: int = DIGEST_WORDS) -> list[str]:
+    w = np.ascontiguousarray(words).view(np.uint32).reshape(-1, nwords)
     return [row.tobytes().hex() for row in w]
 
 

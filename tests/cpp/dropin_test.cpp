@@ -8,6 +8,7 @@
 #include <string>
 #include <vector>
 
+#include "md5.h"
 #include "s3hash_batch.hpp"
 #include "sha256.h"
 
@@ -90,6 +91,29 @@ int main(int argc, char** argv) {
     char t[65];
     for (int i = 0; i < 32; ++i) std::snprintf(t + 2 * i, 3, "%02x", mac[i]);
     report("hmac256 rfc4231", std::string(t) == "5bdcc146bf60754e6a042426089575c75a003f089d2739839dec58b964ec3843");
+  }
+  // md5 drop-in (lib/hash/md5.h): RFC 1321 test suite values, md5_file == md5
+  {
+    auto m = [](const std::string& x) {
+      uint32_t h[4];
+      md5::md5(reinterpret_cast<const uint8_t*>(x.data()), x.size(), h);
+      char t[33];
+      md5::hash_to_text(h, t);
+      return std::string(t);
+    };
+    report("md5 rfc1321", m("") == "d41d8cd98f00b204e9800998ecf8427e" &&
+                              m("abc") == "900150983cd24fb0d6963f7d28e17f72" &&
+                              m("message digest") == "f96b697d7cb7938d525a2f31aaf161d0");
+    std::vector<uint8_t> v(1000003);
+    for (size_t i = 0; i < v.size(); ++i) v[i] = uint8_t(i * 13 + 1);
+    FILE* f = std::fopen("/tmp/s3h_md5_dropin", "wb");
+    std::fwrite(v.data(), 1, v.size(), f);
+    std::fclose(f);
+    uint32_t a[4], b[4];
+    md5::md5_file("/tmp/s3h_md5_dropin", a);
+    md5::md5(v.data(), v.size(), b);
+    std::remove("/tmp/s3h_md5_dropin");
+    report("md5_file", std::memcmp(a, b, 16) == 0);
   }
   // utility.h helpers
   report("utility", to_big_endian(0x0102030405060708ull) == 0x0807060504030201ull &&

@@ -29,7 +29,23 @@ def load_ref():
     lib.ref_hmac256.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                 ctypes.c_uint64, ctypes.c_void_p]
     lib.ref_sha256_stream.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+    lib.ref_md5_stream.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+    lib.ref_md5_file.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
     return lib
+
+
+def ref_md5(ref, buf: bytes) -> str:
+    """MD5 via the reference's md5_file (md5.cpp:132-180; the only padded MD5 entry point)."""
+    import tempfile
+    with tempfile.NamedTemporaryFile(delete=False) as f:
+        f.write(buf)
+        path = f.name
+    out = (ctypes.c_uint32 * 4)()
+    ref.ref_md5_file(path.encode(), out)
+    os.unlink(path)
+    got = bytes(out).hex()
+    assert got == hashlib.md5(buf).hexdigest(), (len(buf), got)
+    return got
 
 
 def load_oracle():
@@ -163,6 +179,29 @@ def main():
         ref.ref_sha256_stream(h, ctypes.create_string_buffer(buf, L or 1), L)
         st.append({"p": 7, "L": L, "state": [int(x) for x in h]})
     out["stream"] = st
+
+    # 9. MD5 (lib/hash/md5.cpp, SURVEY 8(f) "next"): md5_file digests (empty files make the
+    #    reference exit, so L >= 1), md5_stream whole-block states, C2/transfer parts, ETag
+    md = {"edge": [], "stream": [], "c2_parts": [], "transfer": []}
+    for L in [1, 3, 55, 56, 57, 63, 64, 65, 119, 120, 128, 1000, 4096, 65536, (1 << 20) + 13,
+              (16 << 20), (16 << 20) + 1]:
+        md["edge"].append({"p": 7, "L": L, "digest": ref_md5(ref, big[:L] if L <= len(big)
+                                                             else gen(orc, 7, L))})
+    for L in (0, 64, 128, 640, 4096):
+        h = (ctypes.c_uint32 * 4)(0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476)
+        ref.ref_md5_stream(h, ctypes.create_string_buffer(big[:L], L or 1), L)
+        md["stream"].append({"p": 7, "L": L, "state": [int(x) for x in h]})
+    for p in (0, 1, 1023):
+        md["c2_parts"].append({"p": p, "L": L8, "digest": ref_md5(ref, gen(orc, p, L8))})
+    size = 38000007
+    tdata = (np.arange(size, dtype=np.uint64) % 128).astype(np.uint8).tobytes()
+    for prt in out["transfer"]["parts"]:
+        o, n_ = prt["offset"], prt["size"]
+        md["transfer"].append({"offset": o, "size": n_, "digest": ref_md5(ref, tdata[o:o + n_])})
+    # S3 multipart ETag: hex(MD5(concat(binary part MD5s))) + "-" + part count
+    cat = b"".join(bytes.fromhex(x["digest"]) for x in md["transfer"])
+    md["transfer_etag"] = hashlib.md5(cat).hexdigest() + "-%d" % len(md["transfer"])
+    out["md5"] = md
 
     path = os.path.join(HERE, "sha256_golden.json")
     with open(path, "w") as f:

@@ -35,7 +35,31 @@ class Oracle:
         L.oracle_c3_length.restype = ctypes.c_uint64
         L.oracle_sha256_batch.argtypes = [ctypes.c_void_p, u64p, u64p, ctypes.c_uint64,
                                           ctypes.c_void_p, ctypes.c_int]
+        L.oracle_md5.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+        L.oracle_md5_stream.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+        L.oracle_md5_batch.argtypes = [ctypes.c_void_p, u64p, u64p, ctypes.c_uint64,
+                                       ctypes.c_void_p, ctypes.c_int]
         self.L = L
+
+    def md5(self, data: bytes) -> np.ndarray:
+        out = np.zeros(4, dtype=np.uint32)
+        b = bytes(data)
+        self.L.oracle_md5(b, len(b), out.ctypes.data)
+        return out
+
+    def md5_stream(self, state, data: bytes) -> np.ndarray:
+        st = np.array(state, dtype=np.uint32)
+        b = bytes(data)
+        self.L.oracle_md5_stream(st.ctypes.data, b, len(b))
+        return st
+
+    def md5_batch(self, base: np.ndarray, offsets, lengths, threads: int = 8) -> np.ndarray:
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(lengths, dtype=np.uint64)
+        out = np.zeros((offs.size, 4), dtype=np.uint32)
+        self.L.oracle_md5_batch(base.ctypes.data, offs.ctypes.data_as(u64p),
+                                lens.ctypes.data_as(u64p), offs.size, out.ctypes.data, threads)
+        return out
 
     def sha256(self, data: bytes) -> np.ndarray:
         out = np.zeros(8, dtype=np.uint32)

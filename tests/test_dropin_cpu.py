@@ -80,3 +80,17 @@ def test_gpu_entry_points_fail_loudly_without_device():
     assert ei.value.code in (_native.S3H_ENODEV, _native.S3H_EHIP)
     with pytest.raises(s3.S3HashError):
         s3.sha256_batch_host([b"abc"])
+
+
+def test_cpu_md5_golden(golden, oracle):
+    import hashlib
+    md = golden["md5"]
+    big = oracle.generate(7, max(e["L"] for e in md["edge"]))
+    for e in md["edge"]:
+        assert s3.hash_to_text(s3.md5(big[:e["L"]])) == e["digest"], e["L"]
+    assert s3.hash_to_text(s3.md5(b"")) == hashlib.md5(b"").hexdigest()
+
+
+def test_multipart_etag_golden(golden):
+    words = [np.frombuffer(bytes.fromhex(p["digest"]), dtype=np.uint32) for p in golden["md5"]["transfer"]]
+    assert s3.multipart_etag(np.stack(words)) == golden["md5"]["transfer_etag"]

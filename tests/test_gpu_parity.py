@@ -204,3 +204,49 @@ def test_host_path_uniform_stride_2d_copies(torch_cuda, oracle):
     want = oracle.batch(buf, np.arange(n) * stride, np.full(n, L))
     for sl in (64 << 10, 256 << 10, 0):
         assert np.array_equal(s3.sha256_batch_host(views, slice_bytes=sl), want), sl
+
+
+# ------------------------------------------------------------------ MD5
+def test_md5_edges_all_alignments(torch_cuda, oracle, golden):
+    md = golden["md5"]
+    edges = [e for e in md["edge"] if e["L"] <= (1 << 20) + 13]
+    big = np.frombuffer(oracle.generate(7, max(e["L"] for e in edges)), dtype=np.uint8)
+    offs, lens, want, chunks, pos = [], [], [], [], 0
+    for mis in (0, 1, 2, 3, 13):
+        for e in edges:
+            pos += (-pos) % 64 + mis
+            offs.append(pos); lens.append(e["L"]); want.append(e["digest"])
+            chunks.append((pos, big[:e["L"]]))
+            pos += e["L"]
+    host = np.zeros(pos + 64, dtype=np.uint8)
+    for o, c in chunks:
+        host[o:o + c.size] = c
+    data = _dev_buffer(torch_cuda, host)
+    got = s3.digests_to_text(s3.md5_batch_device(data, offs, lens).cpu().numpy(), 4)
+    assert got == want
+
+
+def test_md5_c2_and_ragged_vs_oracle(torch_cuda, oracle, golden):
+    data, offs, lens = _c2(torch_cuda, 1024)
+    out = s3.md5_batch_device(data, offs, lens).cpu().numpy().view(np.uint32)
+    txt = s3.digests_to_text(out, 4)
+    for e in golden["md5"]["c2_parts"]:
+        assert txt[e["p"]] == e["digest"], e["p"]
+    assert np.array_equal(out, oracle.md5_batch(data.cpu().numpy(), offs, lens, threads=16))
+    rng = np.random.default_rng(21)
+    n = 500
+    rl = rng.integers(0, 30000, n)
+    ro = np.cumsum(rng.integers(0, 50, n) + np.concatenate([[0], rl[:-1]]))
+    host = rng.integers(0, 256, int(ro[-1] + rl[-1]) + 8, dtype=np.uint8)
+    got = s3.md5_batch_device(_dev_buffer(torch_cuda, host), ro, rl).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, oracle.md5_batch(host, ro, rl))
+
+
+def test_md5_host_path_transfer_etag(torch_cuda, golden):
+    t = golden["transfer"]
+    data = (np.arange(t["size"], dtype=np.uint64) % 128).astype(np.uint8)
+    views = [data[p["offset"]:p["offset"] + p["size"]] for p in t["parts"]]
+    for sl in (0, 64 << 10):
+        d = s3.md5_batch_host(views, slice_bytes=sl)
+        assert s3.digests_to_text(d, 4) == [p["digest"] for p in golden["md5"]["transfer"]]
+        assert s3.multipart_etag(d) == golden["md5"]["transfer_etag"]

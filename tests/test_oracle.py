@@ -69,3 +69,17 @@ def test_batch_threads(oracle):
     for i in range(40):
         want = hashlib.sha256(base[offs[i]:offs[i] + lens[i]].tobytes()).digest()
         assert got[i].tobytes() == want
+
+
+def test_md5_oracle_golden(oracle, golden):
+    import hashlib
+    md = golden["md5"]
+    big = oracle.generate(7, max(e["L"] for e in md["edge"]))
+    for e in md["edge"]:
+        assert oracle.md5(big[:e["L"]]).tobytes().hex() == e["digest"], e["L"]
+    assert oracle.md5(b"").tobytes().hex() == hashlib.md5(b"").hexdigest()
+    iv = [0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476]
+    for s in md["stream"]:
+        assert list(oracle.md5_stream(iv, big[:s["L"]])) == s["state"], s["L"]
+    for e in md["c2_parts"][:1]:
+        assert oracle.md5(oracle.generate(e["p"], e["L"])).tobytes().hex() == e["digest"]
