@@ -73,6 +73,7 @@ struct s3h_plan_s {
   s3h::Slot* d_slots = nullptr;
   uint32_t* d_out_idx = nullptr;
   uint32_t* d_state = nullptr;  // n*8 chaining words, allocated on first ranged launch
+  uint8_t* d_zero = nullptr;    // 256 zero bytes: load target for out-of-range lanes
 };
 
 namespace {
@@ -133,11 +134,14 @@ int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* le
   DeviceGuard g(device);
   hipError_t e = hipMalloc(&P->d_slots, n * sizeof(s3h::Slot));
   if (e == hipSuccess) e = hipMalloc(&P->d_out_idx, n * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc(&P->d_zero, 256);
+  if (e == hipSuccess) e = hipMemset(P->d_zero, 0, 256);
   if (e == hipSuccess) e = hipMemcpy(P->d_slots, slots.data(), n * sizeof(s3h::Slot), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(P->d_out_idx, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     (void)hipFree(P->d_slots);
     (void)hipFree(P->d_out_idx);
+    (void)hipFree(P->d_zero);
     delete P;
     return fail(e == hipErrorOutOfMemory ? S3H_ENOMEM : S3H_EHIP, "plan upload: %s", hipGetErrorString(e));
   }
@@ -157,6 +161,7 @@ int plan_launch(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint64_t
   A.out_idx = P->d_out_idx;
   A.state = ranged ? P->d_state : nullptr;
   A.digests = d_digests;
+  A.zero = P->d_zero;
   A.blk_begin = b0;
   A.blk_end = b1;
   A.blk_origin = origin;
@@ -322,6 +327,7 @@ int s3h_plan_destroy(s3h_plan_t P) {
   (void)hipFree(P->d_slots);
   (void)hipFree(P->d_out_idx);
   (void)hipFree(P->d_state);
+  (void)hipFree(P->d_zero);
   delete P;
   return S3H_OK;
 }

@@ -102,17 +102,29 @@ __device__ __forceinline__ void schedule_wk(const uint32_t w16[16], uint32_t wk[
 // only touched when p is not dword aligned, so no dword without a part byte is read.
 struct RawBlock { uint32_t d[17]; };
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+// Explicit global (address space 1) pointers: a generic pointer would compile to flat_load,
+// which completes out of order with LDS traffic, so the compiler must drain vmcnt(0) before
+// every use -- defeating the producer's prefetch.  global_load keeps counted vmcnt waits.
+typedef const __attribute__((address_space(1))) v4u32 gv4u32;
+typedef const __attribute__((address_space(1))) uint32_t gu32;
 
-__device__ __forceinline__ void fetch_full(const uint8_t* p, RawBlock& r) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const v4u32* q = reinterpret_cast<const v4u32*>(a & ~uintptr_t(3));
+// Branch-free: when `ok` is false (block outside the part or the launch's range) the same
+// loads read the plan's 256-byte zero page instead, so every lane issues the same loads and
+// the compiler can keep COUNTED vmcnt waits (a divergent branch around the loads makes it
+// drain vmcnt(0) at every use, i.e. no prefetch).  The 17th dword is read from the block
+// only when p is not dword aligned, so no dword without a part byte is ever touched.
+__device__ __forceinline__ void fetch_full(const uint8_t* p, bool ok, const uint8_t* zero,
+                                           RawBlock& r) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(ok ? p : zero);
+  gv4u32* q = reinterpret_cast<gv4u32*>(a & ~uintptr_t(3));
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const v4u32 v = __builtin_nontemporal_load(q + i);
     r.d[4 * i + 0] = v.x; r.d[4 * i + 1] = v.y; r.d[4 * i + 2] = v.z; r.d[4 * i + 3] = v.w;
   }
-  r.d[16] = 0;
-  if (a & 3) r.d[16] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(q + 4));
+  gu32* x = reinterpret_cast<gu32*>((a & 3) ? reinterpret_cast<uintptr_t>(q + 4)
+                                             : reinterpret_cast<uintptr_t>(zero));
+  r.d[16] = __builtin_nontemporal_load(x);
 }
 
 // v_perm selector turning {d[j+1]:d[j]} into the big-endian word at byte shift `sh`.

@@ -31,6 +31,7 @@ struct LaunchArgs {
   const uint32_t* out_idx;   // slot -> output part index
   uint32_t* state;           // n*8 words (slot order); may be null for single-launch plans
   uint32_t* digests;         // n*8 words (part order), bswap32(H_i) like lib/hash to_little
+  const uint8_t* zero;       // 256 zero bytes: target of the loads of out-of-range lanes
   uint64_t blk_begin, blk_end, blk_origin;
   uint32_t n;
 };
@@ -98,10 +99,10 @@ __global__ __launch_bounds__(256) void sha256_lane_kernel(LaunchArgs A) {
   // launch's base may hold nothing beyond blk_end (host streaming ring).
   const uint64_t fend = fetch_end(s.len, A.blk_end);
   RawBlock cur;
-  if (A.blk_begin < fend) fetch_full(p, cur);
+  fetch_full(p, A.blk_begin < fend, A.zero, cur);
   for (uint64_t b = A.blk_begin; b < end; ++b) {
     RawBlock nxt;
-    if (b + 1 < fend) fetch_full(p + 64, nxt);  // prefetch one block ahead
+    fetch_full(p + 64, b + 1 < fend, A.zero, nxt);  // prefetch one block ahead
     uint32_t w[16], wk[64];
     make_block(cur, sel, p, s.len, b, A.blk_end, w);
     schedule_wk(w, wk);
@@ -161,21 +162,21 @@ __global__ __launch_bounds__(kPcThreads) void sha256_pc_kernel(LaunchArgs A) {
     const uint32_t sel = be_selector(uint32_t(reinterpret_cast<uintptr_t>(p) & 3));
     const uint64_t fend = fetch_end(s.len, A.blk_end);
     RawBlock ra, rb;
-    if (b0 < fend) fetch_full(p, ra);
-    if (b0 + 1 < fend) fetch_full(p + 64, rb);
+    fetch_full(p, b0 < fend, A.zero, ra);
+    fetch_full(p + 64, b0 + 1 < fend, A.zero, rb);
     produce_block(ra, sel, p, s.len, b0, A.blk_end, lds_wk[0], lane);
     __syncthreads();
     for (uint64_t k = 1; k <= iters; k += 2) {
       // odd step: block b0+k from rb into buffer 1; refill ra with block b0+k+1
       if (k < iters) {
-        if (b0 + k + 1 < fend) fetch_full(p + 64 * (k + 1), ra);
+        fetch_full(p + 64 * (k + 1), b0 + k + 1 < fend, A.zero, ra);
         produce_block(rb, sel, p + 64 * k, s.len, b0 + k, A.blk_end, lds_wk[1], lane);
       }
       __syncthreads();
       if (k + 1 > iters) break;
       // even step: block b0+k+1 from ra into buffer 0; refill rb with block b0+k+2
       if (k + 1 < iters) {
-        if (b0 + k + 2 < fend) fetch_full(p + 64 * (k + 2), rb);
+        fetch_full(p + 64 * (k + 2), b0 + k + 2 < fend, A.zero, rb);
         produce_block(ra, sel, p + 64 * (k + 1), s.len, b0 + k + 1, A.blk_end, lds_wk[0], lane);
       }
       __syncthreads();
@@ -278,19 +279,19 @@ __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A)
     const uint64_t fend = fetch_end(s.len, A.blk_end);
     const uint64_t bh = b0 + half;  // this lane's first block
     RawBlock ra, rb;
-    if (bh < fend) fetch_full(p, ra);
-    if (bh + 2 < fend) fetch_full(p + 128, rb);
+    fetch_full(p, bh < fend, A.zero, ra);
+    fetch_full(p + 128, bh + 2 < fend, A.zero, rb);
     produce_block(ra, sel, p, s.len, bh, A.blk_end, lds_wk[0][half], part);
     __syncthreads();
     for (uint64_t k = 1; k <= steps; k += 2) {
       if (k < steps) {
-        if (bh + 2 * (k + 1) < fend) fetch_full(p + 128 * (k + 1), ra);
+        fetch_full(p + 128 * (k + 1), bh + 2 * (k + 1) < fend, A.zero, ra);
         produce_block(rb, sel, p + 128 * k, s.len, bh + 2 * k, A.blk_end, lds_wk[1][half], part);
       }
       __syncthreads();
       if (k + 1 > steps) break;
       if (k + 1 < steps) {
-        if (bh + 2 * (k + 2) < fend) fetch_full(p + 128 * (k + 2), rb);
+        fetch_full(p + 128 * (k + 2), bh + 2 * (k + 2) < fend, A.zero, rb);
         produce_block(ra, sel, p + 128 * (k + 1), s.len, bh + 2 * (k + 1), A.blk_end, lds_wk[0][half], part);
       }
       __syncthreads();
@@ -486,28 +487,32 @@ __global__ __launch_bounds__(kPcThreads) void md5_pc_kernel(LaunchArgs A) {
   const uint64_t iters = wg_end - A.blk_begin;
 
   if (wave == 1) {
+    // An MD5 block takes the consumer only ~0.9 us, less than an HBM round trip under load,
+    // so the producer keeps TWO blocks in flight: three register sets rotate, and the load
+    // for block j+2 is issued while block j is produced.
     const uint64_t b0 = A.blk_begin;
     const uint8_t* p = A.base + s.off + 64ull * (b0 - A.blk_origin);
     const uint32_t sel = le_selector(uint32_t(reinterpret_cast<uintptr_t>(p) & 3));
     const uint64_t fend = fetch_end(s.len, A.blk_end);
-    RawBlock ra, rb;
-    if (b0 < fend) fetch_full(p, ra);
-    if (b0 + 1 < fend) fetch_full(p + 64, rb);
+    RawBlock ra, rb, rc;
+    fetch_full(p, b0 < fend, A.zero, ra);
+    fetch_full(p + 64, b0 + 1 < fend, A.zero, rb);
+    fetch_full(p + 128, b0 + 2 < fend, A.zero, rc);
     md5_produce(ra, sel, p, s.len, b0, A.blk_end, lds_km[0], lane);
     __syncthreads();
-    for (uint64_t k = 1; k <= iters; k += 2) {
-      if (k < iters) {
-        if (b0 + k + 1 < fend) fetch_full(p + 64 * (k + 1), ra);
-        md5_produce(rb, sel, p + 64 * k, s.len, b0 + k, A.blk_end, lds_km[1], lane);
-      }
-      __syncthreads();
-      if (k + 1 > iters) break;
-      if (k + 1 < iters) {
-        if (b0 + k + 2 < fend) fetch_full(p + 64 * (k + 2), rb);
-        md5_produce(ra, sel, p + 64 * (k + 1), s.len, b0 + k + 1, A.blk_end, lds_km[0], lane);
-      }
-      __syncthreads();
+#define S3H_MD5_PSTEP(J, NEXT, CUR)                                                        \
+    if ((J) < iters) {                                                                     \
+      fetch_full(p + 64 * ((J) + 2), b0 + (J) + 2 < fend, A.zero, NEXT);                    \
+      md5_produce(CUR, sel, p + 64 * (J), s.len, b0 + (J), A.blk_end, lds_km[(J) & 1], lane); \
+    }                                                                                      \
+    __syncthreads();                                                                       \
+    if ((J) + 1 > iters) break;
+    for (uint64_t j = 1;; j += 3) {
+      S3H_MD5_PSTEP(j, ra, rb)
+      S3H_MD5_PSTEP(j + 1, rb, rc)
+      S3H_MD5_PSTEP(j + 2, rc, ra)
     }
+#undef S3H_MD5_PSTEP
   } else {
     __builtin_amdgcn_s_setprio(3);
     uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};

@@ -49,6 +49,24 @@ KERNEL(k_mix_round, "v_alignbit_b32 %0, %8, %8, %9\n\tv_alignbit_b32 %1, %8, %8,
                     "v_bitop3_b32 %4, %9, %10, %8 bitop3:0x96\n\tv_bfi_b32 %5, %8, %9, %10\n\t"
                     "v_add3_u32 %6, %8, %9, %10\n\tv_add_u32_dpp %7, %8, %9 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5\n\t")
 
+// dependent chains: every instruction reads the previous one's result (%0)
+#define DEP8(op, tail) op " %0, " tail "\n\t" op " %0, " tail "\n\t" op " %0, " tail "\n\t" op " %0, " tail "\n\t" \
+                       op " %0, " tail "\n\t" op " %0, " tail "\n\t" op " %0, " tail "\n\t" op " %0, " tail "\n\t"
+KERNEL(k_dep_add_e32, DEP8("v_add_u32_e32", "%8, %0"))
+KERNEL(k_dep_add3, DEP8("v_add3_u32", "%0, %8, %9"))
+KERNEL(k_dep_alignbit, DEP8("v_alignbit_b32", "%0, %0, 7"))
+KERNEL(k_dep_bitop3, DEP8("v_bitop3_b32", "%0, %8, %9 bitop3:0xca"))
+// MD5-like step: bitop3 -> add3 -> alignbit -> add, each dependent (x2 per 8)
+KERNEL(k_dep_md5, "v_bitop3_b32 %1, %0, %8, %9 bitop3:0xca\n\tv_add3_u32 %1, %1, %10, %9\n\t"
+                  "v_alignbit_b32 %1, %1, %1, 25\n\tv_add_u32_e32 %0, %0, %1\n\t"
+                  "v_bitop3_b32 %1, %0, %8, %9 bitop3:0xca\n\tv_add3_u32 %1, %1, %10, %9\n\t"
+                  "v_alignbit_b32 %1, %1, %1, 25\n\tv_add_u32_e32 %0, %0, %1\n\t")
+// same with VOP2 add instead of add3 (a+K+M precomputed off the chain)
+KERNEL(k_dep_md5b, "v_bitop3_b32 %1, %0, %8, %9 bitop3:0xca\n\tv_add_u32_e32 %1, %10, %1\n\t"
+                   "v_alignbit_b32 %1, %1, %1, 25\n\tv_add_u32_e32 %0, %0, %1\n\t"
+                   "v_bitop3_b32 %1, %0, %8, %9 bitop3:0xca\n\tv_add_u32_e32 %1, %10, %1\n\t"
+                   "v_alignbit_b32 %1, %1, %1, 25\n\tv_add_u32_e32 %0, %0, %1\n\t")
+
 int main() {
   uint32_t* out; uint64_t* cyc;
   CHECK(hipMalloc(&out, 4096));
@@ -58,7 +76,10 @@ int main() {
       {"v_alignbit_b32", k_alignbit}, {"v_bitop3_b32", k_bitop3}, {"v_add3_u32", k_add3},
       {"v_bfi_b32", k_bfi}, {"v_perm_b32", k_perm}, {"v_add_u32_e32", k_add_e32},
       {"v_xor_b32_e32", k_xor_e32}, {"v_add_u32_e64", k_add_e64}, {"v_add_u32_dpp", k_add_dpp},
-      {"v_mov_b32_dpp", k_mov_dpp}, {"v_lshl_add_u32", k_lshl_add}, {"round mix (8)", k_mix_round}};
+      {"v_mov_b32_dpp", k_mov_dpp}, {"v_lshl_add_u32", k_lshl_add}, {"round mix (8)", k_mix_round},
+      {"DEP v_add_u32_e32", k_dep_add_e32}, {"DEP v_add3_u32", k_dep_add3},
+      {"DEP v_alignbit", k_dep_alignbit}, {"DEP v_bitop3", k_dep_bitop3},
+      {"DEP md5 step (add3)", k_dep_md5}, {"DEP md5 step (add)", k_dep_md5b}};
   for (auto& t : T) {
     for (int threads : {64, 512}) {
       uint64_t c = 0;
