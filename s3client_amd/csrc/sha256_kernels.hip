@@ -245,14 +245,25 @@ __device__ __forceinline__ bool pair_is_ahalf(uint32_t lane) { return (lane >> 2
   "v_add_u32_dpp %[" #d "], %[" #d "], %[q3] row_shl:4 row_mask:0xf bank_mask:0x5\n\t"       \
   "v_add_u32_dpp %[" #d "], %[q3], %[q3] row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
 
-// Four rounds (one full rotation of the state names) in one asm statement, so the compiler
-// pads only once per four rounds.
-#define S3H_PAIR_4RND(W1, W2, W3, W4)                                                          \
-  asm volatile(S3H_PAIR_TXT(s0, s1, s2, s3, xa, xb, w1) S3H_PAIR_TXT(s3, s0, s1, s2, xb, xa, w2) \
-               S3H_PAIR_TXT(s2, s3, s0, s1, xa, xb, w3) S3H_PAIR_TXT(s1, s2, s3, s0, xb, xa, w4) \
+// Sixteen rounds (four rotations of the state names) per asm statement (30 operands, the
+// inline-asm maximum): the compiler pads with an s_nop between consecutive asm statements,
+// so fewer, longer statements keep the stream at one VALU per issue slot.
+#define S3H_PAIR_4TXT(wa, wb, wc, wd)                                                         \
+  S3H_PAIR_TXT(s0, s1, s2, s3, xa, xb, wa) S3H_PAIR_TXT(s3, s0, s1, s2, xb, xa, wb)              \
+  S3H_PAIR_TXT(s2, s3, s0, s1, xa, xb, wc) S3H_PAIR_TXT(s1, s2, s3, s0, xb, xa, wd)
+#define S3H_PAIR_16RND(WK, T)                                                                   \
+  asm volatile(S3H_PAIR_4TXT(w1, w2, w3, w4) S3H_PAIR_4TXT(w5, w6, w7, w8)                       \
+               S3H_PAIR_4TXT(w9, w10, w11, w12) S3H_PAIR_4TXT(w13, w14, w15, w16)               \
                : [s0] "+v"(s0), [s1] "+v"(s1), [s2] "+v"(s2), [s3] "+v"(s3), [xa] "+v"(xa),    \
                  [xb] "+v"(xb), [q1] "=&v"(q1), [q2] "=&v"(q2), [q3] "=&v"(q3), [q4] "=&v"(q4)  \
-               : [w1] "v"(W1), [w2] "v"(W2), [w3] "v"(W3), [w4] "v"(W4), [h1] "v"(sh1),         \
+               : [w1] "v"(WK[(T + 1) & 63]), [w2] "v"(WK[(T + 2) & 63]),                       \
+                 [w3] "v"(WK[(T + 3) & 63]), [w4] "v"(WK[(T + 4) & 63]),                       \
+                 [w5] "v"(WK[(T + 5) & 63]), [w6] "v"(WK[(T + 6) & 63]),                       \
+                 [w7] "v"(WK[(T + 7) & 63]), [w8] "v"(WK[(T + 8) & 63]),                       \
+                 [w9] "v"(WK[(T + 9) & 63]), [w10] "v"(WK[(T + 10) & 63]),                     \
+                 [w11] "v"(WK[(T + 11) & 63]), [w12] "v"(WK[(T + 12) & 63]),                   \
+                 [w13] "v"(WK[(T + 13) & 63]), [w14] "v"(WK[(T + 14) & 63]),                   \
+                 [w15] "v"(WK[(T + 15) & 63]), [w16] "v"(WK[(T + 16) & 63]), [h1] "v"(sh1),    \
                  [h2] "v"(sh2), [h3] "v"(sh3), [m] "v"(msk))
 
 __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A) {
@@ -319,33 +330,45 @@ __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A)
     }
     uint32_t xa = 0, xb = 0;  // a-half lanes are never written: their X stays 0
     uint32_t q1, q2, q3, q4;
+    // Slots are sorted by length: every lane is live for blocks below the last slot's count.
+    const uint32_t last = (slot0 + kPairParts <= A.n ? slot0 + kPairParts : A.n) - 1;
+    const uint64_t all_live_end = nblocks(A.slots[last].len);
+    auto block = [&](const uint32_t wk[64], uint64_t i) {
+      const uint32_t t0 = s0, t1 = s1, t2 = s2, t3 = s3;
+      asm volatile(
+          "s_nop 1\n\t"
+          "v_add_u32_dpp %0, %1, %2 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5"
+          : "+v"(xa) : "v"(s3), "v"(wk[0]));
+      S3H_PAIR_16RND(wk, 0);
+      S3H_PAIR_16RND(wk, 16);
+      S3H_PAIR_16RND(wk, 32);
+      S3H_PAIR_16RND(wk, 48);
+      if (b0 + i < all_live_end) {  // uniform branch: no per-lane select
+        s0 += t0; s1 += t1; s2 += t2; s3 += t3;
+      } else {
+        const bool live = (b0 + i) < nb;
+        s0 = live ? s0 + t0 : t0;
+        s1 = live ? s1 + t1 : t1;
+        s2 = live ? s2 + t2 : t2;
+        s3 = live ? s3 + t3 : t3;
+      }
+    };
     __syncthreads();
     for (uint64_t j = 0; j < steps; ++j) {
+      // Both blocks' W+K rows are read up front and waited for ONCE (one exposed LDS latency
+      // per step instead of a counted wait before every 4-round group).
+      const bool second = 2 * j + 1 < iters;
+      uint32_t wk0[64], wk1[64];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint64_t i = 2 * j + h;
-        if (i < iters) {
-          uint32_t wk[64];
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const uint4 v = lds_wk[j & 1][h][q][part];
-            wk[4 * q] = v.x; wk[4 * q + 1] = v.y; wk[4 * q + 2] = v.z; wk[4 * q + 3] = v.w;
-          }
-          const uint32_t t0 = s0, t1 = s1, t2 = s2, t3 = s3;
-          asm volatile(
-              "s_nop 1\n\t"
-              "v_add_u32_dpp %0, %1, %2 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5"
-              : "+v"(xa) : "v"(s3), "v"(wk[0]));
-#pragma unroll
-          for (int t = 0; t < 64; t += 4)
-            S3H_PAIR_4RND(wk[(t + 1) & 63], wk[(t + 2) & 63], wk[(t + 3) & 63], wk[(t + 4) & 63]);
-          const bool live = (b0 + i) < nb;
-          s0 = live ? s0 + t0 : t0;
-          s1 = live ? s1 + t1 : t1;
-          s2 = live ? s2 + t2 : t2;
-          s3 = live ? s3 + t3 : t3;
-        }
+      for (int q = 0; q < 16; ++q) {
+        const uint4 v = lds_wk[j & 1][0][q][part];
+        wk0[4 * q] = v.x; wk0[4 * q + 1] = v.y; wk0[4 * q + 2] = v.z; wk0[4 * q + 3] = v.w;
+        const uint4 u = lds_wk[j & 1][1][q][part];
+        wk1[4 * q] = u.x; wk1[4 * q + 1] = u.y; wk1[4 * q + 2] = u.z; wk1[4 * q + 3] = u.w;
       }
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      block(wk0, 2 * j);
+      if (second) block(wk1, 2 * j + 1);
       __syncthreads();
     }
     if (valid && nb > b0) {
