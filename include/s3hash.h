@@ -107,6 +107,18 @@ int s3h_sha256_batch_host(const uint8_t *const *parts, const uint64_t *lengths, 
 int s3h_md5_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                        uint32_t *digests, int ndevices, uint64_t slice_bytes);
 
+/* ---------------------------------------------------------------- verification
+ * Download-side check of parts against known digests (ranged GETs of
+ * lib/src/download.cpp:88-103; expected = the uploader's x-amz-content-sha256 / Content-MD5).
+ * mismatch[i] = 1 when part i differs; *mismatches = their count.  Blocking.
+ * Device form: d_expected (n x words) and d_mismatch (n bytes) are device pointers. */
+int s3h_verify_batch_device(int device, int algo, const void *d_base, const uint64_t *offsets,
+                            const uint64_t *lengths, uint64_t n, const uint32_t *d_expected,
+                            uint8_t *d_mismatch, uint64_t *mismatches, void *stream);
+int s3h_verify_batch_host(int algo, const uint8_t *const *parts, const uint64_t *lengths,
+                          uint64_t n, const uint32_t *expected, uint8_t *mismatch,
+                          uint64_t *mismatches, int ndevices);
+
 /* ---------------------------------------------------------------- synthetic inputs
  * Fill part i (at d_base + offsets[i], 8-B aligned, lengths[i] bytes) with generator
  * G(seed, part_ids[i], lengths[i]) of SURVEY.md 8(d).  Asynchronous on `stream`. */

@@ -25,7 +25,8 @@ C_ABI_SYMBOLS = (
     "s3h_plan_info", "s3h_sha256_batch_device", "s3h_sha256_batch_host",
     "s3h_generate_parts", "s3h_cpu_sha256", "s3h_cpu_hmac256", "s3h_hash_to_text",
     "s3h_cpu_backend", "s3h_cpu_md5", "s3h_plan_create_ex", "s3h_plan_algo",
-    "s3h_md5_batch_device", "s3h_md5_batch_host",
+    "s3h_md5_batch_device", "s3h_md5_batch_host", "s3h_verify_batch_device",
+    "s3h_verify_batch_host",
 )
 ALGO_SHA256, ALGO_MD5 = 0, 1
 ALGO_IDS = {"sha256": ALGO_SHA256, "md5": ALGO_MD5}
@@ -90,6 +91,12 @@ def lib() -> ctypes.CDLL:
                 getattr(L, name).argtypes = [ctypes.POINTER(ctypes.c_void_p), u64p,
                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
                                              ctypes.c_uint64]
+            L.s3h_verify_batch_host.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), u64p,
+                                                ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                                u64p, ctypes.c_int]
+            L.s3h_verify_batch_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, u64p,
+                                                  u64p, ctypes.c_uint64, ctypes.c_void_p,
+                                                  ctypes.c_void_p, u64p, ctypes.c_void_p]
             L.s3h_md5_batch_device.argtypes = [ctypes.c_int, ctypes.c_void_p, u64p, u64p,
                                                ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
             L.s3h_generate_parts.argtypes = [ctypes.c_int, ctypes.c_void_p, u64p, u64p, u64p,

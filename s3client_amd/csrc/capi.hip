@@ -417,6 +417,59 @@ int s3h_md5_batch_host(const uint8_t* const* parts, const uint64_t* lengths, uin
   return batch_host(S3H_ALGO_MD5, parts, lengths, n, digests, ndevices, slice_bytes);
 }
 
+int s3h_verify_batch_device(int device, int algo, const void* d_base, const uint64_t* offsets,
+                            const uint64_t* lengths, uint64_t n, const uint32_t* d_expected,
+                            uint8_t* d_mismatch, uint64_t* mismatches, void* stream) {
+  if (!d_expected || !d_mismatch || !mismatches) return fail(S3H_EINVAL, "verify: null argument");
+  s3h_plan_s* P = nullptr;
+  if (int rc = plan_build(device, algo, offsets, lengths, n, S3H_KERNEL_AUTO, &P)) return rc;
+  struct Cleanup {
+    s3h_plan_s* P;
+    ~Cleanup() { s3h_plan_destroy(P); }
+  } cleanup{P};
+  DeviceGuard g(device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint32_t dw = digest_words(algo);
+  uint32_t* d_dig = nullptr;
+  unsigned long long* d_count = nullptr;
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&d_dig), n * dw * 4, s));
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&d_count), 8, s));
+  HIP_TRY(hipMemsetAsync(d_count, 0, 8, s));
+  int rc = plan_launch(P, d_base, d_dig, 0, P->max_blocks, 0, s, false);
+  if (rc == S3H_OK) {
+    hipLaunchKernelGGL(s3h::compare_digests_kernel, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, s,
+                       d_dig, d_expected, n, dw, d_mismatch, d_count);
+    unsigned long long c = 0;
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(&c, d_count, 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) rc = fail(S3H_EHIP, "verify: %s", hipGetErrorString(e));
+    *mismatches = c;
+  }
+  (void)hipFreeAsync(d_dig, s);
+  (void)hipFreeAsync(d_count, s);
+  (void)hipStreamSynchronize(s);
+  return rc;
+}
+
+int s3h_verify_batch_host(int algo, const uint8_t* const* parts, const uint64_t* lengths,
+                          uint64_t n, const uint32_t* expected, uint8_t* mismatch,
+                          uint64_t* mismatches, int ndevices) {
+  if (!expected || !mismatch || !mismatches) return fail(S3H_EINVAL, "verify: null argument");
+  if (algo != S3H_ALGO_SHA256 && algo != S3H_ALGO_MD5)
+    return fail(S3H_EINVAL, "verify: unknown algorithm %d", algo);
+  const uint32_t dw = digest_words(algo);
+  std::vector<uint32_t> got(n * dw);
+  if (int rc = batch_host(algo, parts, lengths, n, got.data(), ndevices, 0)) return rc;
+  uint64_t c = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    mismatch[i] = std::memcmp(&got[dw * i], expected + dw * i, dw * 4) != 0;
+    c += mismatch[i];
+  }
+  *mismatches = c;
+  return S3H_OK;
+}
+
 int s3h_generate_parts(int device, void* d_base, const uint64_t* offsets, const uint64_t* lengths,
                        const uint64_t* part_ids, uint64_t n, uint64_t seed, void* stream) {
   if (!d_base || !offsets || !lengths || !part_ids || n == 0 || n > 65535)

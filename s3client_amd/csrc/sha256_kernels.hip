@@ -570,6 +570,21 @@ __global__ __launch_bounds__(kPcThreads) void md5_pc_kernel(LaunchArgs A) {
   }
 }
 
+// ------------------------------------------------------------- verification
+// Download-side verification (ranged GETs of lib/src/download.cpp:88-103):
+// mismatch[i] = digest(i) != expected(i), words compared as stored.
+__global__ __launch_bounds__(256) void compare_digests_kernel(const uint32_t* got,
+                                                              const uint32_t* want, uint64_t n,
+                                                              uint32_t words, uint8_t* mismatch,
+                                                              unsigned long long* count) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (i >= n) return;
+  uint32_t diff = 0;
+  for (uint32_t w = 0; w < words; ++w) diff |= got[words * i + w] ^ want[words * i + w];
+  mismatch[i] = diff != 0;
+  if (diff) atomicAdd(count, 1ull);
+}
+
 // ------------------------------------------------------------- synthetic input generator
 // G(seed, p, L) of SURVEY.md 8(d): word j of part p is splitmix64(x0 + (j+1)*golden),
 // x0 = seed ^ p*0xD1B54A32D192ED03, serialised little-endian.  Parts must start 8-B aligned.

@@ -157,6 +157,45 @@ def md5_batch_host(parts: Sequence, ndevices: int = 0, slice_bytes: int = 0) -> 
     return _host_batch(lib().s3h_md5_batch_host, 4, parts, ndevices, slice_bytes)
 
 
+def verify_batch_host(parts: Sequence, expected, algo: str = "sha256",
+                      ndevices: int = 0) -> np.ndarray:
+    """Download-side verification: bool mask of parts whose digest differs from ``expected``
+    ((n, 8) uint32 SHA-256 or (n, 4) MD5 words, or a list of hex strings)."""
+    a = _native.ALGO_IDS[algo]
+    words = _native.DIGEST_WORDS[a]
+    if len(expected) and isinstance(expected[0], str):
+        expected = np.stack([np.frombuffer(bytes.fromhex(h), dtype=np.uint32) for h in expected])
+    exp = np.ascontiguousarray(expected, dtype=np.uint32).reshape(-1, words)
+    arrs = [np.frombuffer(p, dtype=np.uint8) if isinstance(p, (bytes, bytearray, memoryview))
+            else np.ascontiguousarray(p, dtype=np.uint8).reshape(-1) for p in parts]
+    n = len(arrs)
+    if exp.shape[0] != n:
+        raise ValueError("expected digest count differs from part count")
+    ptrs = (ctypes.c_void_p * n)(*[x.ctypes.data if x.size else 0 for x in arrs])
+    lens = _u64([x.size for x in arrs])
+    mism = np.zeros(n, dtype=np.uint8)
+    cnt = ctypes.c_uint64(0)
+    check(lib().s3h_verify_batch_host(a, ptrs, _p64(lens), n, exp.ctypes.data, mism.ctypes.data,
+                                      ctypes.byref(cnt), ndevices))
+    assert cnt.value == int(mism.sum())
+    return mism.astype(bool)
+
+
+def verify_batch_device(data, offsets, lengths, expected, algo: str = "sha256", stream=None):
+    """Device-resident verification: returns (mismatch count, bool mask on the device)."""
+    import torch
+    a = _native.ALGO_IDS[algo]
+    offs, lens = _u64(offsets), _u64(lengths)
+    mism = torch.zeros(offs.size, dtype=torch.uint8, device=data.device)
+    cnt = ctypes.c_uint64(0)
+    check(lib().s3h_verify_batch_device(data.device.index, a, ctypes.c_void_p(data.data_ptr()),
+                                        _p64(offs), _p64(lens), offs.size,
+                                        ctypes.c_void_p(expected.data_ptr()),
+                                        ctypes.c_void_p(mism.data_ptr()), ctypes.byref(cnt),
+                                        ctypes.c_void_p(_stream_handle(stream))))
+    return cnt.value, mism.bool()
+
+
 def multipart_etag(part_md5s) -> str:
     """S3 multipart ETag: hex(MD5(concatenated binary part MD5s)) + "-" + part count."""
     import hashlib

@@ -250,3 +250,21 @@ def test_md5_host_path_transfer_etag(torch_cuda, golden):
         d = s3.md5_batch_host(views, slice_bytes=sl)
         assert s3.digests_to_text(d, 4) == [p["digest"] for p in golden["md5"]["transfer"]]
         assert s3.multipart_etag(d) == golden["md5"]["transfer_etag"]
+
+
+def test_verify_download_parts(torch_cuda, golden):
+    """Download-side verification: one corrupted byte flags exactly its part."""
+    t = golden["transfer"]
+    data = (np.arange(t["size"], dtype=np.uint64) % 128).astype(np.uint8)
+    views = [data[p["offset"]:p["offset"] + p["size"]].copy() for p in t["parts"]]
+    views[4][12345] ^= 1
+    sha = [p["digest"] for p in t["parts"]]
+    md5s = [p["digest"] for p in golden["md5"]["transfer"]]
+    assert s3.verify_batch_host(views, sha).tolist() == [False] * 4 + [True, False]
+    assert s3.verify_batch_host(views, md5s, algo="md5").tolist() == [False] * 4 + [True, False]
+    dev = torch_cuda.from_numpy(np.concatenate(views)).cuda()
+    offs = np.concatenate([[0], np.cumsum([v.size for v in views])[:-1]])
+    exp = torch_cuda.from_numpy(np.stack([np.frombuffer(bytes.fromhex(h), np.uint32)
+                                          for h in sha]).view(np.int32)).cuda()
+    n, mask = s3.verify_batch_device(dev, offs, [v.size for v in views], exp)
+    assert n == 1 and mask.cpu().tolist() == [False] * 4 + [True, False]
