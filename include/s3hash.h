@@ -119,6 +119,33 @@ int s3h_verify_batch_host(int algo, const uint8_t *const *parts, const uint64_t 
                           uint64_t n, const uint32_t *expected, uint8_t *mismatch,
                           uint64_t *mismatches, int ndevices);
 
+/* ---------------------------------------------------------------- multi-object streams
+ * n messages (objects) hashed incrementally as their bytes arrive in chunks: the batched,
+ * device-resident form of lib/hash's chunked API -- sha256_stream (sha256.cpp:84-144) for the
+ * appends, and the DOCUMENTED contract of sha256_next (sha256.h:73-89: chunks of one buffer,
+ * the last one padded with the buffer's TOTAL length) for the finish.  (The reference's
+ * sha256_next pads with the chunk length and hashes unpadded data)
+ *   update: appends chunk i (lengths[i] bytes, any alignment, 0 allowed) to message i.
+ *           Whole 64-B blocks are compressed on the GPU; each message's < 64-B remainder is
+ *           carried on the device into the next update.  Asynchronous on `stream`; the host
+ *           arrays may be reused on return, the device chunks must stay valid until the
+ *           stream reaches this point.
+ *   final:  pads every message with its total length, writes n digests (words as in the
+ *           batch API) and resets the object to n empty messages.
+ * The chaining state, carries and total lengths live on the device (n x 104 B); one object
+ * may be driven from one host thread at a time.  MD5 (algo 1) follows md5_stream/md5_file. */
+typedef struct s3h_stream_s *s3h_stream_t;
+int s3h_stream_create(int device, int algo, uint64_t n, int kernel, s3h_stream_t *out);
+int s3h_stream_update_device(s3h_stream_t s, const void *d_base, const uint64_t *offsets,
+                             const uint64_t *lengths, void *stream);
+int s3h_stream_final_device(s3h_stream_t s, uint32_t *d_digests, void *stream);
+/* Host-memory forms (blocking): chunks[i] may be null when lengths[i] == 0. */
+int s3h_stream_update_host(s3h_stream_t s, const uint8_t *const *chunks, const uint64_t *lengths);
+int s3h_stream_final_host(s3h_stream_t s, uint32_t *digests);
+/* Bytes appended so far to message i (host bookkeeping; no device sync). */
+int s3h_stream_total(s3h_stream_t s, uint64_t i, uint64_t *total);
+int s3h_stream_destroy(s3h_stream_t s);
+
 /* ---------------------------------------------------------------- synthetic inputs
  * Fill part i (at d_base + offsets[i], 8-B aligned, lengths[i] bytes) with generator
  * G(seed, part_ids[i], lengths[i]) of SURVEY.md 8(d).  Asynchronous on `stream`. */

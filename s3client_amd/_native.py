@@ -26,7 +26,9 @@ C_ABI_SYMBOLS = (
     "s3h_generate_parts", "s3h_cpu_sha256", "s3h_cpu_hmac256", "s3h_hash_to_text",
     "s3h_cpu_backend", "s3h_cpu_md5", "s3h_plan_create_ex", "s3h_plan_algo",
     "s3h_md5_batch_device", "s3h_md5_batch_host", "s3h_verify_batch_device",
-    "s3h_verify_batch_host",
+    "s3h_verify_batch_host", "s3h_stream_create", "s3h_stream_update_device",
+    "s3h_stream_final_device", "s3h_stream_update_host", "s3h_stream_final_host",
+    "s3h_stream_total", "s3h_stream_destroy",
 )
 ALGO_SHA256, ALGO_MD5 = 0, 1
 ALGO_IDS = {"sha256": ALGO_SHA256, "md5": ALGO_MD5}
@@ -111,6 +113,17 @@ def lib() -> ctypes.CDLL:
             L.s3h_cpu_backend.restype = ctypes.c_char_p
             L.s3h_cpu_md5.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
             L.s3h_cpu_md5.restype = None
+            L.s3h_stream_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                            ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+            L.s3h_stream_update_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, u64p, u64p,
+                                                   ctypes.c_void_p]
+            L.s3h_stream_final_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_void_p]
+            L.s3h_stream_update_host.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                                 u64p]
+            L.s3h_stream_final_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            L.s3h_stream_total.argtypes = [ctypes.c_void_p, ctypes.c_uint64, u64p]
+            L.s3h_stream_destroy.argtypes = [ctypes.c_void_p]
             _lib = L
     return _lib
 

@@ -88,6 +88,20 @@ constexpr uint64_t kMaxParts = 1ull << 31;
 
 uint32_t digest_words(int algo) { return algo == S3H_ALGO_MD5 ? 4u : 8u; }
 
+// Slots in descending length order (so block counts descend too, padded or not: the kernels
+// bound a workgroup's loop by its first slot); returns the total compressions.
+uint64_t sort_slots(const uint64_t* offsets, const uint64_t* lengths, uint64_t n, bool nopad,
+                    s3h::Slot* slots, uint32_t* order) {
+  std::iota(order, order + n, 0u);
+  std::stable_sort(order, order + n, [&](uint32_t a, uint32_t b) { return lengths[a] > lengths[b]; });
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    slots[i] = {offsets[order[i]], lengths[order[i]]};
+    total += nopad ? lengths[order[i]] >> 6 : s3h::nblocks(lengths[order[i]]);
+  }
+  return total;
+}
+
 int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* lengths, uint64_t n,
                int kernel, s3h_plan_s** out) {
   *out = nullptr;
@@ -109,16 +123,8 @@ int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* le
     return fail(S3H_EINVAL, "plan: unknown kernel %d", kernel);
 
   std::vector<uint32_t> order(n);
-  std::iota(order.begin(), order.end(), 0u);
-  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-    return s3h::nblocks(lengths[a]) > s3h::nblocks(lengths[b]);
-  });
   std::vector<s3h::Slot> slots(n);
-  uint64_t total = 0;
-  for (uint64_t i = 0; i < n; ++i) {
-    slots[i] = {offsets[order[i]], lengths[order[i]]};
-    total += s3h::nblocks(lengths[order[i]]);
-  }
+  const uint64_t total = sort_slots(offsets, lengths, n, false, slots.data(), order.data());
 
   auto* P = new s3h_plan_s();
   P->device = device;
@@ -149,23 +155,23 @@ int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* le
   return S3H_OK;
 }
 
-int plan_launch(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint64_t b0, uint64_t b1,
-                uint64_t origin, hipStream_t stream, bool ranged) {
-  if (!P || !d_base || !d_digests) return fail(S3H_EINVAL, "launch: null plan/base/digests");
-  if (b1 <= b0) return S3H_OK;
-  DeviceGuard g(P->device);
-  if (ranged && !P->d_state) HIP_TRY(hipMalloc(&P->d_state, P->n * 8 * sizeof(uint32_t)));
+// One launch of P's kernel over blocks [b0, b1) (caller holds the device guard).
+int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t* d_state,
+                uint64_t b0, uint64_t b1, uint64_t origin, uint32_t flags, const uint64_t* d_bits,
+                hipStream_t stream) {
   s3h::LaunchArgs A;
   A.base = static_cast<const uint8_t*>(d_base);
   A.slots = P->d_slots;
   A.out_idx = P->d_out_idx;
-  A.state = ranged ? P->d_state : nullptr;
+  A.state = d_state;
   A.digests = d_digests;
   A.zero = P->d_zero;
+  A.bits = d_bits;
   A.blk_begin = b0;
   A.blk_end = b1;
   A.blk_origin = origin;
   A.n = uint32_t(P->n);
+  A.flags = flags;
   if (P->algo == S3H_ALGO_MD5)
     hipLaunchKernelGGL(s3h::md5_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_PC)
@@ -176,6 +182,16 @@ int plan_launch(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint64_t
     hipLaunchKernelGGL(s3h::sha256_lane_kernel, dim3(P->grid), dim3(256), 0, stream, A);
   HIP_TRY(hipGetLastError());
   return S3H_OK;
+}
+
+int plan_launch(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint64_t b0, uint64_t b1,
+                uint64_t origin, hipStream_t stream, bool ranged) {
+  if (!P || !d_base || !d_digests) return fail(S3H_EINVAL, "launch: null plan/base/digests");
+  if (b1 <= b0) return S3H_OK;
+  DeviceGuard g(P->device);
+  if (ranged && !P->d_state) HIP_TRY(hipMalloc(&P->d_state, P->n * 8 * sizeof(uint32_t)));
+  return launch_args(P, d_base, d_digests, ranged ? P->d_state : nullptr, b0, b1, origin, 0,
+                     nullptr, stream);
 }
 
 // ------------------------------------------------------------------ host streaming path
@@ -289,6 +305,143 @@ int run_host_shard(const HostShard& sh, int algo, const uint8_t* const* parts,
     for (uint64_t j = 0; j < n; ++j)
       std::memcpy(digests + dw * sh.parts[j], &local[dw * j], dw * 4);
   return rc;
+}
+
+// Re-sort a plan's slots for new lengths (same n) and upload them asynchronously from
+// pinned staging (the caller keeps the staging alive until `s` passes the copy).
+int plan_refill(s3h_plan_s* P, const uint64_t* offsets, const uint64_t* lengths, bool nopad,
+                s3h::Slot* h_slots, uint32_t* h_order, hipStream_t s) {
+  P->total_blocks = sort_slots(offsets, lengths, P->n, nopad, h_slots, h_order);
+  P->max_blocks = nopad ? h_slots[0].len >> 6 : s3h::nblocks(h_slots[0].len);
+  HIP_TRY(hipMemcpyAsync(P->d_slots, h_slots, P->n * sizeof(s3h::Slot), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(P->d_out_idx, h_order, P->n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  return S3H_OK;
+}
+
+}  // namespace
+
+// Multi-object stream (include/s3hash.h "multi-object streams").  Host bookkeeping: per
+// message carry length (< 64) and total bytes.  Device: chaining state (message order),
+// 64-B carry and head-block buffers, the splice jobs, three re-sortable plans.
+struct s3h_stream_s {
+  int device = 0, algo = 0;
+  uint64_t n = 0;
+  s3h_plan_s *head = nullptr, *body = nullptr, *fin = nullptr;
+  uint32_t* d_state = nullptr;
+  uint8_t* d_carry = nullptr;
+  uint8_t* d_head = nullptr;
+  s3h::SpliceJob* d_jobs = nullptr;
+  uint64_t* d_bits = nullptr;
+  uint8_t* d_stage = nullptr;  // host-form updates: chunks staged here
+  uint64_t stage_cap = 0;
+  uint32_t* d_dig = nullptr;   // host-form final
+  // pinned staging of one update / final (reused once `staged` has completed)
+  s3h::SpliceJob* h_jobs = nullptr;
+  s3h::Slot* h_slots[2] = {nullptr, nullptr};
+  uint32_t* h_order[2] = {nullptr, nullptr};
+  uint64_t* h_bits = nullptr;
+  hipEvent_t staged = nullptr;
+  hipStream_t own = nullptr;
+  std::vector<uint64_t> total;
+  std::vector<uint32_t> carry;
+  std::vector<uint64_t> offs, lens, offs2, lens2;
+};
+
+namespace {
+
+void stream_free(s3h_stream_s* S) {
+  DeviceGuard g(S->device);
+  if (S->own) (void)hipStreamSynchronize(S->own);
+  if (S->staged) (void)hipEventSynchronize(S->staged);
+  s3h_plan_destroy(S->head);
+  s3h_plan_destroy(S->body);
+  s3h_plan_destroy(S->fin);
+  for (void* p : {(void*)S->d_state, (void*)S->d_carry, (void*)S->d_head, (void*)S->d_jobs,
+                  (void*)S->d_bits, (void*)S->d_stage, (void*)S->d_dig})
+    (void)hipFree(p);
+  (void)hipHostFree(S->h_jobs);
+  if (S->staged) (void)hipEventDestroy(S->staged);
+  if (S->own) (void)hipStreamDestroy(S->own);
+  delete S;
+}
+
+int stream_reset(s3h_stream_s* S, hipStream_t s) {
+  std::fill(S->total.begin(), S->total.end(), 0);
+  std::fill(S->carry.begin(), S->carry.end(), 0u);
+  hipLaunchKernelGGL(s3h::stream_init_kernel, dim3(uint32_t((S->n + 255) / 256)), dim3(256), 0, s,
+                     S->d_state, S->n, int(S->algo == S3H_ALGO_MD5));
+  HIP_TRY(hipGetLastError());
+  return S3H_OK;
+}
+
+int stream_update(s3h_stream_s* S, const uint8_t* base, const uint64_t* offsets,
+                  const uint64_t* lengths, hipStream_t s) {
+  const uint64_t n = S->n;
+  HIP_TRY(hipEventSynchronize(S->staged));  // the previous call's staging has been consumed
+  bool any_splice = false, any_head = false, any_body = false;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t L = lengths[i], off = L ? offsets[i] : 0;
+    const uint32_t c = S->carry[i];
+    s3h::SpliceJob j = {off, 0, c, 0, 0, 0};
+    uint64_t body_off = off, B = 0;
+    if (L == 0) {
+    } else if (c > 0 && c + L < 64) {  // still inside one block: buffer it
+      j.h = uint32_t(L);
+      j.mode = s3h::kSpliceGrow;
+      S->carry[i] = c + uint32_t(L);
+    } else {
+      j.h = c > 0 ? 64 - c : 0;  // bytes that complete the carried block
+      body_off = off + j.h;
+      B = (L - j.h) & ~uint64_t(63);
+      j.r = uint32_t(L - j.h - B);
+      j.tail = body_off + B;
+      j.mode = (c > 0 ? s3h::kSpliceHead : 0) | (j.r ? s3h::kSpliceReset : 0);
+      S->carry[i] = j.r;
+    }
+    S->total[i] += L;
+    S->h_jobs[i] = j;
+    any_splice |= j.mode != 0;
+    any_head |= (j.mode & s3h::kSpliceHead) != 0;
+    any_body |= B != 0;
+    S->offs[i] = 64 * i;
+    S->lens[i] = (j.mode & s3h::kSpliceHead) ? 64 : 0;
+    S->offs2[i] = body_off;
+    S->lens2[i] = B;
+  }
+  if (any_splice) {
+    HIP_TRY(hipMemcpyAsync(S->d_jobs, S->h_jobs, n * sizeof(s3h::SpliceJob), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(s3h::stream_splice_kernel, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, s,
+                       base, S->d_jobs, S->d_carry, S->d_head, n);
+    HIP_TRY(hipGetLastError());
+  }
+  constexpr uint32_t kAppend = s3h::kNoPad | s3h::kResume;
+  if (any_head) {  // the blocks straddling the previous update and this one come first
+    if (int rc = plan_refill(S->head, S->offs.data(), S->lens.data(), true, S->h_slots[0], S->h_order[0], s)) return rc;
+    if (int rc = launch_args(S->head, S->d_head, nullptr, S->d_state, 0, 1, 0, kAppend, nullptr, s)) return rc;
+  }
+  if (any_body) {
+    if (int rc = plan_refill(S->body, S->offs2.data(), S->lens2.data(), true, S->h_slots[1], S->h_order[1], s)) return rc;
+    if (int rc = launch_args(S->body, base, nullptr, S->d_state, 0, S->body->max_blocks, 0, kAppend, nullptr, s)) return rc;
+  }
+  HIP_TRY(hipEventRecord(S->staged, s));
+  return S3H_OK;
+}
+
+int stream_final(s3h_stream_s* S, uint32_t* d_digests, hipStream_t s) {
+  const uint64_t n = S->n;
+  HIP_TRY(hipEventSynchronize(S->staged));
+  for (uint64_t i = 0; i < n; ++i) {
+    S->offs[i] = 64 * i;
+    S->lens[i] = S->carry[i];
+    S->h_bits[i] = S->total[i] << 3;
+  }
+  HIP_TRY(hipMemcpyAsync(S->d_bits, S->h_bits, n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  if (int rc = plan_refill(S->fin, S->offs.data(), S->lens.data(), false, S->h_slots[0], S->h_order[0], s)) return rc;
+  // one or two padded blocks per message, starting from the appended state
+  if (int rc = launch_args(S->fin, S->d_carry, d_digests, S->d_state, 0, S->fin->max_blocks, 0,
+                           s3h::kResume, S->d_bits, s)) return rc;
+  HIP_TRY(hipEventRecord(S->staged, s));
+  return stream_reset(S, s);
 }
 
 }  // namespace
@@ -495,6 +648,128 @@ int s3h_generate_parts(int device, void* d_base, const uint64_t* offsets, const 
   HIP_TRY(hipFreeAsync(d_g, s));
   // the host vector `g` must outlive the async copy
   HIP_TRY(hipStreamSynchronize(s));
+  return S3H_OK;
+}
+
+int s3h_stream_create(int device, int algo, uint64_t n, int kernel, s3h_stream_t* out) {
+  if (!out) return fail(S3H_EINVAL, "stream: null out-pointer");
+  *out = nullptr;
+  if (n == 0 || n > kMaxParts) return fail(S3H_EINVAL, "stream: need 0 < n <= 2^31");
+  std::vector<uint64_t> zeros(n, 0);
+  auto* S = new s3h_stream_s();
+  S->device = device;
+  S->algo = algo;
+  S->n = n;
+  S->total.assign(n, 0);
+  S->carry.assign(n, 0);
+  S->offs.assign(n, 0);
+  S->lens.assign(n, 0);
+  S->offs2.assign(n, 0);
+  S->lens2.assign(n, 0);
+  int rc = plan_build(device, algo, zeros.data(), zeros.data(), n, kernel, &S->head);
+  if (!rc) rc = plan_build(device, algo, zeros.data(), zeros.data(), n, kernel, &S->body);
+  if (!rc) rc = plan_build(device, algo, zeros.data(), zeros.data(), n, kernel, &S->fin);
+  if (rc) {
+    stream_free(S);
+    return rc;
+  }
+  DeviceGuard g(device);
+  hipError_t e = hipMalloc(&S->d_state, n * 32);
+  if (e == hipSuccess) e = hipMalloc(&S->d_carry, n * 64);
+  if (e == hipSuccess) e = hipMalloc(&S->d_head, n * 64);
+  if (e == hipSuccess) e = hipMalloc(&S->d_jobs, n * sizeof(s3h::SpliceJob));
+  if (e == hipSuccess) e = hipMalloc(&S->d_bits, n * 8);
+  const size_t per = sizeof(s3h::SpliceJob) + 2 * (sizeof(s3h::Slot) + 4) + 8;
+  uint8_t* pin = nullptr;
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&pin), n * per, hipHostMallocDefault);
+  if (e == hipSuccess) {
+    S->h_jobs = reinterpret_cast<s3h::SpliceJob*>(pin);
+    S->h_slots[0] = reinterpret_cast<s3h::Slot*>(pin + n * sizeof(s3h::SpliceJob));
+    S->h_slots[1] = S->h_slots[0] + n;
+    S->h_bits = reinterpret_cast<uint64_t*>(S->h_slots[1] + n);
+    S->h_order[0] = reinterpret_cast<uint32_t*>(S->h_bits + n);
+    S->h_order[1] = S->h_order[0] + n;
+    e = hipEventCreateWithFlags(&S->staged, hipEventDisableTiming);
+  }
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&S->own, hipStreamNonBlocking);
+  if (e == hipSuccess) {
+    rc = stream_reset(S, S->own);
+    if (!rc && hipStreamSynchronize(S->own) != hipSuccess) rc = fail(S3H_EHIP, "stream: init failed");
+  } else {
+    rc = fail(e == hipErrorOutOfMemory ? S3H_ENOMEM : S3H_EHIP, "stream: %s", hipGetErrorString(e));
+  }
+  if (rc) {
+    stream_free(S);
+    return rc;
+  }
+  *out = S;
+  return S3H_OK;
+}
+
+int s3h_stream_update_device(s3h_stream_t S, const void* d_base, const uint64_t* offsets,
+                             const uint64_t* lengths, void* stream) {
+  if (!S || !lengths || (!offsets && S->n)) return fail(S3H_EINVAL, "stream update: null argument");
+  bool any = false;
+  for (uint64_t i = 0; i < S->n; ++i) any |= lengths[i] != 0;
+  if (any && !d_base) return fail(S3H_EINVAL, "stream update: null d_base");
+  DeviceGuard g(S->device);
+  return stream_update(S, static_cast<const uint8_t*>(d_base), offsets, lengths,
+                       static_cast<hipStream_t>(stream));
+}
+
+int s3h_stream_final_device(s3h_stream_t S, uint32_t* d_digests, void* stream) {
+  if (!S || !d_digests) return fail(S3H_EINVAL, "stream final: null argument");
+  DeviceGuard g(S->device);
+  return stream_final(S, d_digests, static_cast<hipStream_t>(stream));
+}
+
+int s3h_stream_update_host(s3h_stream_t S, const uint8_t* const* chunks, const uint64_t* lengths) {
+  if (!S || !chunks || !lengths) return fail(S3H_EINVAL, "stream update: null argument");
+  std::vector<uint64_t> offs(S->n);
+  uint64_t sum = 0;
+  for (uint64_t i = 0; i < S->n; ++i) {
+    if (lengths[i] && !chunks[i]) return fail(S3H_EINVAL, "stream update: chunk %llu is null", (unsigned long long)i);
+    offs[i] = sum;
+    sum += (lengths[i] + 63) & ~uint64_t(63);
+  }
+  DeviceGuard g(S->device);
+  if (sum > S->stage_cap) {
+    HIP_TRY(hipStreamSynchronize(S->own));
+    (void)hipFree(S->d_stage);
+    S->d_stage = nullptr;
+    S->stage_cap = 0;
+    HIP_TRY(hipMalloc(&S->d_stage, sum));
+    S->stage_cap = sum;
+  }
+  for (uint64_t i = 0; i < S->n; ++i)
+    if (lengths[i])
+      HIP_TRY(hipMemcpyAsync(S->d_stage + offs[i], chunks[i], lengths[i], hipMemcpyHostToDevice, S->own));
+  int rc = stream_update(S, S->d_stage, offs.data(), lengths, S->own);
+  hipError_t e = hipStreamSynchronize(S->own);  // chunks may be released on return
+  if (!rc && e != hipSuccess) rc = fail(S3H_EHIP, "stream update: %s", hipGetErrorString(e));
+  return rc;
+}
+
+int s3h_stream_final_host(s3h_stream_t S, uint32_t* digests) {
+  if (!S || !digests) return fail(S3H_EINVAL, "stream final: null argument");
+  DeviceGuard g(S->device);
+  const uint64_t bytes = S->n * digest_words(S->algo) * 4;
+  if (!S->d_dig) HIP_TRY(hipMalloc(&S->d_dig, S->n * 32));
+  int rc = stream_final(S, S->d_dig, S->own);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(digests, S->d_dig, bytes, hipMemcpyDeviceToHost, S->own));
+  HIP_TRY(hipStreamSynchronize(S->own));
+  return S3H_OK;
+}
+
+int s3h_stream_total(s3h_stream_t S, uint64_t i, uint64_t* total) {
+  if (!S || !total || i >= S->n) return fail(S3H_EINVAL, "stream total: bad argument");
+  *total = S->total[i];
+  return S3H_OK;
+}
+
+int s3h_stream_destroy(s3h_stream_t S) {
+  if (S) stream_free(S);
   return S3H_OK;
 }
 

@@ -140,8 +140,10 @@ __device__ __forceinline__ void decode_full(const RawBlock& r, uint32_t sel, uin
 // Tail block `blk` >= floor(len/64) of a part whose block-`blk` bytes start at `p`:
 // the last data bytes, 0x80, zeros, and the big-endian bit length in the final block
 // (lib/hash/utility.cpp:42-56 alloc_padded, synthesized in registers -- never in HBM).
-__device__ __forceinline__ void build_tail(const uint8_t* p, uint64_t len, uint64_t blk,
-                                           uint32_t w[16]) {
+// `bits` is the WHOLE message's bit length: 8*len for a one-shot part, larger for the final
+// segment of a streamed message (len == total mod 64 then, so the block count agrees).
+__device__ __forceinline__ void build_tail(const uint8_t* p, uint64_t len, uint64_t bits,
+                                           uint64_t blk, uint32_t w[16]) {
   const uint64_t nfull = len >> 6;
   const int rem = (blk == nfull) ? int(len & 63) : -1;  // data bytes in this block
 #pragma unroll
@@ -158,7 +160,6 @@ __device__ __forceinline__ void build_tail(const uint8_t* p, uint64_t len, uint6
     w[j] = x;
   }
   if (blk == nblocks(len) - 1) {
-    const uint64_t bits = len << 3;
     w[14] = uint32_t(bits >> 32);
     w[15] = uint32_t(bits);
   }

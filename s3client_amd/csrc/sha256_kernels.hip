@@ -18,29 +18,52 @@
 //   sha256_lane_kernel (fused) -- one lane does schedule + rounds; no LDS, 8 waves/SIMD.
 //       Used when parts are plentiful enough to saturate every SIMD (>= ~128K parts).
 //
-// Both kernels are resumable: a launch processes blocks [blk_begin, blk_end) of every part,
-// loading/saving the 8-word chaining state in `state` (slot order) between launches.  The
-// device-resident path is one launch over [0, max); the host path streams slices.
+// All kernels are resumable: a launch processes blocks [blk_begin, blk_end) of every part,
+// loading/saving the 8-word chaining state in `state` (message order) between launches.  The
+// device-resident path is one launch over [0, max); the host path streams slices; the
+// multi-object stream (s3h_stream_*) runs unpadded launches over appended whole blocks
+// (kNoPad | kResume) and a final padded launch with each message's total bit length.
 #include "sha256_device.hpp"
 
 namespace s3h {
 
+// LaunchArgs::flags
+constexpr uint32_t kNoPad = 1;   // hash only the slot's whole 64-B blocks; never pad or emit
+constexpr uint32_t kResume = 2;  // load the chaining state even at blk_begin == 0
+
 struct LaunchArgs {
   const uint8_t* base;       // part p's block b is at base + slots[p].off + 64*(b - blk_origin)
   const Slot* slots;         // sorted by nblocks descending
-  const uint32_t* out_idx;   // slot -> output part index
-  uint32_t* state;           // n*8 words (slot order); may be null for single-launch plans
+  const uint32_t* out_idx;   // slot -> output part (message) index
+  uint32_t* state;           // n*8 words (message order); may be null for single-launch plans
   uint32_t* digests;         // n*8 words (part order), bswap32(H_i) like lib/hash to_little
   const uint8_t* zero;       // 256 zero bytes: target of the loads of out-of-range lanes
+  const uint64_t* bits;      // per-message bit length for the padding (null: 8 * slot length)
   uint64_t blk_begin, blk_end, blk_origin;
   uint32_t n;
+  uint32_t flags;
 };
 
+// Compressions the launch sequence runs for a slot of `len` bytes.
+__device__ __forceinline__ uint64_t slot_blocks(const LaunchArgs& A, uint64_t len) {
+  return (A.flags & kNoPad) ? (len >> 6) : nblocks(len);
+}
+__device__ __forceinline__ bool resumes(const LaunchArgs& A) {
+  return A.state != nullptr && (A.blk_begin > 0 || (A.flags & kResume));
+}
+// The chain of a slot with `nb` blocks ends inside this launch and its digest is written.
+__device__ __forceinline__ bool emits(const LaunchArgs& A, uint64_t nb) {
+  return !(A.flags & kNoPad) && nb <= A.blk_end;
+}
+__device__ __forceinline__ uint64_t msg_bits(const LaunchArgs& A, uint32_t slot, uint64_t len) {
+  return A.bits ? A.bits[A.out_idx[slot]] : len << 3;
+}
+
 __device__ __forceinline__ void load_state(const LaunchArgs& A, uint32_t slot, uint32_t st[8]) {
-  if (A.blk_begin == 0 || A.state == nullptr) {
+  if (!resumes(A)) {
     init_state(st);
   } else {
-    const uint4* s = reinterpret_cast<const uint4*>(A.state + 8ull * slot);
+    const uint4* s = reinterpret_cast<const uint4*>(A.state + 8ull * A.out_idx[slot]);
     const uint4 x = s[0], y = s[1];
     st[0] = x.x; st[1] = x.y; st[2] = x.z; st[3] = x.w;
     st[4] = y.x; st[5] = y.y; st[6] = y.z; st[7] = y.w;
@@ -49,12 +72,12 @@ __device__ __forceinline__ void load_state(const LaunchArgs& A, uint32_t slot, u
 
 __device__ __forceinline__ void store_result(const LaunchArgs& A, uint32_t slot, uint64_t nb,
                                              const uint32_t st[8]) {
-  if (nb <= A.blk_end) {  // chain finished inside this launch: emit the digest
+  if (emits(A, nb)) {  // chain finished inside this launch: emit the digest
     uint4* o = reinterpret_cast<uint4*>(A.digests + 8ull * A.out_idx[slot]);
     o[0] = make_uint4(bswap(st[0]), bswap(st[1]), bswap(st[2]), bswap(st[3]));
     o[1] = make_uint4(bswap(st[4]), bswap(st[5]), bswap(st[6]), bswap(st[7]));
   } else if (A.state) {
-    uint4* s = reinterpret_cast<uint4*>(A.state + 8ull * slot);
+    uint4* s = reinterpret_cast<uint4*>(A.state + 8ull * A.out_idx[slot]);
     s[0] = make_uint4(st[0], st[1], st[2], st[3]);
     s[1] = make_uint4(st[4], st[5], st[6], st[7]);
   }
@@ -71,15 +94,15 @@ __device__ __forceinline__ uint64_t fetch_end(uint64_t len, uint64_t blk_end) {
 // Blocks at or past `limit` (the launch's blk_end) are never consumed; they are zero-filled
 // without touching memory (the pair producer's odd lanes can step one block past the range).
 __device__ __forceinline__ void make_block(const RawBlock& r, uint32_t sel, const uint8_t* p,
-                                           uint64_t len, uint64_t blk, uint64_t limit,
-                                           uint32_t w[16]) {
+                                           uint64_t len, uint64_t bits, uint64_t blk,
+                                           uint64_t limit, uint32_t w[16]) {
   if (blk >= limit) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) w[j] = 0;
   } else if (blk < (len >> 6)) {
     decode_full(r, sel, w);
   } else {
-    build_tail(p, len, blk, w);
+    build_tail(p, len, bits, blk, w);
   }
 }
 
@@ -88,8 +111,9 @@ __global__ __launch_bounds__(256) void sha256_lane_kernel(LaunchArgs A) {
   const uint32_t slot = blockIdx.x * 256u + threadIdx.x;
   if (slot >= A.n) return;
   const Slot s = A.slots[slot];
-  const uint64_t nb = nblocks(s.len);
+  const uint64_t nb = slot_blocks(A, s.len);
   if (nb <= A.blk_begin) return;  // finished in an earlier launch
+  const uint64_t bits = msg_bits(A, slot, s.len);
   const uint64_t end = nb < A.blk_end ? nb : A.blk_end;
   uint32_t st[8];
   load_state(A, slot, st);
@@ -104,7 +128,7 @@ __global__ __launch_bounds__(256) void sha256_lane_kernel(LaunchArgs A) {
     RawBlock nxt;
     fetch_full(p + 64, b + 1 < fend, A.zero, nxt);  // prefetch one block ahead
     uint32_t w[16], wk[64];
-    make_block(cur, sel, p, s.len, b, A.blk_end, w);
+    make_block(cur, sel, p, s.len, bits, b, A.blk_end, w);
     schedule_wk(w, wk);
     uint32_t t[8];
 #pragma unroll
@@ -122,10 +146,10 @@ __global__ __launch_bounds__(256) void sha256_lane_kernel(LaunchArgs A) {
 // Decode + pad + schedule one block and store W[t]+K[t] as 16 x 16 B rows of LDS.
 template <int kRow>
 __device__ __forceinline__ void produce_block(const RawBlock& r, uint32_t sel, const uint8_t* bp,
-                                              uint64_t len, uint64_t blk, uint64_t limit,
-                                              uint4 (*buf)[kRow], uint32_t lane) {
+                                              uint64_t len, uint64_t bits, uint64_t blk,
+                                              uint64_t limit, uint4 (*buf)[kRow], uint32_t lane) {
   uint32_t w[16], wk[64];
-  make_block(r, sel, bp, len, blk, limit, w);
+  make_block(r, sel, bp, len, bits, blk, limit, w);
   schedule_wk(w, wk);
 #pragma unroll
   for (int q = 0; q < 16; ++q)
@@ -144,10 +168,10 @@ __global__ __launch_bounds__(kPcThreads) void sha256_pc_kernel(LaunchArgs A) {
   const bool valid = slot < A.n;
   Slot s = {0, 0};
   if (valid) s = A.slots[slot];
-  const uint64_t nb = valid ? nblocks(s.len) : 0;
+  const uint64_t nb = valid ? slot_blocks(A, s.len) : 0;
   // Slots are sorted by block count, so the workgroup's first slot bounds the loop; the
   // trip count is identical in both waves, so their s_barrier counts match.
-  const uint64_t wg_nb = nblocks(A.slots[slot0].len);
+  const uint64_t wg_nb = slot_blocks(A, A.slots[slot0].len);
   const uint64_t wg_end = wg_nb < A.blk_end ? wg_nb : A.blk_end;
   if (wg_end <= A.blk_begin) return;  // whole workgroup done in earlier launches
   const uint64_t iters = wg_end - A.blk_begin;
@@ -161,23 +185,24 @@ __global__ __launch_bounds__(kPcThreads) void sha256_pc_kernel(LaunchArgs A) {
     const uint8_t* p = A.base + s.off + 64ull * (b0 - A.blk_origin);
     const uint32_t sel = be_selector(uint32_t(reinterpret_cast<uintptr_t>(p) & 3));
     const uint64_t fend = fetch_end(s.len, A.blk_end);
+    const uint64_t bits = valid ? msg_bits(A, slot, s.len) : 0;
     RawBlock ra, rb;
     fetch_full(p, b0 < fend, A.zero, ra);
     fetch_full(p + 64, b0 + 1 < fend, A.zero, rb);
-    produce_block(ra, sel, p, s.len, b0, A.blk_end, lds_wk[0], lane);
+    produce_block(ra, sel, p, s.len, bits, b0, A.blk_end, lds_wk[0], lane);
     __syncthreads();
     for (uint64_t k = 1; k <= iters; k += 2) {
       // odd step: block b0+k from rb into buffer 1; refill ra with block b0+k+1
       if (k < iters) {
         fetch_full(p + 64 * (k + 1), b0 + k + 1 < fend, A.zero, ra);
-        produce_block(rb, sel, p + 64 * k, s.len, b0 + k, A.blk_end, lds_wk[1], lane);
+        produce_block(rb, sel, p + 64 * k, s.len, bits, b0 + k, A.blk_end, lds_wk[1], lane);
       }
       __syncthreads();
       if (k + 1 > iters) break;
       // even step: block b0+k+1 from ra into buffer 0; refill rb with block b0+k+2
       if (k + 1 < iters) {
         fetch_full(p + 64 * (k + 2), b0 + k + 2 < fend, A.zero, rb);
-        produce_block(ra, sel, p + 64 * (k + 1), s.len, b0 + k + 1, A.blk_end, lds_wk[0], lane);
+        produce_block(ra, sel, p + 64 * (k + 1), s.len, bits, b0 + k + 1, A.blk_end, lds_wk[0], lane);
       }
       __syncthreads();
     }
@@ -273,7 +298,7 @@ __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A)
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t slot0 = blockIdx.x * kPairParts;
   const uint64_t b0 = A.blk_begin;
-  const uint64_t wg_nb = nblocks(A.slots[slot0].len);
+  const uint64_t wg_nb = slot_blocks(A, A.slots[slot0].len);
   const uint64_t wg_end = wg_nb < A.blk_end ? wg_nb : A.blk_end;
   if (wg_end <= b0) return;
   const uint64_t iters = wg_end - b0;          // blocks this launch, uniform in the workgroup
@@ -289,21 +314,22 @@ __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A)
     const uint32_t sel = be_selector(uint32_t(reinterpret_cast<uintptr_t>(A.base + s.off) & 3));
     const uint64_t fend = fetch_end(s.len, A.blk_end);
     const uint64_t bh = b0 + half;  // this lane's first block
+    const uint64_t bits = slot < A.n ? msg_bits(A, slot, s.len) : 0;
     RawBlock ra, rb;
     fetch_full(p, bh < fend, A.zero, ra);
     fetch_full(p + 128, bh + 2 < fend, A.zero, rb);
-    produce_block(ra, sel, p, s.len, bh, A.blk_end, lds_wk[0][half], part);
+    produce_block(ra, sel, p, s.len, bits, bh, A.blk_end, lds_wk[0][half], part);
     __syncthreads();
     for (uint64_t k = 1; k <= steps; k += 2) {
       if (k < steps) {
         fetch_full(p + 128 * (k + 1), bh + 2 * (k + 1) < fend, A.zero, ra);
-        produce_block(rb, sel, p + 128 * k, s.len, bh + 2 * k, A.blk_end, lds_wk[1][half], part);
+        produce_block(rb, sel, p + 128 * k, s.len, bits, bh + 2 * k, A.blk_end, lds_wk[1][half], part);
       }
       __syncthreads();
       if (k + 1 > steps) break;
       if (k + 1 < steps) {
         fetch_full(p + 128 * (k + 2), bh + 2 * (k + 2) < fend, A.zero, rb);
-        produce_block(ra, sel, p + 128 * (k + 1), s.len, bh + 2 * (k + 1), A.blk_end, lds_wk[0][half], part);
+        produce_block(ra, sel, p + 128 * (k + 1), s.len, bits, bh + 2 * (k + 1), A.blk_end, lds_wk[0][half], part);
       }
       __syncthreads();
     }
@@ -314,13 +340,13 @@ __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A)
     const bool ahalf = pair_is_ahalf(lane);
     const uint32_t slot = slot0 + part;
     const bool valid = slot < A.n;
-    const uint64_t nb = valid ? nblocks(A.slots[slot].len) : 0;
+    const uint64_t nb = valid ? slot_blocks(A, A.slots[slot].len) : 0;
     const uint32_t sh1 = ahalf ? 2u : 6u, sh2 = ahalf ? 13u : 11u, sh3 = ahalf ? 22u : 25u;
     const uint32_t msk = ahalf ? 0xffffffffu : 0u;
     const uint32_t w0 = ahalf ? 0u : 4u;  // which half of the chaining state this lane holds
     uint32_t s0, s1, s2, s3;
-    if (valid && b0 > 0 && A.state) {
-      const uint4 v = reinterpret_cast<const uint4*>(A.state + 8ull * slot + w0)[0];
+    if (valid && resumes(A)) {
+      const uint4 v = reinterpret_cast<const uint4*>(A.state + 8ull * A.out_idx[slot] + w0)[0];
       s0 = v.x; s1 = v.y; s2 = v.z; s3 = v.w;
     } else {
       s0 = ahalf ? 0x6a09e667u : 0x510e527fu;
@@ -332,7 +358,7 @@ __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A)
     uint32_t q1, q2, q3, q4;
     // Slots are sorted by length: every lane is live for blocks below the last slot's count.
     const uint32_t last = (slot0 + kPairParts <= A.n ? slot0 + kPairParts : A.n) - 1;
-    const uint64_t all_live_end = nblocks(A.slots[last].len);
+    const uint64_t all_live_end = slot_blocks(A, A.slots[last].len);
     auto block = [&](const uint32_t wk[64], uint64_t i) {
       const uint32_t t0 = s0, t1 = s1, t2 = s2, t3 = s3;
       asm volatile(
@@ -372,11 +398,11 @@ __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A)
       __syncthreads();
     }
     if (valid && nb > b0) {
-      if (nb <= A.blk_end) {
+      if (emits(A, nb)) {
         uint4* o = reinterpret_cast<uint4*>(A.digests + 8ull * A.out_idx[slot] + w0);
         o[0] = make_uint4(bswap(s0), bswap(s1), bswap(s2), bswap(s3));
       } else if (A.state) {
-        reinterpret_cast<uint4*>(A.state + 8ull * slot + w0)[0] = make_uint4(s0, s1, s2, s3);
+        reinterpret_cast<uint4*>(A.state + 8ull * A.out_idx[slot] + w0)[0] = make_uint4(s0, s1, s2, s3);
       }
     }
   }
@@ -393,8 +419,8 @@ __device__ __forceinline__ uint32_t le_selector(uint32_t sh) {
   return ((sh + 3) << 24) | ((sh + 2) << 16) | ((sh + 1) << 8) | sh;
 }
 
-__device__ __forceinline__ void md5_tail(const uint8_t* p, uint64_t len, uint64_t blk,
-                                         uint32_t w[16]) {
+__device__ __forceinline__ void md5_tail(const uint8_t* p, uint64_t len, uint64_t bits,
+                                         uint64_t blk, uint32_t w[16]) {
   const uint64_t nfull = len >> 6;
   const int rem = (blk == nfull) ? int(len & 63) : -1;
 #pragma unroll
@@ -411,7 +437,6 @@ __device__ __forceinline__ void md5_tail(const uint8_t* p, uint64_t len, uint64_
     w[j] = x;
   }
   if (blk == nblocks(len) - 1) {
-    const uint64_t bits = len << 3;
     w[14] = uint32_t(bits);
     w[15] = uint32_t(bits >> 32);
   }
@@ -474,8 +499,8 @@ __device__ __forceinline__ void md5_steps(uint32_t& a, uint32_t& b, uint32_t& c,
 }
 
 __device__ __forceinline__ void md5_produce(const RawBlock& r, uint32_t sel, const uint8_t* bp,
-                                            uint64_t len, uint64_t blk, uint64_t limit,
-                                            uint4 (*buf)[64], uint32_t lane) {
+                                            uint64_t len, uint64_t bits, uint64_t blk,
+                                            uint64_t limit, uint4 (*buf)[64], uint32_t lane) {
   uint32_t w[16];
   if (blk >= limit) {
 #pragma unroll
@@ -484,7 +509,7 @@ __device__ __forceinline__ void md5_produce(const RawBlock& r, uint32_t sel, con
 #pragma unroll
     for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_perm(r.d[j + 1], r.d[j], sel);
   } else {
-    md5_tail(bp, len, blk, w);
+    md5_tail(bp, len, bits, blk, w);
   }
   uint32_t km[64];
 #pragma unroll
@@ -503,8 +528,8 @@ __global__ __launch_bounds__(kPcThreads) void md5_pc_kernel(LaunchArgs A) {
   const bool valid = slot < A.n;
   Slot s = {0, 0};
   if (valid) s = A.slots[slot];
-  const uint64_t nb = valid ? nblocks(s.len) : 0;
-  const uint64_t wg_nb = nblocks(A.slots[slot0].len);
+  const uint64_t nb = valid ? slot_blocks(A, s.len) : 0;
+  const uint64_t wg_nb = slot_blocks(A, A.slots[slot0].len);
   const uint64_t wg_end = wg_nb < A.blk_end ? wg_nb : A.blk_end;
   if (wg_end <= A.blk_begin) return;
   const uint64_t iters = wg_end - A.blk_begin;
@@ -517,16 +542,17 @@ __global__ __launch_bounds__(kPcThreads) void md5_pc_kernel(LaunchArgs A) {
     const uint8_t* p = A.base + s.off + 64ull * (b0 - A.blk_origin);
     const uint32_t sel = le_selector(uint32_t(reinterpret_cast<uintptr_t>(p) & 3));
     const uint64_t fend = fetch_end(s.len, A.blk_end);
+    const uint64_t bits = valid ? msg_bits(A, slot, s.len) : 0;
     RawBlock ra, rb, rc;
     fetch_full(p, b0 < fend, A.zero, ra);
     fetch_full(p + 64, b0 + 1 < fend, A.zero, rb);
     fetch_full(p + 128, b0 + 2 < fend, A.zero, rc);
-    md5_produce(ra, sel, p, s.len, b0, A.blk_end, lds_km[0], lane);
+    md5_produce(ra, sel, p, s.len, bits, b0, A.blk_end, lds_km[0], lane);
     __syncthreads();
 #define S3H_MD5_PSTEP(J, NEXT, CUR)                                                        \
     if ((J) < iters) {                                                                     \
       fetch_full(p + 64 * ((J) + 2), b0 + (J) + 2 < fend, A.zero, NEXT);                    \
-      md5_produce(CUR, sel, p + 64 * (J), s.len, b0 + (J), A.blk_end, lds_km[(J) & 1], lane); \
+      md5_produce(CUR, sel, p + 64 * (J), s.len, bits, b0 + (J), A.blk_end, lds_km[(J) & 1], lane); \
     }                                                                                      \
     __syncthreads();                                                                       \
     if ((J) + 1 > iters) break;
@@ -539,8 +565,8 @@ __global__ __launch_bounds__(kPcThreads) void md5_pc_kernel(LaunchArgs A) {
   } else {
     __builtin_amdgcn_s_setprio(3);
     uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
-    if (valid && A.blk_begin > 0 && A.state) {
-      const uint4 v = reinterpret_cast<const uint4*>(A.state + 8ull * slot)[0];
+    if (valid && resumes(A)) {
+      const uint4 v = reinterpret_cast<const uint4*>(A.state + 8ull * A.out_idx[slot])[0];
       st[0] = v.x; st[1] = v.y; st[2] = v.z; st[3] = v.w;
     }
     __syncthreads();
@@ -561,11 +587,12 @@ __global__ __launch_bounds__(kPcThreads) void md5_pc_kernel(LaunchArgs A) {
       __syncthreads();
     }
     if (valid && nb > A.blk_begin) {
-      if (nb <= A.blk_end)
+      if (emits(A, nb))
         reinterpret_cast<uint4*>(A.digests + 4ull * A.out_idx[slot])[0] =
             make_uint4(st[0], st[1], st[2], st[3]);
       else if (A.state)
-        reinterpret_cast<uint4*>(A.state + 8ull * slot)[0] = make_uint4(st[0], st[1], st[2], st[3]);
+        reinterpret_cast<uint4*>(A.state + 8ull * A.out_idx[slot])[0] =
+            make_uint4(st[0], st[1], st[2], st[3]);
     }
   }
 }
@@ -583,6 +610,50 @@ __global__ __launch_bounds__(256) void compare_digests_kernel(const uint32_t* go
   for (uint32_t w = 0; w < words; ++w) diff |= got[words * i + w] ^ want[words * i + w];
   mismatch[i] = diff != 0;
   if (diff) atomicAdd(count, 1ull);
+}
+
+// ------------------------------------------------------------- multi-object streams
+// Carry bookkeeping of one s3h_stream update, one thread per message (<= 127 bytes moved):
+//   kSpliceHead : head[i] = carry[i][0:c] ++ chunk[0:h]   (c + h == 64: the block that
+//                 straddles the previous update and this one, hashed by the head launch)
+//   kSpliceGrow : carry[i][c:c+h] = chunk[0:h]           (still < 64 B buffered)
+//   kSpliceReset: carry[i][0:r] = chunk[tail:tail+r]     (the new < 64-B remainder)
+// The head block is built before the carry is overwritten (same thread, program order).
+struct SpliceJob {
+  uint64_t src, tail;  // chunk start / new-remainder start, offsets from the update's base
+  uint32_t c, h, r, mode;
+};
+constexpr uint32_t kSpliceHead = 1, kSpliceGrow = 2, kSpliceReset = 4;
+
+__global__ __launch_bounds__(256) void stream_splice_kernel(const uint8_t* base,
+                                                            const SpliceJob* jobs, uint8_t* carry,
+                                                            uint8_t* head, uint64_t n) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (i >= n) return;
+  const SpliceJob j = jobs[i];
+  uint8_t* cy = carry + 64 * i;
+  if (j.mode & kSpliceHead) {
+    uint8_t* hb = head + 64 * i;
+    for (uint32_t k = 0; k < j.c; ++k) hb[k] = cy[k];
+    for (uint32_t k = 0; k < j.h; ++k) hb[j.c + k] = base[j.src + k];
+  }
+  if (j.mode & kSpliceGrow)
+    for (uint32_t k = 0; k < j.h; ++k) cy[j.c + k] = base[j.src + k];
+  if (j.mode & kSpliceReset)
+    for (uint32_t k = 0; k < j.r; ++k) cy[k] = base[j.tail + k];
+}
+
+// Chaining state of n empty messages (8-word stride for both algorithms).
+__global__ __launch_bounds__(256) void stream_init_kernel(uint32_t* state, uint64_t n, int md5) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (i >= n) return;
+  uint4* s = reinterpret_cast<uint4*>(state + 8 * i);
+  if (md5) {
+    s[0] = make_uint4(0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u);
+  } else {
+    s[0] = make_uint4(0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au);
+    s[1] = make_uint4(0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u);
+  }
 }
 
 // ------------------------------------------------------------- synthetic input generator

@@ -197,10 +197,82 @@ def verify_batch_device(data, offsets, lengths, expected, algo: str = "sha256", 
 
 
 def multipart_etag(part_md5s) -> str:
-    """S3 multipart ETag: hex(MD5(concatenated binary part MD5s)) + "-" + part count."""
-    import hashlib
+    """S3 multipart ETag: hex(MD5(concatenated binary part MD5s)) + "-" + part count.
+    The outer MD5 (16 B per part) runs on the lib/hash MD5 drop-in."""
     w = np.ascontiguousarray(part_md5s, dtype=np.uint32).reshape(-1, 4)
-    return hashlib.md5(w.tobytes()).hexdigest() + f"-{w.shape[0]}"
+    return md5(w.tobytes()).tobytes().hex() + f"-{w.shape[0]}"
+
+
+class Stream:
+    """n messages (objects) hashed incrementally on the GPU as chunks arrive
+    (s3h_stream_*, include/s3hash.h): sha256_stream semantics per append and the documented
+    sha256_next contract (lib/hash/sha256.h:73-89) at ``final()`` -- the digest of the
+    concatenation of every chunk appended since the previous ``final()``.
+
+    ``update(chunks)`` takes one chunk per message: host ``bytes``/numpy arrays (blocking),
+    or, with ``update_device``, a device tensor plus offsets/lengths (asynchronous)."""
+
+    def __init__(self, n: int, device: int = 0, algo: str = "sha256", kernel: str | int = "auto"):
+        k = kernel if isinstance(kernel, int) else _native.KERNEL_IDS[kernel]
+        self.algo = _native.ALGO_IDS[algo]
+        self.words = _native.DIGEST_WORDS[self.algo]
+        self.n, self.device = int(n), device
+        h = ctypes.c_void_p()
+        check(lib().s3h_stream_create(device, self.algo, self.n, k, ctypes.byref(h)))
+        self._h = h
+
+    def update(self, chunks: Sequence) -> None:
+        if len(chunks) != self.n:
+            raise ValueError(f"need one chunk per message ({self.n})")
+        arrs = [np.frombuffer(c, dtype=np.uint8) if isinstance(c, (bytes, bytearray, memoryview))
+                else np.ascontiguousarray(c, dtype=np.uint8).reshape(-1) for c in chunks]
+        ptrs = (ctypes.c_void_p * self.n)(*[a.ctypes.data if a.size else 0 for a in arrs])
+        lens = _u64([a.size for a in arrs])
+        check(lib().s3h_stream_update_host(self._h, ptrs, _p64(lens)))
+
+    def update_device(self, data, offsets, lengths, stream=None) -> None:
+        offs, lens = _u64(offsets), _u64(lengths)
+        if offs.size != self.n or lens.size != self.n:
+            raise ValueError(f"need one chunk per message ({self.n})")
+        if lens.any() and int((offs + lens)[lens > 0].max()) > data.numel() * data.element_size():
+            raise ValueError("chunk extends past the data tensor")
+        check(lib().s3h_stream_update_device(self._h, ctypes.c_void_p(data.data_ptr()),
+                                             _p64(offs), _p64(lens),
+                                             ctypes.c_void_p(_stream_handle(stream))))
+
+    def final(self) -> np.ndarray:
+        """(n, words) uint32 digests; the object restarts with n empty messages."""
+        out = np.zeros((self.n, self.words), dtype=np.uint32)
+        check(lib().s3h_stream_final_host(self._h, out.ctypes.data))
+        return out
+
+    def final_device(self, digests, stream=None) -> None:
+        if digests.numel() * digests.element_size() < 4 * self.words * self.n:
+            raise ValueError("digests buffer too small")
+        check(lib().s3h_stream_final_device(self._h, ctypes.c_void_p(digests.data_ptr()),
+                                            ctypes.c_void_p(_stream_handle(stream))))
+
+    def total(self, i: int) -> int:
+        t = ctypes.c_uint64()
+        check(lib().s3h_stream_total(self._h, i, ctypes.byref(t)))
+        return t.value
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().s3h_stream_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def sha256_batch_host(parts: Sequence, ndevices: int = 0, slice_bytes: int = 0) -> np.ndarray:

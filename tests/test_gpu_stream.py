@@ -1,0 +1,132 @@
+"""GPU parity of the multi-object stream (s3h_stream_*).
+
+A stream appends chunks to n messages and finishes them with the documented sha256_next
+contract (lib/hash/sha256.h:73-89): the digest must equal the one-shot digest of the
+concatenation of every chunk (oracle_sha256 / oracle_md5 over the joined bytes), bit-exact,
+for every chunk schedule -- empty chunks, chunks that stay inside one block, chunks that
+complete a carried block exactly, multi-block chunks at any alignment."""
+import numpy as np
+import pytest
+
+import s3client_amd as s3
+
+pytestmark = pytest.mark.gpu
+KERNELS = ["pair", "pc", "lane"]
+
+
+def _schedule(rng, n, rounds, maxlen):
+    """Per-round chunk lengths with the carry edge cases mixed in."""
+    special = np.array([0, 1, 3, 55, 56, 63, 64, 65, 127, 128, 129, 200])
+    out = []
+    for _ in range(rounds):
+        lens = rng.integers(0, maxlen, n)
+        pick = rng.random(n) < 0.5
+        lens[pick] = rng.choice(special, int(pick.sum()))
+        out.append(lens)
+    return out
+
+
+def _oracle_digest(oracle, algo, data: bytes):
+    return oracle.sha256(data) if algo == "sha256" else oracle.md5(data)
+
+
+def _check_stream(oracle, algo, kernel, n, rounds, maxlen, seed, finals=2):
+    rng = np.random.default_rng(seed)
+    with s3.Stream(n, algo=algo, kernel=kernel) as st:
+        for f in range(finals):
+            msgs = [bytearray() for _ in range(n)]
+            for lens in _schedule(rng, n, rounds, maxlen):
+                chunks = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in lens]
+                st.update(chunks)
+                for i, c in enumerate(chunks):
+                    msgs[i] += c
+            assert all(st.total(i) == len(msgs[i]) for i in range(n))
+            got = st.final()
+            want = np.stack([_oracle_digest(oracle, algo, bytes(m)) for m in msgs])
+            bad = [i for i in range(n) if not np.array_equal(got[i], want[i])]
+            assert not bad, (f, bad[:8], [len(msgs[i]) for i in bad[:8]])
+            assert all(st.total(i) == 0 for i in range(n))  # final() restarts the messages
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_stream_sha256_random_schedules(torch_cuda, oracle, kernel):
+    _check_stream(oracle, "sha256", kernel, n=150, rounds=6, maxlen=3000, seed=11)
+
+
+def test_stream_md5_random_schedules(torch_cuda, oracle):
+    _check_stream(oracle, "md5", "auto", n=150, rounds=6, maxlen=3000, seed=12)
+
+
+def test_stream_empty_messages(torch_cuda, oracle):
+    """No update at all / only empty chunks: the digest of the empty message."""
+    with s3.Stream(5) as st:
+        got = st.final()
+        st.update([b""] * 5)
+        got2 = st.final()
+    want = oracle.sha256(b"")
+    assert all(np.array_equal(g, want) for g in got) and np.array_equal(got, got2)
+    with s3.Stream(3, algo="md5") as st:
+        assert all(np.array_equal(g, oracle.md5(b"")) for g in st.final())
+
+
+def test_stream_device_chunks_unaligned(torch_cuda, oracle):
+    """update_device: chunks at arbitrary offsets of a device tensor, final into HBM."""
+    torch = torch_cuda
+    rng = np.random.default_rng(5)
+    n, rounds = 64, 5
+    msgs = [bytearray() for _ in range(n)]
+    with s3.Stream(n) as st:
+        for lens in _schedule(rng, n, rounds, 70000):
+            gaps = rng.integers(0, 8, n)
+            offs = np.cumsum(gaps + np.concatenate([[0], lens[:-1]]))
+            host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 1, dtype=np.uint8)
+            data = torch.from_numpy(host).cuda()
+            st.update_device(data, offs, lens)
+            torch.cuda.synchronize()
+            for i in range(n):
+                msgs[i] += host[offs[i]:offs[i] + lens[i]].tobytes()
+        out = torch.zeros((n, 8), dtype=torch.int32, device="cuda")
+        st.final_device(out)
+        torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    want = np.stack([oracle.sha256(bytes(m)) for m in msgs])
+    assert np.array_equal(got, want)
+
+
+def test_stream_large_objects_match_batch(torch_cuda, oracle, golden):
+    """Eight 8 MiB C2 parts streamed in ragged chunks (1 B .. 3 MiB) hash to the golden
+    one-shot digests of lib/hash (tests/golden c2_parts)."""
+    parts = golden["c2_parts"][:8]
+    bufs = [np.frombuffer(oracle.generate(p["p"], p["L"]), dtype=np.uint8) for p in parts]
+    rng = np.random.default_rng(9)
+    pos = [0] * len(bufs)
+    with s3.Stream(len(bufs)) as st:
+        while any(pos[i] < bufs[i].size for i in range(len(bufs))):
+            chunks = []
+            for i, b in enumerate(bufs):
+                L = int(rng.choice([1, 63, 64, 4097, 1 << 20, 3 << 20]))
+                chunks.append(b[pos[i]:pos[i] + L])
+                pos[i] = min(pos[i] + L, b.size)
+            st.update(chunks)
+        got = s3.digests_to_text(st.final())
+    assert got == [p["digest"] for p in parts]
+
+
+def test_stream_many_messages_pc_lane_policy(torch_cuda, oracle):
+    """n above the pair/pc thresholds: AUTO picks pc / lane plans for the stream too."""
+    rng = np.random.default_rng(3)
+    n = 70000
+    lens1 = rng.integers(0, 150, n)
+    lens2 = rng.integers(0, 150, n)
+    base1 = rng.integers(0, 256, int(lens1.sum()), dtype=np.uint8)
+    base2 = rng.integers(0, 256, int(lens2.sum()), dtype=np.uint8)
+    o1 = np.concatenate([[0], np.cumsum(lens1)[:-1]])
+    o2 = np.concatenate([[0], np.cumsum(lens2)[:-1]])
+    with s3.Stream(n) as st:
+        st.update([base1[o1[i]:o1[i] + lens1[i]] for i in range(n)])
+        st.update([base2[o2[i]:o2[i] + lens2[i]] for i in range(n)])
+        got = st.final()
+    idx = rng.choice(n, 400, replace=False)
+    for i in idx:
+        m = base1[o1[i]:o1[i] + lens1[i]].tobytes() + base2[o2[i]:o2[i] + lens2[i]].tobytes()
+        assert np.array_equal(got[i], oracle.sha256(m)), i
