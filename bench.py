@@ -51,8 +51,10 @@ def parse():
     ap.add_argument("--cpu-sample-parts", type=int, default=384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--slice-bytes", type=int, default=0, help="host mode: bytes per part per slice")
-    ap.add_argument("--mode", default="device", choices=["device", "host"],
-                    help="host: H2D-inclusive rate from pinned host memory (not the metric)")
+    ap.add_argument("--mode", default="device", choices=["device", "host", "stream"],
+                    help="host: H2D-inclusive rate from pinned host memory; stream: the parts "
+                         "appended chunk by chunk through s3h_stream_* (neither is the metric)")
+    ap.add_argument("--chunk-bytes", type=int, default=MIB, help="stream mode: bytes per append")
     return ap.parse_args()
 
 
@@ -177,6 +179,8 @@ def main():
 
     if args.mode == "host":
         return host_mode(args, s3, torch, dist, data, ids, lens, offs, world, rank, name)
+    if args.mode == "stream":
+        return stream_mode(args, s3, torch, data, ids, lens, offs, rank, name, stream)
 
     for _ in range(args.warmup):
         plan.launch(data, digests, stream)
@@ -302,6 +306,51 @@ def host_mode(args, s3, torch, dist, data, ids, lens, offs, world, rank, name):
                           "n_gpus": 1, "steps": args.steps,
                           "config": {"workload": name, "slice_bytes": args.slice_bytes or "auto"},
                           "fixture_mismatches": int(bad), "ms_per_batch": round(wall * 1e3, 2)}))
+    return 0
+
+
+def stream_mode(args, s3, torch, data, ids, lens, offs, rank, name, stream):
+    """Each part as one streamed object: appended in --chunk-bytes chunks (any size, so the
+    carried partial blocks are exercised when it is not a multiple of 64), then finished."""
+    n = len(lens)
+    algo = args.algo
+    st = s3.Stream(n, device=torch.cuda.current_device(), algo=algo, kernel=args.kernel)
+    out = torch.zeros((n, st.words), dtype=torch.int32, device=data.device)
+    cb = args.chunk_bytes
+    nupd = int((int(lens.max()) + cb - 1) // cb)
+
+    def one_object_pass():
+        for k in range(nupd):
+            lk = np.minimum(np.maximum(lens.astype(np.int64) - k * cb, 0), cb).astype(np.uint64)
+            st.update_device(data, offs + np.uint64(k * cb), lk, stream)
+        st.final_device(out, stream)
+
+    for _ in range(args.warmup):
+        one_object_pass()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_object_pass()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / max(1, args.steps)
+    gd = out.cpu().numpy().view(np.uint32)
+    with open(os.path.join(ROOT, "tests", "golden", "sha256_golden.json")) as f:
+        gold = json.load(f)
+    src = gold["c2_parts"] if algo == "sha256" else gold["md5"]["c2_parts"]
+    fixtures = {e["p"]: e["digest"] for e in src} if not args.part_bytes else {}
+    checked = [int(p) for p in ids if int(p) in fixtures]
+    bad = sum(s3.hash_to_text(gd[s]) != fixtures[int(p)]
+              for s, p in enumerate(ids) if int(p) in fixtures)
+    if rank == 0:
+        print(json.dumps({"metric": f"streamed-object {algo.upper()} GiB/s (s3h_stream_*, "
+                          "device-resident chunks; SURVEY 8(f).2, not the metric)",
+                          "value": round(float(lens.sum()) / 2**30 / wall, 3), "unit": "GiB/s",
+                          "n_gpus": 1, "steps": args.steps,
+                          "config": {"workload": name, "objects": n, "chunk_bytes": cb,
+                                     "updates_per_object": nupd},
+                          "parity": {"fixtures_checked": len(checked), "mismatches": int(bad)},
+                          "ms_per_pass": round(wall * 1e3, 2)}))
+    st.close()
     return 0
 
 
