@@ -119,7 +119,8 @@ int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* le
   }
   if (kernel == S3H_KERNEL_AUTO)
     kernel = n <= kPairMaxParts ? S3H_KERNEL_PAIR : n <= kPcMaxParts ? S3H_KERNEL_PC : S3H_KERNEL_LANE;
-  if (kernel != S3H_KERNEL_PC && kernel != S3H_KERNEL_LANE && kernel != S3H_KERNEL_PAIR)
+  if (kernel != S3H_KERNEL_PC && kernel != S3H_KERNEL_LANE && kernel != S3H_KERNEL_PAIR &&
+      kernel != S3H_KERNEL_QUAD)
     return fail(S3H_EINVAL, "plan: unknown kernel %d", kernel);
 
   std::vector<uint32_t> order(n);
@@ -135,6 +136,7 @@ int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* le
   P->max_blocks = s3h::nblocks(slots[0].len);
   P->grid = kernel == S3H_KERNEL_PC     ? uint32_t((n + 63) / 64)
             : kernel == S3H_KERNEL_PAIR ? uint32_t((n + s3h::kPairParts - 1) / s3h::kPairParts)
+            : kernel == S3H_KERNEL_QUAD ? uint32_t((n + s3h::kQuadParts - 1) / s3h::kQuadParts)
                                         : uint32_t((n + 255) / 256);
 
   DeviceGuard g(device);
@@ -176,6 +178,8 @@ int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t
     hipLaunchKernelGGL(s3h::md5_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_PC)
     hipLaunchKernelGGL(s3h::sha256_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_QUAD)
+    hipLaunchKernelGGL(s3h::sha256_quad_kernel, dim3(P->grid), dim3(s3h::kQuadThreads), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_PAIR)
     hipLaunchKernelGGL(s3h::sha256_pair_kernel, dim3(P->grid), dim3(s3h::kPairThreads), 0, stream, A);
   else

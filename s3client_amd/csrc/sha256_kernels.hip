@@ -408,6 +408,167 @@ __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A)
   }
 }
 
+// ------------------------------------------------------------- lane-quad kernel
+// Each half of a chain's state lives on a QUAD of lanes (one DPP bank): the e-quad (banks 0
+// and 2) holds e,f,g,h in all four lanes, the a-quad (banks 1 and 3, partner = lane + 4) holds
+// a,b,c,d.  Sigma needs one rotation per lane instead of three: lane k of a quad rotates by
+// its own amount (e: 6, 11, 25, 6; a: 2, 13, 22, 2) and two quad_perm v_xor_b32_dpp fold the
+// three rotations into every lane of the quad.  The rest of the round is the pair kernel's:
+// Ch and Maj as one bfi over a per-lane selector, the e-half's h+W+K precomputed, two
+// bank-masked adds exchanging T1 and d between the quads.  9 VALU per round instead of 10,
+// at 8 chains per wave (the chip has lanes to spare for every BASELINE config).
+// Hazards: the first xor_dpp reads the rotation 3 instructions after it is written (2 wait
+// states needed); the a-quad's exchange reads T1 two instructions after the add3.
+constexpr int kQuadThreads = 128;
+constexpr int kQuadParts = 8;
+
+#define S3H_QUAD_TXT(a, b, c, d, x, xn, wn)                                                   \
+  "v_alignbit_b32 %[q1], %[" #a "], %[" #a "], %[h1]\n\t"                                     \
+  "v_bitop3_b32 %[q4], %[" #a "], %[" #b "], %[m] bitop3:0xd2\n\t"                            \
+  "v_bfi_b32 %[q2], %[q4], %[" #b "], %[" #c "]\n\t"                                          \
+  "v_xor_b32_dpp %[q3], %[q1], %[q1] quad_perm:[1,2,0,1] row_mask:0xf bank_mask:0xf\n\t"     \
+  "v_xor_b32_dpp %[q3], %[q1], %[q3] quad_perm:[2,0,1,2] row_mask:0xf bank_mask:0xf\n\t"     \
+  "v_add3_u32 %[q3], %[" #x "], %[q3], %[q2]\n\t"                                             \
+  "v_add_u32_dpp %[" #xn "], %[" #c "], %[" #wn "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5\n\t" \
+  "v_add_u32_dpp %[" #d "], %[" #d "], %[q3] row_shl:4 row_mask:0xf bank_mask:0x5\n\t"       \
+  "v_add_u32_dpp %[" #d "], %[q3], %[q3] row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+
+#define S3H_QUAD_4TXT(wa, wb, wc, wd)                                                         \
+  S3H_QUAD_TXT(s0, s1, s2, s3, xa, xb, wa) S3H_QUAD_TXT(s3, s0, s1, s2, xb, xa, wb)              \
+  S3H_QUAD_TXT(s2, s3, s0, s1, xa, xb, wc) S3H_QUAD_TXT(s1, s2, s3, s0, xb, xa, wd)
+#define S3H_QUAD_16RND(WK, T)                                                                   \
+  asm volatile(S3H_QUAD_4TXT(w1, w2, w3, w4) S3H_QUAD_4TXT(w5, w6, w7, w8)                       \
+               S3H_QUAD_4TXT(w9, w10, w11, w12) S3H_QUAD_4TXT(w13, w14, w15, w16)               \
+               : [s0] "+v"(s0), [s1] "+v"(s1), [s2] "+v"(s2), [s3] "+v"(s3), [xa] "+v"(xa),    \
+                 [xb] "+v"(xb), [q1] "=&v"(q1), [q2] "=&v"(q2), [q3] "=&v"(q3), [q4] "=&v"(q4)  \
+               : [w1] "v"(WK[(T + 1) & 63]), [w2] "v"(WK[(T + 2) & 63]),                       \
+                 [w3] "v"(WK[(T + 3) & 63]), [w4] "v"(WK[(T + 4) & 63]),                       \
+                 [w5] "v"(WK[(T + 5) & 63]), [w6] "v"(WK[(T + 6) & 63]),                       \
+                 [w7] "v"(WK[(T + 7) & 63]), [w8] "v"(WK[(T + 8) & 63]),                       \
+                 [w9] "v"(WK[(T + 9) & 63]), [w10] "v"(WK[(T + 10) & 63]),                     \
+                 [w11] "v"(WK[(T + 11) & 63]), [w12] "v"(WK[(T + 12) & 63]),                   \
+                 [w13] "v"(WK[(T + 13) & 63]), [w14] "v"(WK[(T + 14) & 63]),                   \
+                 [w15] "v"(WK[(T + 15) & 63]), [w16] "v"(WK[(T + 16) & 63]), [h1] "v"(sh),     \
+                 [m] "v"(msk))
+
+__global__ __launch_bounds__(kQuadThreads) void sha256_quad_kernel(LaunchArgs A) {
+  __shared__ uint4 lds_wk[2][2][16][kQuadParts];  // [buffer][block in step][round group][part]
+
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t slot0 = blockIdx.x * kQuadParts;
+  const uint64_t b0 = A.blk_begin;
+  const uint64_t wg_nb = slot_blocks(A, A.slots[slot0].len);
+  const uint64_t wg_end = wg_nb < A.blk_end ? wg_nb : A.blk_end;
+  if (wg_end <= b0) return;
+  const uint64_t iters = wg_end - b0;
+  const uint64_t steps = (iters + 1) >> 1;
+
+  if (wave == 1) {
+    // ---------------------------------------------------------------- producer
+    // Lanes 0-15 carry (part, even/odd block); lanes 16-63 repeat them (same loads, same LDS
+    // writes), which keeps every lane on one branch-free path at no extra issue cost.
+    const uint32_t part = lane & 7u, half = (lane >> 3) & 1u;
+    const uint32_t slot = slot0 + part;
+    Slot s = {0, 0};
+    if (slot < A.n) s = A.slots[slot];
+    const uint8_t* p = A.base + s.off + 64ull * (b0 + half - A.blk_origin);
+    const uint32_t sel = be_selector(uint32_t(reinterpret_cast<uintptr_t>(A.base + s.off) & 3));
+    const uint64_t fend = fetch_end(s.len, A.blk_end);
+    const uint64_t bh = b0 + half;
+    const uint64_t bits = slot < A.n ? msg_bits(A, slot, s.len) : 0;
+    RawBlock ra, rb;
+    fetch_full(p, bh < fend, A.zero, ra);
+    fetch_full(p + 128, bh + 2 < fend, A.zero, rb);
+    produce_block(ra, sel, p, s.len, bits, bh, A.blk_end, lds_wk[0][half], part);
+    __syncthreads();
+    for (uint64_t k = 1; k <= steps; k += 2) {
+      if (k < steps) {
+        fetch_full(p + 128 * (k + 1), bh + 2 * (k + 1) < fend, A.zero, ra);
+        produce_block(rb, sel, p + 128 * k, s.len, bits, bh + 2 * k, A.blk_end, lds_wk[1][half], part);
+      }
+      __syncthreads();
+      if (k + 1 > steps) break;
+      if (k + 1 < steps) {
+        fetch_full(p + 128 * (k + 2), bh + 2 * (k + 2) < fend, A.zero, rb);
+        produce_block(ra, sel, p + 128 * (k + 1), s.len, bits, bh + 2 * (k + 1), A.blk_end, lds_wk[0][half], part);
+      }
+      __syncthreads();
+    }
+  } else {
+    // ---------------------------------------------------------------- consumer
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t part = (lane >> 4) * 2u + ((lane >> 3) & 1u);
+    const bool ahalf = (lane >> 2) & 1u;
+    const uint32_t k4 = lane & 3u;
+    const uint32_t slot = slot0 + part;
+    const bool valid = slot < A.n;
+    const uint64_t nb = valid ? slot_blocks(A, A.slots[slot].len) : 0;
+    const uint32_t sh = ahalf ? (k4 == 1 ? 13u : k4 == 2 ? 22u : 2u)
+                              : (k4 == 1 ? 11u : k4 == 2 ? 25u : 6u);
+    const uint32_t msk = ahalf ? 0xffffffffu : 0u;
+    const uint32_t w0 = ahalf ? 0u : 4u;
+    uint32_t s0, s1, s2, s3;
+    if (valid && resumes(A)) {
+      const uint4 v = reinterpret_cast<const uint4*>(A.state + 8ull * A.out_idx[slot] + w0)[0];
+      s0 = v.x; s1 = v.y; s2 = v.z; s3 = v.w;
+    } else {
+      s0 = ahalf ? 0x6a09e667u : 0x510e527fu;
+      s1 = ahalf ? 0xbb67ae85u : 0x9b05688cu;
+      s2 = ahalf ? 0x3c6ef372u : 0x1f83d9abu;
+      s3 = ahalf ? 0xa54ff53au : 0x5be0cd19u;
+    }
+    uint32_t xa = 0, xb = 0;
+    uint32_t q1, q2, q3, q4;
+    const uint32_t last = (slot0 + kQuadParts <= A.n ? slot0 + kQuadParts : A.n) - 1;
+    const uint64_t all_live_end = slot_blocks(A, A.slots[last].len);
+    auto block = [&](const uint32_t wk[64], uint64_t i) {
+      const uint32_t t0 = s0, t1 = s1, t2 = s2, t3 = s3;
+      asm volatile(
+          "s_nop 1\n\t"
+          "v_add_u32_dpp %0, %1, %2 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5"
+          : "+v"(xa) : "v"(s3), "v"(wk[0]));
+      S3H_QUAD_16RND(wk, 0);
+      S3H_QUAD_16RND(wk, 16);
+      S3H_QUAD_16RND(wk, 32);
+      S3H_QUAD_16RND(wk, 48);
+      if (b0 + i < all_live_end) {
+        s0 += t0; s1 += t1; s2 += t2; s3 += t3;
+      } else {
+        const bool live = (b0 + i) < nb;
+        s0 = live ? s0 + t0 : t0;
+        s1 = live ? s1 + t1 : t1;
+        s2 = live ? s2 + t2 : t2;
+        s3 = live ? s3 + t3 : t3;
+      }
+    };
+    __syncthreads();
+    for (uint64_t j = 0; j < steps; ++j) {
+      const bool second = 2 * j + 1 < iters;
+      uint32_t wk0[64], wk1[64];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const uint4 v = lds_wk[j & 1][0][q][part];
+        wk0[4 * q] = v.x; wk0[4 * q + 1] = v.y; wk0[4 * q + 2] = v.z; wk0[4 * q + 3] = v.w;
+        const uint4 u = lds_wk[j & 1][1][q][part];
+        wk1[4 * q] = u.x; wk1[4 * q + 1] = u.y; wk1[4 * q + 2] = u.z; wk1[4 * q + 3] = u.w;
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      block(wk0, 2 * j);
+      if (second) block(wk1, 2 * j + 1);
+      __syncthreads();
+    }
+    if (valid && nb > b0 && k4 == 0) {
+      if (emits(A, nb)) {
+        uint4* o = reinterpret_cast<uint4*>(A.digests + 8ull * A.out_idx[slot] + w0);
+        o[0] = make_uint4(bswap(s0), bswap(s1), bswap(s2), bswap(s3));
+      } else if (A.state) {
+        reinterpret_cast<uint4*>(A.state + 8ull * A.out_idx[slot] + w0)[0] = make_uint4(s0, s1, s2, s3);
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------- MD5 (producer/consumer)
 // Batched MD5 for Content-MD5 / multipart-ETag verification (reference
 // lib/hash/md5.cpp:71-116 for the step function, :158-172 for the padding).  Same

@@ -9,7 +9,7 @@ import s3client_amd as s3
 
 pytestmark = pytest.mark.gpu
 SEED = 20241008
-KERNELS = ["pair", "pc", "lane"]
+KERNELS = ["quad", "pair", "pc", "lane"]
 
 
 def _dev_buffer(torch, host: np.ndarray):
@@ -110,7 +110,7 @@ def test_c2_full_batch_bit_exact(torch_cuda, oracle, golden, kernel):
     txt = s3.digests_to_text(out)
     for e in golden["c2_parts"]:
         assert txt[e["p"]] == e["digest"], e["p"]
-    if kernel == "pair":
+    if kernel in ("quad", "pair"):
         host = data.cpu().numpy()
         want = oracle.batch(host, offs, lens, threads=16)
         assert np.array_equal(out, want)
