@@ -10,6 +10,7 @@
 #include <atomic>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -74,19 +75,36 @@ struct s3h_plan_s {
   uint32_t* d_out_idx = nullptr;
   uint32_t* d_state = nullptr;  // n*8 chaining words, allocated on first ranged launch
   uint8_t* d_zero = nullptr;    // 256 zero bytes: load target for out-of-range lanes
+  int quad_waves = 1;           // quad kernel: consumer waves per workgroup (1-4)
 };
 
 namespace {
 
-// Kernel choice by part count (profiles/r01_sweep_parts_256KiB.jsonl): while parts are
-// scarcer than SIMDs x 32, per-chain latency rules and the lane-pair kernel (10 VALU/round per
-// wave) wins; once consumer+producer waves fill every SIMD the total instruction count rules:
-// producer/consumer up to 64K parts, then the fused one-lane-per-part kernel.
+// Kernel choice by part count (profiles/r01_sweep_parts_256KiB.jsonl,
+// profiles/r01_sweep_quad_waves.jsonl): while every consumer wave can own a SIMD, per-chain
+// latency rules and the lane-quad kernel (9 VALU/round, 8 chains per wave) wins -- one
+// consumer wave per workgroup up to 2,048 parts, two up to 4,096 (256 workgroups = one per
+// CU); then the lane-pair kernel (10 VALU/round, 32 chains per wave) until consumer+producer
+// waves fill every SIMD and total instruction count rules: producer/consumer up to 64K parts,
+// then the fused one-lane-per-part kernel.
+constexpr uint64_t kQuadMaxParts = 4096;
 constexpr uint64_t kPairMaxParts = 32768;
 constexpr uint64_t kPcMaxParts = 65536;
 constexpr uint64_t kMaxParts = 1ull << 31;
 
 uint32_t digest_words(int algo) { return algo == S3H_ALGO_MD5 ? 4u : 8u; }
+
+// Quad kernel: consumer waves per workgroup -- the fewest that keep the grid within one
+// workgroup per CU (256); S3H_QUAD_WAVES=1..4 overrides (sweeps).
+int quad_waves(uint64_t n) {
+  static const int forced = [] {
+    const char* e = std::getenv("S3H_QUAD_WAVES");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 1 && v <= 4 ? v : 0;
+  }();
+  if (forced) return forced;
+  return n <= 256ull * s3h::kQuadChainsPerWave ? 1 : 2;
+}
 
 // Slots in descending length order (so block counts descend too, padded or not: the kernels
 // bound a workgroup's loop by its first slot); returns the total compressions.
@@ -118,7 +136,10 @@ int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* le
     kernel = S3H_KERNEL_PC;
   }
   if (kernel == S3H_KERNEL_AUTO)
-    kernel = n <= kPairMaxParts ? S3H_KERNEL_PAIR : n <= kPcMaxParts ? S3H_KERNEL_PC : S3H_KERNEL_LANE;
+    kernel = n <= kQuadMaxParts ? S3H_KERNEL_QUAD
+             : n <= kPairMaxParts ? S3H_KERNEL_PAIR
+             : n <= kPcMaxParts   ? S3H_KERNEL_PC
+                                  : S3H_KERNEL_LANE;
   if (kernel != S3H_KERNEL_PC && kernel != S3H_KERNEL_LANE && kernel != S3H_KERNEL_PAIR &&
       kernel != S3H_KERNEL_QUAD)
     return fail(S3H_EINVAL, "plan: unknown kernel %d", kernel);
@@ -134,9 +155,10 @@ int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* le
   P->n = n;
   P->total_blocks = total;
   P->max_blocks = s3h::nblocks(slots[0].len);
+  P->quad_waves = quad_waves(n);
   P->grid = kernel == S3H_KERNEL_PC     ? uint32_t((n + 63) / 64)
             : kernel == S3H_KERNEL_PAIR ? uint32_t((n + s3h::kPairParts - 1) / s3h::kPairParts)
-            : kernel == S3H_KERNEL_QUAD ? uint32_t((n + s3h::kQuadParts - 1) / s3h::kQuadParts)
+            : kernel == S3H_KERNEL_QUAD ? uint32_t((n + 8 * quad_waves(n) - 1) / (8 * quad_waves(n)))
                                         : uint32_t((n + 255) / 256);
 
   DeviceGuard g(device);
@@ -178,8 +200,14 @@ int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t
     hipLaunchKernelGGL(s3h::md5_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_PC)
     hipLaunchKernelGGL(s3h::sha256_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 1)
+    hipLaunchKernelGGL(s3h::sha256_quad_kernel<1>, dim3(P->grid), dim3(128), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 2)
+    hipLaunchKernelGGL(s3h::sha256_quad_kernel<2>, dim3(P->grid), dim3(192), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 3)
+    hipLaunchKernelGGL(s3h::sha256_quad_kernel<3>, dim3(P->grid), dim3(256), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_QUAD)
-    hipLaunchKernelGGL(s3h::sha256_quad_kernel, dim3(P->grid), dim3(s3h::kQuadThreads), 0, stream, A);
+    hipLaunchKernelGGL(s3h::sha256_quad_kernel<4>, dim3(P->grid), dim3(320), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_PAIR)
     hipLaunchKernelGGL(s3h::sha256_pair_kernel, dim3(P->grid), dim3(s3h::kPairThreads), 0, stream, A);
   else

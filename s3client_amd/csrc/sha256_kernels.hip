@@ -6,17 +6,22 @@
 // same issue slot whether 1 or 64 lanes are active, so each lane carries its own part and
 // the workgroup is the staging / scheduling unit.
 //
-// Two kernels:
-//   sha256_pc_kernel   (producer/consumer) -- a 128-thread workgroup = 64 parts.  Wave 1
-//       (producer) streams each lane's 64-byte blocks from HBM, decodes them (alignment +
-//       big-endian in one v_perm per word), synthesises the padding, expands the message
-//       schedule and writes W[t]+K[t] into an LDS double buffer.  Wave 0 (consumer) runs
-//       only the 64-round chain (~14 VALU per round), reading W+K with ds_read_b128.  A
-//       chain issues ~920 instead of ~1400 instructions per block, so each part hashes
-//       ~1.5x faster.  This is the right kernel while parts are scarcer than SIMD lanes
-//       (every BASELINE config: 1024-8192 parts per GPU vs 1024 SIMDs x 64 lanes).
+// Kernels (AUTO picks by part count, capi.hip):
+//   sha256_quad_kernel (<= 4,096 parts) -- each chain on 8 lanes: half-states on lane quads,
+//       one rotation per lane + quad_perm xor_dpp -> 9 VALU per round; NC consumer waves and
+//       one producer wave per workgroup.  Fastest per chain: the C2 metric kernel.
+//   sha256_pair_kernel (<= 32,768) -- each chain on a lane pair, 10 VALU per round, 32 chains
+//       per consumer wave: 3.6x less issue per chain than quad once the SIMDs fill.
+//   sha256_pc_kernel   (<= 65,536) -- one lane per chain, ~14 VALU per round.  In all three
+//       the producer wave streams each lane's 64-byte blocks from HBM, decodes them
+//       (alignment + big-endian in one v_perm per word), synthesises the padding, expands
+//       the message schedule and writes W[t]+K[t] into an LDS double buffer; the consumer
+//       wave runs only the 64-round chain.
 //   sha256_lane_kernel (fused) -- one lane does schedule + rounds; no LDS, 8 waves/SIMD.
-//       Used when parts are plentiful enough to saturate every SIMD (>= ~128K parts).
+//       Used when parts are plentiful enough to saturate every SIMD (> 65,536 parts).
+//   md5_pc_kernel -- MD5 in the producer/consumer shape.
+// A wave issues ~1 VALU per 4.7-5 cycles whatever the op (profiles/r01_ubench_*), so per-chain
+// speed = 1 / (chain VALU per block): every design choice above removes chain instructions.
 //
 // All kernels are resumable: a launch processes blocks [blk_begin, blk_end) of every part,
 // loading/saving the 8-word chaining state in `state` (message order) between launches.  The
@@ -416,11 +421,12 @@ __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A)
 // three rotations into every lane of the quad.  The rest of the round is the pair kernel's:
 // Ch and Maj as one bfi over a per-lane selector, the e-half's h+W+K precomputed, two
 // bank-masked adds exchanging T1 and d between the quads.  9 VALU per round instead of 10,
-// at 8 chains per wave (the chip has lanes to spare for every BASELINE config).
+// at 8 chains per wave.  A workgroup is NC consumer waves (8 chains each) and one producer
+// wave that feeds all of them (2 blocks x 8*NC chains per step), so the producer's issue cost
+// per chain matches the pair kernel's once NC = 4.
 // Hazards: the first xor_dpp reads the rotation 3 instructions after it is written (2 wait
 // states needed); the a-quad's exchange reads T1 two instructions after the add3.
-constexpr int kQuadThreads = 128;
-constexpr int kQuadParts = 8;
+constexpr int kQuadChainsPerWave = 8;
 
 #define S3H_QUAD_TXT(a, b, c, d, x, xn, wn)                                                   \
   "v_alignbit_b32 %[q1], %[" #a "], %[" #a "], %[h1]\n\t"                                     \
@@ -451,12 +457,14 @@ constexpr int kQuadParts = 8;
                  [w15] "v"(WK[(T + 15) & 63]), [w16] "v"(WK[(T + 16) & 63]), [h1] "v"(sh),     \
                  [m] "v"(msk))
 
-__global__ __launch_bounds__(kQuadThreads) void sha256_quad_kernel(LaunchArgs A) {
-  __shared__ uint4 lds_wk[2][2][16][kQuadParts];  // [buffer][block in step][round group][part]
+template <int NC>
+__global__ __launch_bounds__(64 * (NC + 1)) void sha256_quad_kernel(LaunchArgs A) {
+  constexpr uint32_t kParts = kQuadChainsPerWave * NC;
+  __shared__ uint4 lds_wk[2][2][16][kParts];  // [buffer][block in step][round group][part]
 
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t slot0 = blockIdx.x * kQuadParts;
+  const uint32_t slot0 = blockIdx.x * kParts;
   const uint64_t b0 = A.blk_begin;
   const uint64_t wg_nb = slot_blocks(A, A.slots[slot0].len);
   const uint64_t wg_end = wg_nb < A.blk_end ? wg_nb : A.blk_end;
@@ -464,11 +472,12 @@ __global__ __launch_bounds__(kQuadThreads) void sha256_quad_kernel(LaunchArgs A)
   const uint64_t iters = wg_end - b0;
   const uint64_t steps = (iters + 1) >> 1;
 
-  if (wave == 1) {
+  if (wave == NC) {
     // ---------------------------------------------------------------- producer
-    // Lanes 0-15 carry (part, even/odd block); lanes 16-63 repeat them (same loads, same LDS
-    // writes), which keeps every lane on one branch-free path at no extra issue cost.
-    const uint32_t part = lane & 7u, half = (lane >> 3) & 1u;
+    // Lanes 0 .. 2*kParts-1 carry (part, even/odd block); higher lanes repeat them (same loads,
+    // same LDS writes), which keeps every lane on one branch-free path at no extra issue cost.
+    const uint32_t pl = lane % (2 * kParts);
+    const uint32_t part = pl >> 1, half = pl & 1u;
     const uint32_t slot = slot0 + part;
     Slot s = {0, 0};
     if (slot < A.n) s = A.slots[slot];
@@ -498,7 +507,7 @@ __global__ __launch_bounds__(kQuadThreads) void sha256_quad_kernel(LaunchArgs A)
   } else {
     // ---------------------------------------------------------------- consumer
     __builtin_amdgcn_s_setprio(3);
-    const uint32_t part = (lane >> 4) * 2u + ((lane >> 3) & 1u);
+    const uint32_t part = kQuadChainsPerWave * wave + (lane >> 4) * 2u + ((lane >> 3) & 1u);
     const bool ahalf = (lane >> 2) & 1u;
     const uint32_t k4 = lane & 3u;
     const uint32_t slot = slot0 + part;
@@ -520,7 +529,7 @@ __global__ __launch_bounds__(kQuadThreads) void sha256_quad_kernel(LaunchArgs A)
     }
     uint32_t xa = 0, xb = 0;
     uint32_t q1, q2, q3, q4;
-    const uint32_t last = (slot0 + kQuadParts <= A.n ? slot0 + kQuadParts : A.n) - 1;
+    const uint32_t last = (slot0 + kParts <= A.n ? slot0 + kParts : A.n) - 1;
     const uint64_t all_live_end = slot_blocks(A, A.slots[last].len);
     auto block = [&](const uint32_t wk[64], uint64_t i) {
       const uint32_t t0 = s0, t1 = s1, t2 = s2, t3 = s3;
