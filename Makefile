@@ -41,7 +41,7 @@ apps/build/s3-upload-hash: apps/s3_upload_hash.cpp s3client_amd/host/aws_sign.cp
 	$(CXX) -O2 -std=c++17 -pthread -Iinclude -Is3client_amd/host -o $@ $< s3client_amd/host/aws_sign.cpp \
 	    -L$(LIBDIR) -ls3hash -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
-tests/cpp/build/dropin_test: tests/cpp/dropin_test.cpp $(LIB)
+tests/cpp/build/dropin_test: tests/cpp/dropin_test.cpp include/s3hash_batch.hpp $(LIB)
 	@mkdir -p tests/cpp/build
 	$(CXX) -O2 -std=c++17 -Iinclude -o $@ $< -L$(LIBDIR) -ls3hash -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)'
 

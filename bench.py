@@ -34,7 +34,7 @@ CLOCK_GHZ = 2.4                 # in-kernel clock measured by tools/ubench (2.39
 # pair = 640 round VALU + state/X bookkeeping + 16 ds_read_b128).  A lone wave issues about
 # one instruction per 5 cycles (profiles/r01_ubench_valu_issue.txt): this, not HBM, bounds
 # each part's chain.
-CHAIN_INSTR_PER_BLOCK = {"quad": 608, "pair": 672, "pc": 923, "lane": 1425, "md5-pc": 280}
+CHAIN_INSTR_PER_BLOCK = {"quad": 592, "pair": 672, "pc": 923, "lane": 1425, "md5-pc": 280}
 
 
 def parse():

@@ -59,4 +59,49 @@ inline std::vector<std::string> payload_hashes(const std::vector<const uint8_t*>
   return out;
 }
 
+// n objects hashed as their bodies arrive (s3h_stream_*): append() one chunk per object
+// (any length, 0 allowed), finish() -> n digests of everything appended since the last
+// finish(), after which the object restarts with n empty messages.  The batched, on-device
+// form of sha256_stream + the documented sha256_next contract (sha256.h:73-97).
+class stream_batch {
+ public:
+  explicit stream_batch(uint64_t n, int device = 0, int algo = S3H_ALGO_SHA256)
+      : n_(n), words_(algo == S3H_ALGO_MD5 ? 4 : 8) {
+    batch_check(s3h_stream_create(device, algo, n, S3H_KERNEL_AUTO, &s_));
+  }
+  ~stream_batch() { s3h_stream_destroy(s_); }
+  stream_batch(const stream_batch&) = delete;
+  stream_batch& operator=(const stream_batch&) = delete;
+
+  void append(const std::vector<const uint8_t*>& chunks, const std::vector<uint64_t>& lengths) {
+    if (chunks.size() != n_ || lengths.size() != n_)
+      throw std::invalid_argument("stream_batch: one chunk per object");
+    batch_check(s3h_stream_update_host(s_, chunks.data(), lengths.data()));
+  }
+  std::vector<uint32_t> finish() {
+    std::vector<uint32_t> out(words_ * n_);
+    batch_check(s3h_stream_final_host(s_, out.data()));
+    return out;
+  }
+  std::vector<std::string> finish_hex() {
+    const std::vector<uint32_t> d = finish();
+    std::vector<std::string> out(n_);
+    static const char* hexd = "0123456789abcdef";
+    for (uint64_t i = 0; i < n_; ++i) {
+      const uint8_t* b = reinterpret_cast<const uint8_t*>(&d[words_ * i]);
+      for (uint32_t k = 0; k < 4 * words_; ++k) {
+        out[i] += hexd[b[k] >> 4];
+        out[i] += hexd[b[k] & 15];
+      }
+    }
+    return out;
+  }
+  uint64_t size() const { return n_; }
+
+ private:
+  s3h_stream_t s_ = nullptr;
+  uint64_t n_;
+  uint32_t words_;
+};
+
 }  // namespace sha256

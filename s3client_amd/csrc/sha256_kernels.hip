@@ -428,34 +428,37 @@ __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A)
 // states needed); the a-quad's exchange reads T1 two instructions after the add3.
 constexpr int kQuadChainsPerWave = 8;
 
-#define S3H_QUAD_TXT(a, b, c, d, x, xn, wn)                                                   \
+// One quad round.  W+K reaches the e-quad by DPP broadcast: lane L of every quad holds W+K
+// rows L, L+4, L+8, L+12 (4 ds_read_b128 per block instead of 16), and the h+W+K precompute
+// reads word `wreg` of lane L with quad_perm:[L,L,L,L] (an LDS-loaded source: no DPP hazard).
+// `din`/`dout`: the d slot read / written (different only in the first four rounds of a block,
+// which read the block-start state s0..s3 and write fresh n0..n3, so the state survives for
+// the feed-forward without copies).
+#define S3H_QR(a, b, c, din, dout, x, xn, wreg, L)                                            \
   "v_alignbit_b32 %[q1], %[" #a "], %[" #a "], %[h1]\n\t"                                     \
   "v_bitop3_b32 %[q4], %[" #a "], %[" #b "], %[m] bitop3:0xd2\n\t"                            \
   "v_bfi_b32 %[q2], %[q4], %[" #b "], %[" #c "]\n\t"                                          \
   "v_xor_b32_dpp %[q3], %[q1], %[q1] quad_perm:[1,2,0,1] row_mask:0xf bank_mask:0xf\n\t"     \
   "v_xor_b32_dpp %[q3], %[q1], %[q3] quad_perm:[2,0,1,2] row_mask:0xf bank_mask:0xf\n\t"     \
   "v_add3_u32 %[q3], %[" #x "], %[q3], %[q2]\n\t"                                             \
-  "v_add_u32_dpp %[" #xn "], %[" #c "], %[" #wn "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5\n\t" \
-  "v_add_u32_dpp %[" #d "], %[" #d "], %[q3] row_shl:4 row_mask:0xf bank_mask:0x5\n\t"       \
-  "v_add_u32_dpp %[" #d "], %[q3], %[q3] row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+  "v_add_u32_dpp %[" #xn "], %[" #wreg "], %[" #c "] quad_perm:[" #L "," #L "," #L "," #L     \
+  "] row_mask:0xf bank_mask:0x5\n\t"                                                          \
+  "v_add_u32_dpp %[" #dout "], %[" #din "], %[q3] row_shl:4 row_mask:0xf bank_mask:0x5\n\t"  \
+  "v_add_u32_dpp %[" #dout "], %[q3], %[q3] row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
 
-#define S3H_QUAD_4TXT(wa, wb, wc, wd)                                                         \
-  S3H_QUAD_TXT(s0, s1, s2, s3, xa, xb, wa) S3H_QUAD_TXT(s3, s0, s1, s2, xb, xa, wb)              \
-  S3H_QUAD_TXT(s2, s3, s0, s1, xa, xb, wc) S3H_QUAD_TXT(s1, s2, s3, s0, xb, xa, wd)
-#define S3H_QUAD_16RND(WK, T)                                                                   \
-  asm volatile(S3H_QUAD_4TXT(w1, w2, w3, w4) S3H_QUAD_4TXT(w5, w6, w7, w8)                       \
-               S3H_QUAD_4TXT(w9, w10, w11, w12) S3H_QUAD_4TXT(w13, w14, w15, w16)               \
-               : [s0] "+v"(s0), [s1] "+v"(s1), [s2] "+v"(s2), [s3] "+v"(s3), [xa] "+v"(xa),    \
-                 [xb] "+v"(xb), [q1] "=&v"(q1), [q2] "=&v"(q2), [q3] "=&v"(q3), [q4] "=&v"(q4)  \
-               : [w1] "v"(WK[(T + 1) & 63]), [w2] "v"(WK[(T + 2) & 63]),                       \
-                 [w3] "v"(WK[(T + 3) & 63]), [w4] "v"(WK[(T + 4) & 63]),                       \
-                 [w5] "v"(WK[(T + 5) & 63]), [w6] "v"(WK[(T + 6) & 63]),                       \
-                 [w7] "v"(WK[(T + 7) & 63]), [w8] "v"(WK[(T + 8) & 63]),                       \
-                 [w9] "v"(WK[(T + 9) & 63]), [w10] "v"(WK[(T + 10) & 63]),                     \
-                 [w11] "v"(WK[(T + 11) & 63]), [w12] "v"(WK[(T + 12) & 63]),                   \
-                 [w13] "v"(WK[(T + 13) & 63]), [w14] "v"(WK[(T + 14) & 63]),                   \
-                 [w15] "v"(WK[(T + 15) & 63]), [w16] "v"(WK[(T + 16) & 63]), [h1] "v"(sh),     \
-                 [m] "v"(msk))
+// Four in-place rounds on n0..n3; rounds use words 1,2,3 of lane L, then word 0 of lane LN
+// from register set WS (the next group's first word).
+#define S3H_QG(S, L, WN, LN)                                                                   \
+  S3H_QR(n0, n1, n2, n3, n3, xa, xb, S##1, L) S3H_QR(n3, n0, n1, n2, n2, xb, xa, S##2, L)        \
+  S3H_QR(n2, n3, n0, n1, n1, xa, xb, S##3, L) S3H_QR(n1, n2, n3, n0, n0, xb, xa, WN, LN)
+// The block's first four rounds: read s0..s3, write n3, n2, n1, n0.
+#define S3H_QG_FIRST                                                                           \
+  S3H_QR(s0, s1, s2, s3, n3, xa, xb, a1, 0) S3H_QR(n3, s0, s1, s2, n2, xb, xa, a2, 0)            \
+  S3H_QR(n2, n3, s0, s1, n1, xa, xb, a3, 0) S3H_QR(n1, n2, n3, s0, n0, xb, xa, a0, 1)
+// 16 rounds of register set S (rounds 16m..16m+15 use set m on lanes 0..3), ending with the
+// next set's word 0 (NX).
+#define S3H_Q16(S, NX) S3H_QG(S, 0, S##0, 1) S3H_QG(S, 1, S##0, 2) S3H_QG(S, 2, S##0, 3) S3H_QG(S, 3, NX, 0)
+#define S3H_Q16_FIRST S3H_QG_FIRST S3H_QG(a, 1, a0, 2) S3H_QG(a, 2, a0, 3) S3H_QG(a, 3, b0, 0)
 
 template <int NC>
 __global__ __launch_bounds__(64 * (NC + 1)) void sha256_quad_kernel(LaunchArgs A) {
@@ -528,43 +531,52 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_quad_kernel(LaunchArgs A
       s3 = ahalf ? 0xa54ff53au : 0x5be0cd19u;
     }
     uint32_t xa = 0, xb = 0;
-    uint32_t q1, q2, q3, q4;
+    uint32_t q1, q2, q3, q4, n0, n1, n2, n3;
     const uint32_t last = (slot0 + kParts <= A.n ? slot0 + kParts : A.n) - 1;
     const uint64_t all_live_end = slot_blocks(A, A.slots[last].len);
-    auto block = [&](const uint32_t wk[64], uint64_t i) {
-      const uint32_t t0 = s0, t1 = s1, t2 = s2, t3 = s3;
+    // W[j] = W+K row (k4 + 4j) of the block: word w of round 16j + 4r + w sits on lane r.
+    auto block = [&](const uint4 W[4], uint64_t i) {
       asm volatile(
           "s_nop 1\n\t"
-          "v_add_u32_dpp %0, %1, %2 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5"
-          : "+v"(xa) : "v"(s3), "v"(wk[0]));
-      S3H_QUAD_16RND(wk, 0);
-      S3H_QUAD_16RND(wk, 16);
-      S3H_QUAD_16RND(wk, 32);
-      S3H_QUAD_16RND(wk, 48);
+          "v_add_u32_dpp %0, %1, %2 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0x5"
+          : "+v"(xa) : "v"(W[0].x), "v"(s3));
+      asm volatile(S3H_Q16_FIRST S3H_Q16(b, c0)
+                   : [n0] "=&v"(n0), [n1] "=&v"(n1), [n2] "=&v"(n2), [n3] "=&v"(n3),
+                     [xa] "+v"(xa), [xb] "+v"(xb), [q1] "=&v"(q1), [q2] "=&v"(q2),
+                     [q3] "=&v"(q3), [q4] "=&v"(q4)
+                   : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3),
+                     [a0] "v"(W[0].x), [a1] "v"(W[0].y), [a2] "v"(W[0].z), [a3] "v"(W[0].w),
+                     [b0] "v"(W[1].x), [b1] "v"(W[1].y), [b2] "v"(W[1].z), [b3] "v"(W[1].w),
+                     [c0] "v"(W[2].x), [h1] "v"(sh), [m] "v"(msk));
+      asm volatile(S3H_Q16(c, d0) S3H_Q16(d, d0)
+                   : [n0] "+v"(n0), [n1] "+v"(n1), [n2] "+v"(n2), [n3] "+v"(n3),
+                     [xa] "+v"(xa), [xb] "+v"(xb), [q1] "=&v"(q1), [q2] "=&v"(q2),
+                     [q3] "=&v"(q3), [q4] "=&v"(q4)
+                   : [c0] "v"(W[2].x), [c1] "v"(W[2].y), [c2] "v"(W[2].z), [c3] "v"(W[2].w),
+                     [d0] "v"(W[3].x), [d1] "v"(W[3].y), [d2] "v"(W[3].z), [d3] "v"(W[3].w),
+                     [h1] "v"(sh), [m] "v"(msk));
       if (b0 + i < all_live_end) {
-        s0 += t0; s1 += t1; s2 += t2; s3 += t3;
+        s0 += n0; s1 += n1; s2 += n2; s3 += n3;
       } else {
         const bool live = (b0 + i) < nb;
-        s0 = live ? s0 + t0 : t0;
-        s1 = live ? s1 + t1 : t1;
-        s2 = live ? s2 + t2 : t2;
-        s3 = live ? s3 + t3 : t3;
+        s0 = live ? s0 + n0 : s0;
+        s1 = live ? s1 + n1 : s1;
+        s2 = live ? s2 + n2 : s2;
+        s3 = live ? s3 + n3 : s3;
       }
     };
     __syncthreads();
     for (uint64_t j = 0; j < steps; ++j) {
       const bool second = 2 * j + 1 < iters;
-      uint32_t wk0[64], wk1[64];
+      uint4 w0[4], w1[4];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const uint4 v = lds_wk[j & 1][0][q][part];
-        wk0[4 * q] = v.x; wk0[4 * q + 1] = v.y; wk0[4 * q + 2] = v.z; wk0[4 * q + 3] = v.w;
-        const uint4 u = lds_wk[j & 1][1][q][part];
-        wk1[4 * q] = u.x; wk1[4 * q + 1] = u.y; wk1[4 * q + 2] = u.z; wk1[4 * q + 3] = u.w;
+      for (int q = 0; q < 4; ++q) {
+        w0[q] = lds_wk[j & 1][0][k4 + 4 * q][part];
+        w1[q] = lds_wk[j & 1][1][k4 + 4 * q][part];
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-      block(wk0, 2 * j);
-      if (second) block(wk1, 2 * j + 1);
+      block(w0, 2 * j);
+      if (second) block(w1, 2 * j + 1);
       __syncthreads();
     }
     if (valid && nb > b0 && k4 == 0) {

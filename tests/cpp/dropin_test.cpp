@@ -4,6 +4,7 @@
 // exercises every exported symbol.  `--gpu` also runs the batched C++ API on the GPU.
 // Output: CSV "Hash,<action>,0|1," like the reference tests (test/utility.cpp:87-95).
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -132,6 +133,28 @@ int main(int argc, char** argv) {
     bool ok = true;
     for (size_t i = 0; i < msgs.size(); ++i) ok &= hex[i] == digest(msgs[i]);
     report("gpu batch payload_hashes", ok);
+    // the same messages streamed in ragged chunks through sha256::stream_batch
+    sha256::stream_batch sb(msgs.size());
+    std::vector<size_t> pos(msgs.size(), 0);
+    const size_t steps[] = {1, 63, 64, 65, 1000, 1 << 20};
+    for (int round = 0;; ++round) {
+      bool more = false;
+      std::vector<const uint8_t*> cp(msgs.size());
+      std::vector<uint64_t> cl(msgs.size());
+      for (size_t i = 0; i < msgs.size(); ++i) {
+        const size_t take = std::min(steps[(round + i) % 6], msgs[i].size() - pos[i]);
+        cp[i] = reinterpret_cast<const uint8_t*>(msgs[i].data()) + pos[i];
+        cl[i] = take;
+        pos[i] += take;
+        more |= take > 0;
+      }
+      if (!more) break;
+      sb.append(cp, cl);
+    }
+    const auto sh = sb.finish_hex();
+    bool sok = true;
+    for (size_t i = 0; i < msgs.size(); ++i) sok &= sh[i] == digest(msgs[i]);
+    report("gpu stream_batch", sok);
   }
   return fails ? 1 : 0;
 }

@@ -36,7 +36,9 @@ def test_dropin_kats(programs):
 @pytest.mark.gpu
 def test_dropin_gpu_batch(programs):
     rc, rows = _run(os.path.join(programs, "dropin_test"), "--gpu")
-    assert rc == 0 and rows[-1][1] == "gpu batch payload_hashes" and rows[-1][2] == "1", rows
+    assert rc == 0, rows
+    got = {r[1]: r[2] for r in rows}
+    assert got["gpu batch payload_hashes"] == "1" and got["gpu stream_batch"] == "1", rows
 
 
 def _xfer_file(tmp_path, golden):
