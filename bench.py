@@ -30,6 +30,7 @@ SEED = 20241008
 MIB = 1 << 20
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 CLOCK_GHZ = 2.4                 # in-kernel clock measured by tools/ubench (2.39-2.40 GHz)
+LONE_WAVE_CPI = 4.70            # one wave alone, round-shaped VALU stream (tools/ubench_round)
 # Instructions one chain's wave issues per 64-B block (ISA audit: `make isa`, consumer loop;
 # pair = 640 round VALU + state/X bookkeeping + 16 ds_read_b128).  A lone wave issues about
 # one instruction per 5 cycles (profiles/r01_ubench_valu_issue.txt): this, not HBM, bounds
@@ -236,11 +237,20 @@ def main():
     # many of the chip's 256 CU x 4 SIMD x 64 = 65,536 lanes the batch can occupy
     chain_gbps = float(lens.max()) / (kern_ms / 1e3) / 1e9
     cyc_per_block = kern_ms / 1e3 * CLOCK_GHZ * 1e9 / info["max_blocks"]
+    cpi = cyc_per_block / CHAIN_INSTR_PER_BLOCK[kname]
     issue = {"bound": "per-wave instruction issue of each part's sequential chain",
              "chain_instr_per_block": CHAIN_INSTR_PER_BLOCK[kname],
              "cycles_per_block": round(cyc_per_block, 1),
-             "cycles_per_instr": round(cyc_per_block / CHAIN_INSTR_PER_BLOCK[kname], 3),
-             "lone_wave_issue_cycles_measured": 5.1, "clock_GHz_assumed": CLOCK_GHZ}
+             "cycles_per_instr": round(cpi, 3),
+             # floor: a lone wave's measured issue rate on a round-shaped stream
+             # (profiles/r01_ubench_pair_round.txt, 4.70 cycles per instruction)
+             "lone_wave_issue_cycles_measured": LONE_WAVE_CPI,
+             "frac": round(LONE_WAVE_CPI / cpi, 4), "clock_GHz_assumed": CLOCK_GHZ,
+             # chip-wide INT32-VALU roof (256 CU x 64 lanes x clock / VALU per
+             # block of the one-lane-per-part kernel x 64 B) and the parallelism ceiling
+             "valu_roof_GBps": round(256 * 64 * CLOCK_GHZ * 1e9 / CHAIN_INSTR_PER_BLOCK["lane"]
+                                     * 64 / 1e9, 1),
+             "parallelism_ceiling": round(min(len(lens), 65536) / 65536, 5)}
 
     if rank == 0:
         line = {

@@ -94,6 +94,17 @@ constexpr uint64_t kMaxParts = 1ull << 31;
 
 uint32_t digest_words(int algo) { return algo == S3H_ALGO_MD5 ? 4u : 8u; }
 
+// Wave-priority experiment knob for the quad kernel (S3H_PRIO=1: no s_setprio, 2: producer
+// at priority 3 as well); default: consumers at 3.
+uint32_t prio_flags() {
+  static const uint32_t f = [] {
+    const char* e = std::getenv("S3H_PRIO");
+    const int v = e ? std::atoi(e) : 0;
+    return v == 1 ? s3h::kPrioNone : v == 2 ? s3h::kPrioAll : 0u;
+  }();
+  return f;
+}
+
 // Quad kernel: consumer waves per workgroup -- the fewest that keep the grid within one
 // workgroup per CU (256); S3H_QUAD_WAVES=1..4 overrides (sweeps).
 int quad_waves(uint64_t n) {
@@ -195,7 +206,7 @@ int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t
   A.blk_end = b1;
   A.blk_origin = origin;
   A.n = uint32_t(P->n);
-  A.flags = flags;
+  A.flags = flags | prio_flags();
   if (P->algo == S3H_ALGO_MD5)
     hipLaunchKernelGGL(s3h::md5_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_PC)

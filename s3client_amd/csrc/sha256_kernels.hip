@@ -35,6 +35,8 @@ namespace s3h {
 // LaunchArgs::flags
 constexpr uint32_t kNoPad = 1;   // hash only the slot's whole 64-B blocks; never pad or emit
 constexpr uint32_t kResume = 2;  // load the chaining state even at blk_begin == 0
+constexpr uint32_t kPrioNone = 4;  // experiment (S3H_PRIO=1): consumers keep priority 0
+constexpr uint32_t kPrioAll = 8;   // experiment (S3H_PRIO=2): producer raises priority too
 
 struct LaunchArgs {
   const uint8_t* base;       // part p's block b is at base + slots[p].off + 64*(b - blk_origin)
@@ -477,6 +479,7 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_quad_kernel(LaunchArgs A
 
   if (wave == NC) {
     // ---------------------------------------------------------------- producer
+    if (A.flags & kPrioAll) __builtin_amdgcn_s_setprio(3);
     // Lanes 0 .. 2*kParts-1 carry (part, even/odd block); higher lanes repeat them (same loads,
     // same LDS writes), which keeps every lane on one branch-free path at no extra issue cost.
     const uint32_t pl = lane % (2 * kParts);
@@ -509,7 +512,7 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_quad_kernel(LaunchArgs A
     }
   } else {
     // ---------------------------------------------------------------- consumer
-    __builtin_amdgcn_s_setprio(3);
+    if (!(A.flags & kPrioNone)) __builtin_amdgcn_s_setprio(3);
     const uint32_t part = kQuadChainsPerWave * wave + (lane >> 4) * 2u + ((lane >> 3) & 1u);
     const bool ahalf = (lane >> 2) & 1u;
     const uint32_t k4 = lane & 3u;

@@ -13,9 +13,10 @@
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
   printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
-template <int W>
+template <int W, bool kBigVgpr>
 __global__ __launch_bounds__(64 * W) void probe(uint32_t* out, long long spin) {
   __shared__ uint4 lds[2 * 2 * 16 * 8 * (W - 1 > 0 ? W - 1 : 1)];
+  if (kBigVgpr) asm volatile("s_nop 0" ::: "v159");  // allocate 160 VGPRs like the quad kernel
   if (threadIdx.x < 16) lds[threadIdx.x] = make_uint4(threadIdx.x, 0, 0, 0);
   __syncthreads();
   const long long t0 = clock64();
@@ -30,12 +31,12 @@ __global__ __launch_bounds__(64 * W) void probe(uint32_t* out, long long spin) {
   }
 }
 
-template <int W>
+template <int W, bool kBigVgpr = false>
 int run(int grid) {
   uint32_t* d;
   const size_t nw = size_t(grid) * W;
   CHECK(hipMalloc(&d, nw * 8));
-  hipLaunchKernelGGL(probe<W>, dim3(grid), dim3(64 * W), 0, 0, d, 2000000LL);
+  hipLaunchKernelGGL((probe<W, kBigVgpr>), dim3(grid), dim3(64 * W), 0, 0, d, 2000000LL);
   CHECK(hipDeviceSynchronize());
   std::vector<uint32_t> h(nw * 2);
   CHECK(hipMemcpy(h.data(), d, nw * 8, hipMemcpyDeviceToHost));
@@ -62,8 +63,8 @@ int run(int grid) {
   for (auto& kv : cu)
     for (auto& s : kv.second)
       if (s.second > 1) shared_simd_waves += s.second;
-  printf("waves/WG=%d grid=%4d: CUs used %3zu, max WGs/CU %d, max waves/SIMD %d, waves on shared "
-         "SIMDs %4d, CUs with 1/2/3/4 WGs: %d/%d/%d/%d, XCDs:", W, grid, cu.size(), max_wg,
+  printf("%s waves/WG=%d grid=%4d: CUs used %3zu, max WGs/CU %d, max waves/SIMD %d, waves on shared "
+         "SIMDs %4d, CUs with 1/2/3/4 WGs: %d/%d/%d/%d, XCDs:", kBigVgpr ? "vgpr160" : "vgpr-lo", W, grid, cu.size(), max_wg,
          max_simd, shared_simd_waves, hist[1], hist[2], hist[3], hist[4]);
   for (auto& x : per_xcc) printf(" %d:%d", x.first, x.second);
   printf("\n");
@@ -76,6 +77,12 @@ int main() {
     run<3>(grid);
     run<4>(grid);
     run<5>(grid);
+  }
+  for (int grid : {32, 43, 128, 256, 512}) {
+    run<2, true>(grid);
+    run<3, true>(grid);
+    run<4, true>(grid);
+    run<5, true>(grid);
   }
   return 0;
 }
