@@ -94,6 +94,15 @@ constexpr uint64_t kMaxParts = 1ull << 31;
 
 uint32_t digest_words(int algo) { return algo == S3H_ALGO_MD5 ? 4u : 8u; }
 
+// Shadow-consumer experiment knob (S3H_QUAD_SHADOW=1).
+bool quad_shadow() {
+  static const bool on = [] {
+    const char* e = std::getenv("S3H_QUAD_SHADOW");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
+
 // Wave-priority experiment knob for the quad kernel (S3H_PRIO=1: no s_setprio, 2: producer
 // at priority 3 as well); default: consumers at 3.
 uint32_t prio_flags() {
@@ -211,6 +220,10 @@ int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t
     hipLaunchKernelGGL(s3h::md5_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_PC)
     hipLaunchKernelGGL(s3h::sha256_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 1 && quad_shadow())
+    hipLaunchKernelGGL((s3h::sha256_quad_kernel<1, 1>), dim3(P->grid), dim3(192), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 2 && quad_shadow())
+    hipLaunchKernelGGL((s3h::sha256_quad_kernel<2, 1>), dim3(P->grid), dim3(320), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 1)
     hipLaunchKernelGGL(s3h::sha256_quad_kernel<1>, dim3(P->grid), dim3(128), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 2)

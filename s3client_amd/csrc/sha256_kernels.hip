@@ -277,6 +277,12 @@ __device__ __forceinline__ bool pair_is_ahalf(uint32_t lane) { return (lane >> 2
   "v_add_u32_dpp %[" #d "], %[" #d "], %[q3] row_shl:4 row_mask:0xf bank_mask:0x5\n\t"       \
   "v_add_u32_dpp %[" #d "], %[q3], %[q3] row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
 
+// Every round instruction is 8 bytes (VOP3 / DPP).  An 8-byte instruction at an address
+// = 4 (mod 8) issues at ~5.05 instead of ~4.05 cycles (tools/ubench_cu_waves.hip,
+// profiles/r01_ubench_alignment.txt), so each round statement starts 8-byte aligned: the
+// assembler pads with one 4-byte s_nop when the preceding code leaves it misaligned.
+#define S3H_ALIGN8 ".p2align 3\n\t"
+
 // Sixteen rounds (four rotations of the state names) per asm statement (30 operands, the
 // inline-asm maximum): the compiler pads with an s_nop between consecutive asm statements,
 // so fewer, longer statements keep the stream at one VALU per issue slot.
@@ -284,7 +290,7 @@ __device__ __forceinline__ bool pair_is_ahalf(uint32_t lane) { return (lane >> 2
   S3H_PAIR_TXT(s0, s1, s2, s3, xa, xb, wa) S3H_PAIR_TXT(s3, s0, s1, s2, xb, xa, wb)              \
   S3H_PAIR_TXT(s2, s3, s0, s1, xa, xb, wc) S3H_PAIR_TXT(s1, s2, s3, s0, xb, xa, wd)
 #define S3H_PAIR_16RND(WK, T)                                                                   \
-  asm volatile(S3H_PAIR_4TXT(w1, w2, w3, w4) S3H_PAIR_4TXT(w5, w6, w7, w8)                       \
+  asm volatile(S3H_ALIGN8 S3H_PAIR_4TXT(w1, w2, w3, w4) S3H_PAIR_4TXT(w5, w6, w7, w8)                       \
                S3H_PAIR_4TXT(w9, w10, w11, w12) S3H_PAIR_4TXT(w13, w14, w15, w16)               \
                : [s0] "+v"(s0), [s1] "+v"(s1), [s2] "+v"(s2), [s3] "+v"(s3), [xa] "+v"(xa),    \
                  [xb] "+v"(xb), [q1] "=&v"(q1), [q2] "=&v"(q2), [q3] "=&v"(q3), [q4] "=&v"(q4)  \
@@ -369,7 +375,7 @@ __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A)
     auto block = [&](const uint32_t wk[64], uint64_t i) {
       const uint32_t t0 = s0, t1 = s1, t2 = s2, t3 = s3;
       asm volatile(
-          "s_nop 1\n\t"
+          "s_nop 1\n\t" S3H_ALIGN8
           "v_add_u32_dpp %0, %1, %2 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5"
           : "+v"(xa) : "v"(s3), "v"(wk[0]));
       S3H_PAIR_16RND(wk, 0);
@@ -462,9 +468,12 @@ constexpr int kQuadChainsPerWave = 8;
 #define S3H_Q16(S, NX) S3H_QG(S, 0, S##0, 1) S3H_QG(S, 1, S##0, 2) S3H_QG(S, 2, S##0, 3) S3H_QG(S, 3, NX, 0)
 #define S3H_Q16_FIRST S3H_QG_FIRST S3H_QG(a, 1, a0, 2) S3H_QG(a, 2, a0, 3) S3H_QG(a, 3, b0, 0)
 
-template <int NC>
-__global__ __launch_bounds__(64 * (NC + 1)) void sha256_quad_kernel(LaunchArgs A) {
+template <int NC, int SH = 0>
+__global__ __launch_bounds__(64 * (NC * (1 + SH) + 1)) void sha256_quad_kernel(LaunchArgs A) {
+  // SH = 1: every consumer wave has a SHADOW wave (wave + NC) running the identical
+  // instruction stream on the same chains, output discarded (issue-rate experiment).
   constexpr uint32_t kParts = kQuadChainsPerWave * NC;
+  constexpr uint32_t kProducer = NC * (1 + SH);
   __shared__ uint4 lds_wk[2][2][16][kParts];  // [buffer][block in step][round group][part]
 
   const uint32_t lane = threadIdx.x & 63u;
@@ -477,7 +486,7 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_quad_kernel(LaunchArgs A
   const uint64_t iters = wg_end - b0;
   const uint64_t steps = (iters + 1) >> 1;
 
-  if (wave == NC) {
+  if (wave == kProducer) {
     // ---------------------------------------------------------------- producer
     if (A.flags & kPrioAll) __builtin_amdgcn_s_setprio(3);
     // Lanes 0 .. 2*kParts-1 carry (part, even/odd block); higher lanes repeat them (same loads,
@@ -513,7 +522,8 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_quad_kernel(LaunchArgs A
   } else {
     // ---------------------------------------------------------------- consumer
     if (!(A.flags & kPrioNone)) __builtin_amdgcn_s_setprio(3);
-    const uint32_t part = kQuadChainsPerWave * wave + (lane >> 4) * 2u + ((lane >> 3) & 1u);
+    const uint32_t cw = wave % NC;  // chain group (a shadow wave repeats wave cw's chains)
+    const uint32_t part = kQuadChainsPerWave * cw + (lane >> 4) * 2u + ((lane >> 3) & 1u);
     const bool ahalf = (lane >> 2) & 1u;
     const uint32_t k4 = lane & 3u;
     const uint32_t slot = slot0 + part;
@@ -540,10 +550,10 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_quad_kernel(LaunchArgs A
     // W[j] = W+K row (k4 + 4j) of the block: word w of round 16j + 4r + w sits on lane r.
     auto block = [&](const uint4 W[4], uint64_t i) {
       asm volatile(
-          "s_nop 1\n\t"
+          "s_nop 1\n\t" S3H_ALIGN8
           "v_add_u32_dpp %0, %1, %2 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0x5"
           : "+v"(xa) : "v"(W[0].x), "v"(s3));
-      asm volatile(S3H_Q16_FIRST S3H_Q16(b, c0)
+      asm volatile(S3H_ALIGN8 S3H_Q16_FIRST S3H_Q16(b, c0)
                    : [n0] "=&v"(n0), [n1] "=&v"(n1), [n2] "=&v"(n2), [n3] "=&v"(n3),
                      [xa] "+v"(xa), [xb] "+v"(xb), [q1] "=&v"(q1), [q2] "=&v"(q2),
                      [q3] "=&v"(q3), [q4] "=&v"(q4)
@@ -551,7 +561,7 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_quad_kernel(LaunchArgs A
                      [a0] "v"(W[0].x), [a1] "v"(W[0].y), [a2] "v"(W[0].z), [a3] "v"(W[0].w),
                      [b0] "v"(W[1].x), [b1] "v"(W[1].y), [b2] "v"(W[1].z), [b3] "v"(W[1].w),
                      [c0] "v"(W[2].x), [h1] "v"(sh), [m] "v"(msk));
-      asm volatile(S3H_Q16(c, d0) S3H_Q16(d, d0)
+      asm volatile(S3H_ALIGN8 S3H_Q16(c, d0) S3H_Q16(d, d0)
                    : [n0] "+v"(n0), [n1] "+v"(n1), [n2] "+v"(n2), [n3] "+v"(n3),
                      [xa] "+v"(xa), [xb] "+v"(xb), [q1] "=&v"(q1), [q2] "=&v"(q2),
                      [q3] "=&v"(q3), [q4] "=&v"(q4)
@@ -582,7 +592,7 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_quad_kernel(LaunchArgs A
       if (second) block(w1, 2 * j + 1);
       __syncthreads();
     }
-    if (valid && nb > b0 && k4 == 0) {
+    if (valid && nb > b0 && k4 == 0 && wave < NC) {
       if (emits(A, nb)) {
         uint4* o = reinterpret_cast<uint4*>(A.digests + 8ull * A.out_idx[slot] + w0);
         o[0] = make_uint4(bswap(s0), bswap(s1), bswap(s2), bswap(s3));

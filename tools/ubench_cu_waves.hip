@@ -203,6 +203,117 @@ int run_pair2(const char* label) {
   return 0;
 }
 
+// Same-code pair with a workgroup barrier per iteration (B = 1), plus 8 ds_read_b128 and an
+// lgkmcnt(0) wait before it (B = 2): the consumer loop's synchronisation, without producers.
+template <int B>
+__global__ __launch_bounds__(128) void pair_sync(uint32_t* out, uint32_t* cyc, int iters) {
+  __shared__ uint4 lds[512];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  lds[threadIdx.x] = make_uint4(lane, lane, lane, lane);
+  __syncthreads();
+  uint32_t s0 = lane * 3 + 1, s1 = lane * 5 + 2, s2 = lane * 7 + 3, s3 = lane * 11 + 4;
+  uint32_t xa = 0, xb = 0, q1, q2, q3, q4;
+  uint32_t w = lane ^ 0x1234;
+  const uint32_t sh = 6 + (lane & 3), msk = (lane & 4) ? ~0u : 0u;
+  uint64_t t0, t1;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  for (int i = 0; i < iters; ++i) {
+    if (B == 2) {
+      uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint4 v = lds[(lane & 3) + 4 * k + 64 * (i & 1)];
+        acc.x ^= v.x; acc.y ^= v.y;
+      }
+      w ^= acc.x ^ acc.y;
+    }
+    asm volatile(Q64
+                 : [s0] "+v"(s0), [s1] "+v"(s1), [s2] "+v"(s2), [s3] "+v"(s3), [xa] "+v"(xa),
+                   [xb] "+v"(xb), [q1] "=&v"(q1), [q2] "=&v"(q2), [q3] "=&v"(q3), [q4] "=&v"(q4)
+                 : [w] "v"(w), [h1] "v"(sh), [m] "v"(msk));
+    __syncthreads();
+  }
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+  out[blockIdx.x * 128 + threadIdx.x] = s0 ^ s1 ^ s2 ^ s3;
+  if (lane == 0) cyc[blockIdx.x * 2 + wave] = uint32_t(t1 - t0);
+}
+
+template <int B>
+int run_sync(const char* label) {
+  const int iters = 400, grid = 64;
+  uint32_t *out, *cyc;
+  CHECK(hipMalloc(&out, size_t(grid) * 128 * 4));
+  CHECK(hipMalloc(&cyc, size_t(grid) * 2 * 4));
+  for (int rep = 0; rep < 2; ++rep) {
+    hipLaunchKernelGGL(pair_sync<B>, dim3(grid), dim3(128), 0, 0, out, cyc, iters);
+    CHECK(hipDeviceSynchronize());
+  }
+  std::vector<uint32_t> h(grid * 2);
+  CHECK(hipMemcpy(h.data(), cyc, h.size() * 4, hipMemcpyDeviceToHost));
+  double s0 = 0, s1 = 0;
+  for (int b = 0; b < grid; ++b) {
+    s0 += double(h[2 * b]) / (double(iters) * 64 * 9);
+    s1 += double(h[2 * b + 1]) / (double(iters) * 64 * 9);
+  }
+  printf("sync %-34s: wave0 %.3f  wave1 %.3f cycles/instr (incl. sync)\n", label, s0 / grid, s1 / grid);
+  CHECK(hipFree(out));
+  CHECK(hipFree(cyc));
+  return 0;
+}
+
+// Same-code pair with a barrier per iteration; after each barrier wave 1 waits D extra cycles
+// (s_nop D-1, D in 1..8; D = 9..16: two s_nops) before its rounds: does a phase offset
+// restore the paired issue rate?
+template <int D>
+__global__ __launch_bounds__(128) void pair_phase(uint32_t* out, uint32_t* cyc, int iters) {
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t s0 = lane * 3 + 1, s1 = lane * 5 + 2, s2 = lane * 7 + 3, s3 = lane * 11 + 4;
+  uint32_t xa = 0, xb = 0, q1, q2, q3, q4;
+  const uint32_t w = lane ^ 0x1234, sh = 6 + (lane & 3), msk = (lane & 4) ? ~0u : 0u;
+  uint64_t t0, t1;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  for (int i = 0; i < iters; ++i) {
+    if (wave == 1) {
+      if (D >= 1 && D <= 8) asm volatile("s_nop %0" ::"i"(D >= 1 && D <= 8 ? D - 1 : 0));
+      if (D > 8) asm volatile("s_nop 7\n\ts_nop %0" ::"i"(D > 8 ? D - 9 : 0));
+    }
+    asm volatile(Q64
+                 : [s0] "+v"(s0), [s1] "+v"(s1), [s2] "+v"(s2), [s3] "+v"(s3), [xa] "+v"(xa),
+                   [xb] "+v"(xb), [q1] "=&v"(q1), [q2] "=&v"(q2), [q3] "=&v"(q3), [q4] "=&v"(q4)
+                 : [w] "v"(w), [h1] "v"(sh), [m] "v"(msk));
+    __syncthreads();
+  }
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+  out[blockIdx.x * 128 + threadIdx.x] = s0 ^ s1 ^ s2 ^ s3;
+  if (lane == 0) cyc[blockIdx.x * 2 + wave] = uint32_t(t1 - t0);
+}
+
+template <int D>
+int run_phase() {
+  const int iters = 400, grid = 64;
+  uint32_t *out, *cyc;
+  CHECK(hipMalloc(&out, size_t(grid) * 128 * 4));
+  CHECK(hipMalloc(&cyc, size_t(grid) * 2 * 4));
+  for (int rep = 0; rep < 2; ++rep) {
+    hipLaunchKernelGGL(pair_phase<D>, dim3(grid), dim3(128), 0, 0, out, cyc, iters);
+    CHECK(hipDeviceSynchronize());
+  }
+  std::vector<uint32_t> h(grid * 2);
+  CHECK(hipMemcpy(h.data(), cyc, h.size() * 4, hipMemcpyDeviceToHost));
+  double s0 = 0, s1 = 0;
+  for (int b = 0; b < grid; ++b) {
+    s0 += double(h[2 * b]) / (double(iters) * 64 * 9);
+    s1 += double(h[2 * b + 1]) / (double(iters) * 64 * 9);
+  }
+  printf("phase wave1 +%2d nop-cycles after barrier: wave0 %.3f  wave1 %.3f cycles/instr\n", D,
+         s0 / grid, s1 / grid);
+  CHECK(hipFree(out));
+  CHECK(hipFree(cyc));
+  return 0;
+}
+
 int main() {
   for (int grid : {1, 64, 256}) {
     run<1>(grid, 0x1, "1 wave/CU");
@@ -212,6 +323,11 @@ int main() {
     run<4>(grid, 0x7, "3 busy of a 4-wave WG");
     run<8>(grid, 0xff, "8 waves (2 per SIMD)");
   }
+  run_phase<0>(); run_phase<1>(); run_phase<2>(); run_phase<3>(); run_phase<4>();
+  run_phase<5>(); run_phase<6>(); run_phase<7>(); run_phase<8>(); run_phase<10>();
+  run_phase<12>(); run_phase<14>(); run_phase<16>();
+  run_sync<1>("same code + s_barrier/iter");
+  run_sync<2>("same code + 8 ds_read + barrier/iter");
   run_pair2<0, true>("same code");
   run_pair2<1, true>("same code");
   run_pair2<4, true>("same code");
