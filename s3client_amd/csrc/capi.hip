@@ -94,6 +94,15 @@ constexpr uint64_t kMaxParts = 1ull << 31;
 
 uint32_t digest_words(int algo) { return algo == S3H_ALGO_MD5 ? 4u : 8u; }
 
+// Blocks-per-step experiment knob for the NC = 1 quad kernel (S3H_QUAD_BPS=2|4; default 8).
+int quad_bps() {
+  static const int v = [] {
+    const char* e = std::getenv("S3H_QUAD_BPS");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
 // Shadow-consumer experiment knob (S3H_QUAD_SHADOW=1).
 bool quad_shadow() {
   static const bool on = [] {
@@ -224,6 +233,10 @@ int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t
     hipLaunchKernelGGL((s3h::sha256_quad_kernel<1, 1>), dim3(P->grid), dim3(192), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 2 && quad_shadow())
     hipLaunchKernelGGL((s3h::sha256_quad_kernel<2, 1>), dim3(P->grid), dim3(320), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 1 && quad_bps() == 2)
+    hipLaunchKernelGGL((s3h::sha256_quad_kernel<1, 0, 2>), dim3(P->grid), dim3(128), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 1 && quad_bps() == 4)
+    hipLaunchKernelGGL((s3h::sha256_quad_kernel<1, 0, 4>), dim3(P->grid), dim3(128), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 1)
     hipLaunchKernelGGL(s3h::sha256_quad_kernel<1>, dim3(P->grid), dim3(128), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 2)

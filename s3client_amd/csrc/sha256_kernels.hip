@@ -468,13 +468,18 @@ constexpr int kQuadChainsPerWave = 8;
 #define S3H_Q16(S, NX) S3H_QG(S, 0, S##0, 1) S3H_QG(S, 1, S##0, 2) S3H_QG(S, 2, S##0, 3) S3H_QG(S, 3, NX, 0)
 #define S3H_Q16_FIRST S3H_QG_FIRST S3H_QG(a, 1, a0, 2) S3H_QG(a, 2, a0, 3) S3H_QG(a, 3, b0, 0)
 
-template <int NC, int SH = 0>
+template <int NC, int SH = 0, int BPS = 0>
 __global__ __launch_bounds__(64 * (NC * (1 + SH) + 1)) void sha256_quad_kernel(LaunchArgs A) {
   // SH = 1: every consumer wave has a SHADOW wave (wave + NC) running the identical
   // instruction stream on the same chains, output discarded (issue-rate experiment).
   constexpr uint32_t kParts = kQuadChainsPerWave * NC;
   constexpr uint32_t kProducer = NC * (1 + SH);
-  __shared__ uint4 lds_wk[2][2][16][kParts];  // [buffer][block in step][round group][part]
+  // Blocks per step: the producer's 64 lanes each make one (part, block) per step, so a step
+  // covers 64 / kParts blocks (8 at NC = 1) for the same producer issue time, and the
+  // consumers pass one barrier per step instead of one per 2 blocks.
+  constexpr uint32_t kBps = BPS ? BPS : 64 / kParts >= 2 ? 64 / kParts : 2;
+  constexpr uint32_t kLanes = kParts * kBps;  // producer lanes with distinct work (<= 64)
+  __shared__ uint4 lds_wk[2][kBps][16][kParts];  // [buffer][block in step][row][part]
 
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -484,38 +489,40 @@ __global__ __launch_bounds__(64 * (NC * (1 + SH) + 1)) void sha256_quad_kernel(L
   const uint64_t wg_end = wg_nb < A.blk_end ? wg_nb : A.blk_end;
   if (wg_end <= b0) return;
   const uint64_t iters = wg_end - b0;
-  const uint64_t steps = (iters + 1) >> 1;
+  const uint64_t steps = (iters + kBps - 1) / kBps;
 
   if (wave == kProducer) {
     // ---------------------------------------------------------------- producer
     if (A.flags & kPrioAll) __builtin_amdgcn_s_setprio(3);
-    // Lanes 0 .. 2*kParts-1 carry (part, even/odd block); higher lanes repeat them (same loads,
-    // same LDS writes), which keeps every lane on one branch-free path at no extra issue cost.
-    const uint32_t pl = lane % (2 * kParts);
-    const uint32_t part = pl >> 1, half = pl & 1u;
+    // Lane = (part, block h of the step): consecutive lanes take consecutive blocks of one
+    // part (coalesced 64*kBps-byte runs).  Lanes >= kLanes repeat lanes 0.. (same loads, same
+    // LDS writes), which keeps every lane on one branch-free path at no extra issue cost.
+    const uint32_t pl = lane % kLanes;
+    const uint32_t part = pl / kBps, h = pl % kBps;
     const uint32_t slot = slot0 + part;
     Slot s = {0, 0};
     if (slot < A.n) s = A.slots[slot];
-    const uint8_t* p = A.base + s.off + 64ull * (b0 + half - A.blk_origin);
+    const uint8_t* p = A.base + s.off + 64ull * (b0 + h - A.blk_origin);
     const uint32_t sel = be_selector(uint32_t(reinterpret_cast<uintptr_t>(A.base + s.off) & 3));
     const uint64_t fend = fetch_end(s.len, A.blk_end);
-    const uint64_t bh = b0 + half;
+    const uint64_t bh = b0 + h;
     const uint64_t bits = slot < A.n ? msg_bits(A, slot, s.len) : 0;
+    constexpr uint64_t kStride = 64ull * kBps;
     RawBlock ra, rb;
     fetch_full(p, bh < fend, A.zero, ra);
-    fetch_full(p + 128, bh + 2 < fend, A.zero, rb);
-    produce_block(ra, sel, p, s.len, bits, bh, A.blk_end, lds_wk[0][half], part);
+    fetch_full(p + kStride, bh + kBps < fend, A.zero, rb);
+    produce_block(ra, sel, p, s.len, bits, bh, A.blk_end, lds_wk[0][h], part);
     __syncthreads();
     for (uint64_t k = 1; k <= steps; k += 2) {
       if (k < steps) {
-        fetch_full(p + 128 * (k + 1), bh + 2 * (k + 1) < fend, A.zero, ra);
-        produce_block(rb, sel, p + 128 * k, s.len, bits, bh + 2 * k, A.blk_end, lds_wk[1][half], part);
+        fetch_full(p + kStride * (k + 1), bh + kBps * (k + 1) < fend, A.zero, ra);
+        produce_block(rb, sel, p + kStride * k, s.len, bits, bh + kBps * k, A.blk_end, lds_wk[1][h], part);
       }
       __syncthreads();
       if (k + 1 > steps) break;
       if (k + 1 < steps) {
-        fetch_full(p + 128 * (k + 2), bh + 2 * (k + 2) < fend, A.zero, rb);
-        produce_block(ra, sel, p + 128 * (k + 1), s.len, bits, bh + 2 * (k + 1), A.blk_end, lds_wk[0][half], part);
+        fetch_full(p + kStride * (k + 2), bh + kBps * (k + 2) < fend, A.zero, rb);
+        produce_block(ra, sel, p + kStride * (k + 1), s.len, bits, bh + kBps * (k + 1), A.blk_end, lds_wk[0][h], part);
       }
       __syncthreads();
     }
@@ -578,18 +585,25 @@ __global__ __launch_bounds__(64 * (NC * (1 + SH) + 1)) void sha256_quad_kernel(L
         s3 = live ? s3 + n3 : s3;
       }
     };
+    auto load = [&](uint4 W[4], uint32_t buf, uint32_t blk) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) W[q] = lds_wk[buf][blk][k4 + 4 * q][part];
+    };
     __syncthreads();
     for (uint64_t j = 0; j < steps; ++j) {
-      const bool second = 2 * j + 1 < iters;
-      uint4 w0[4], w1[4];
+      // The next block's W+K is read while the current block runs: only the step's first read
+      // waits on LDS latency.
+      const uint32_t buf = uint32_t(j & 1);
+      const uint64_t base_i = kBps * j;
+      uint4 wa[4], wb[4];
+      load(wa, buf, 0);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        w0[q] = lds_wk[j & 1][0][k4 + 4 * q][part];
-        w1[q] = lds_wk[j & 1][1][k4 + 4 * q][part];
+      for (uint32_t i = 0; i < kBps; i += 2) {
+        load(wb, buf, i + 1);
+        if (base_i + i < iters) block(wa, base_i + i);
+        if (i + 2 < kBps) load(wa, buf, i + 2);
+        if (base_i + i + 1 < iters) block(wb, base_i + i + 1);
       }
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-      block(w0, 2 * j);
-      if (second) block(w1, 2 * j + 1);
       __syncthreads();
     }
     if (valid && nb > b0 && k4 == 0 && wave < NC) {
