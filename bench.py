@@ -35,7 +35,7 @@ LONE_WAVE_CPI = 4.70            # one wave alone, round-shaped VALU stream (tool
 # pair = 640 round VALU + state/X bookkeeping + 16 ds_read_b128).  A lone wave issues about
 # one instruction per 5 cycles (profiles/r01_ubench_valu_issue.txt): this, not HBM, bounds
 # each part's chain.
-CHAIN_INSTR_PER_BLOCK = {"quad": 592, "pair": 672, "pc": 923, "lane": 1425, "md5-pc": 280}
+CHAIN_INSTR_PER_BLOCK = {"skew": 541, "quad": 592, "pair": 672, "pc": 923, "lane": 1425, "md5-pc": 280}
 
 
 def parse():
@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4"])
     ap.add_argument("--parts-per-gpu", type=int, default=0, help="override batch size")
     ap.add_argument("--part-bytes", type=int, default=0, help="override part size (sweeps)")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "quad", "pair", "pc", "lane"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "skew", "quad", "pair", "pc", "lane"])
     ap.add_argument("--algo", default="sha256", choices=["sha256", "md5"],
                     help="md5: the SURVEY 8(f) Content-MD5/ETag kernel (not the metric)")
     ap.add_argument("--cpu-sample-parts", type=int, default=384)

@@ -165,12 +165,12 @@ int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* le
     kernel = S3H_KERNEL_PC;
   }
   if (kernel == S3H_KERNEL_AUTO)
-    kernel = n <= kQuadMaxParts ? S3H_KERNEL_QUAD
+    kernel = n <= kQuadMaxParts ? S3H_KERNEL_SKEW
              : n <= kPairMaxParts ? S3H_KERNEL_PAIR
              : n <= kPcMaxParts   ? S3H_KERNEL_PC
                                   : S3H_KERNEL_LANE;
   if (kernel != S3H_KERNEL_PC && kernel != S3H_KERNEL_LANE && kernel != S3H_KERNEL_PAIR &&
-      kernel != S3H_KERNEL_QUAD)
+      kernel != S3H_KERNEL_QUAD && kernel != S3H_KERNEL_SKEW)
     return fail(S3H_EINVAL, "plan: unknown kernel %d", kernel);
 
   std::vector<uint32_t> order(n);
@@ -184,10 +184,11 @@ int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* le
   P->n = n;
   P->total_blocks = total;
   P->max_blocks = s3h::nblocks(slots[0].len);
-  P->quad_waves = quad_waves(n);
+  P->quad_waves = kernel == S3H_KERNEL_SKEW && quad_waves(n) > 2 ? 2 : quad_waves(n);
   P->grid = kernel == S3H_KERNEL_PC     ? uint32_t((n + 63) / 64)
             : kernel == S3H_KERNEL_PAIR ? uint32_t((n + s3h::kPairParts - 1) / s3h::kPairParts)
-            : kernel == S3H_KERNEL_QUAD ? uint32_t((n + 8 * quad_waves(n) - 1) / (8 * quad_waves(n)))
+            : kernel == S3H_KERNEL_QUAD || kernel == S3H_KERNEL_SKEW
+                ? uint32_t((n + 8 * P->quad_waves - 1) / (8 * P->quad_waves))
                                         : uint32_t((n + 255) / 256);
 
   DeviceGuard g(device);
@@ -227,6 +228,10 @@ int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t
   A.flags = flags | prio_flags();
   if (P->algo == S3H_ALGO_MD5)
     hipLaunchKernelGGL(s3h::md5_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_SKEW && P->quad_waves == 1)
+    hipLaunchKernelGGL(s3h::sha256_skew_kernel<1>, dim3(P->grid), dim3(128), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_SKEW)
+    hipLaunchKernelGGL(s3h::sha256_skew_kernel<2>, dim3(P->grid), dim3(192), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_PC)
     hipLaunchKernelGGL(s3h::sha256_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 1 && quad_shadow())

@@ -617,6 +617,227 @@ __global__ __launch_bounds__(64 * (NC * (1 + SH) + 1)) void sha256_quad_kernel(L
   }
 }
 
+// ------------------------------------------------------------- skewed lane-octet kernel
+// The quad kernel's lane layout (each chain on 8 lanes: e-quad + a-quad) with the a-quad run
+// two rounds BEHIND the e-quad (tools/gen_skew.py derives and simulates the schedule).  The
+// skew turns both halves' updates into "own nonlinear part + one precomputed sum", and the
+// sum for the next round is one row_half_mirror DPP add (cross term + W+K) plus one v_xad
+// (own term, negated in the a-quad by a per-lane mask): 8 VALU per round instead of 9.  The
+// pipeline runs across blocks (the a-quad finishes block k in block k+1's first two rounds);
+// the feed-forward and three boundary corrections add 11 VALU per block: 523 per block in all,
+// against the quad kernel's 592.  Each lane needs its own copy of every W+K word (the DPP
+// operand slot carries the cross term), so the consumer reads all 16 rows per block; the
+// a-quad lanes read a column of ones (their "W" restores the +1 of ~x = -x - 1).
+#include "sha256_skew_rounds.inc"
+
+#define S3H_SKEW_STATE                                                                        \
+  [g0_0] "+v"(g00), [g0_1] "+v"(g01), [g1_0] "+v"(g10), [g1_1] "+v"(g11), [e0_0] "+v"(e00),    \
+      [e0_1] "+v"(e01), [e0_2] "+v"(e02), [e0_3] "+v"(e03), [e1_0] "+v"(e10), [e1_1] "+v"(e11), \
+      [e1_2] "+v"(e12), [e1_3] "+v"(e13), [n0] "+v"(n0), [n1] "+v"(n1), [n2] "+v"(n2),          \
+      [n3] "+v"(n3), [x0] "+v"(x0), [x1] "+v"(x1), [q1] "=&v"(q1), [q3] "=&v"(q3),               \
+      [sl] "=&v"(sl), [cm] "=&v"(cm), [t] "=&v"(tt)
+#define S3H_SKEW_W(W)                                                                           \
+  [w1] "v"(W[1]), [w2] "v"(W[2]), [w3] "v"(W[3]), [w4] "v"(W[4]), [w5] "v"(W[5]), [w6] "v"(W[6]), \
+      [w7] "v"(W[7]), [w8] "v"(W[8]), [w9] "v"(W[9]), [w10] "v"(W[10]), [w11] "v"(W[11]),         \
+      [w12] "v"(W[12]), [w13] "v"(W[13]), [w14] "v"(W[14]), [w15] "v"(W[15]), [w16] "v"(W[16]),   \
+      [w17] "v"(W[17]), [w18] "v"(W[18]), [w19] "v"(W[19]), [w20] "v"(W[20]), [w21] "v"(W[21]),   \
+      [w22] "v"(W[22]), [w23] "v"(W[23]), [w24] "v"(W[24]), [w25] "v"(W[25]), [w26] "v"(W[26]),   \
+      [w27] "v"(W[27]), [w28] "v"(W[28]), [w29] "v"(W[29]), [w30] "v"(W[30]), [w31] "v"(W[31]),   \
+      [w32] "v"(W[32]), [w33] "v"(W[33]), [w34] "v"(W[34]), [w35] "v"(W[35]), [w36] "v"(W[36]),   \
+      [w37] "v"(W[37]), [w38] "v"(W[38]), [w39] "v"(W[39]), [w40] "v"(W[40]), [w41] "v"(W[41]),   \
+      [w42] "v"(W[42]), [w43] "v"(W[43]), [w44] "v"(W[44]), [w45] "v"(W[45]), [w46] "v"(W[46]),   \
+      [w47] "v"(W[47]), [w48] "v"(W[48]), [w49] "v"(W[49]), [w50] "v"(W[50]), [w51] "v"(W[51]),   \
+      [w52] "v"(W[52]), [w53] "v"(W[53]), [w54] "v"(W[54]), [w55] "v"(W[55]), [w56] "v"(W[56]),   \
+      [w57] "v"(W[57]), [w58] "v"(W[58]), [w59] "v"(W[59]), [w60] "v"(W[60]), [w61] "v"(W[61]),   \
+      [w62] "v"(W[62]), [w63] "v"(W[63]), [am] "v"(am), [mk] "v"(mk)
+
+template <int NC>
+__global__ __launch_bounds__(64 * (NC + 1)) void sha256_skew_kernel(LaunchArgs A) {
+  constexpr uint32_t kParts = kQuadChainsPerWave * NC;
+  constexpr uint32_t kBps = 64 / kParts >= 2 ? 64 / kParts : 2;  // blocks per producer step
+  constexpr uint32_t kLanes = kParts * kBps;
+  constexpr uint32_t kCols = kParts + 1;  // column kParts holds ones (read by the a-quads)
+  __shared__ uint4 lds_wk[2][kBps][16][kCols];
+
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t slot0 = blockIdx.x * kParts;
+  const uint64_t b0 = A.blk_begin;
+  const uint64_t wg_nb = slot_blocks(A, A.slots[slot0].len);
+  const uint64_t wg_end = wg_nb < A.blk_end ? wg_nb : A.blk_end;
+  if (wg_end <= b0) return;
+  const uint64_t iters = wg_end - b0;
+  const uint64_t steps = (iters + kBps - 1) / kBps;
+
+  if (wave == NC) {
+    // ---------------------------------------------------------------- producer (as quad)
+    for (uint32_t i = lane; i < 2 * kBps * 16; i += 64)
+      lds_wk[i / (kBps * 16)][(i / 16) % kBps][i % 16][kParts] = make_uint4(1u, 1u, 1u, 1u);
+    const uint32_t pl = lane % kLanes;
+    const uint32_t part = pl / kBps, h = pl % kBps;
+    const uint32_t slot = slot0 + part;
+    Slot s = {0, 0};
+    if (slot < A.n) s = A.slots[slot];
+    const uint8_t* p = A.base + s.off + 64ull * (b0 + h - A.blk_origin);
+    const uint32_t sel = be_selector(uint32_t(reinterpret_cast<uintptr_t>(A.base + s.off) & 3));
+    const uint64_t fend = fetch_end(s.len, A.blk_end);
+    const uint64_t bh = b0 + h;
+    const uint64_t bits = slot < A.n ? msg_bits(A, slot, s.len) : 0;
+    constexpr uint64_t kStride = 64ull * kBps;
+    RawBlock ra, rb;
+    fetch_full(p, bh < fend, A.zero, ra);
+    fetch_full(p + kStride, bh + kBps < fend, A.zero, rb);
+    produce_block(ra, sel, p, s.len, bits, bh, A.blk_end, lds_wk[0][h], part);
+    __syncthreads();
+    for (uint64_t k = 1; k <= steps; k += 2) {
+      if (k < steps) {
+        fetch_full(p + kStride * (k + 1), bh + kBps * (k + 1) < fend, A.zero, ra);
+        produce_block(rb, sel, p + kStride * k, s.len, bits, bh + kBps * k, A.blk_end, lds_wk[1][h], part);
+      }
+      __syncthreads();
+      if (k + 1 > steps) break;
+      if (k + 1 < steps) {
+        fetch_full(p + kStride * (k + 2), bh + kBps * (k + 2) < fend, A.zero, rb);
+        produce_block(ra, sel, p + kStride * (k + 1), s.len, bits, bh + kBps * (k + 1), A.blk_end, lds_wk[0][h], part);
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  // ------------------------------------------------------------------ consumer
+  if (!(A.flags & kPrioNone)) __builtin_amdgcn_s_setprio(3);
+  const uint32_t part = kQuadChainsPerWave * wave + (lane >> 3);
+  const bool ahalf = (lane >> 2) & 1u;
+  const uint32_t k4 = lane & 3u;
+  const uint32_t slot = slot0 + part;
+  const bool valid = slot < A.n;
+  const uint64_t nb = valid ? slot_blocks(A, A.slots[slot].len) : 0;
+  const uint32_t last_slot = (slot0 + kParts <= A.n ? slot0 + kParts : A.n) - 1;
+  const uint64_t live_end = slot_blocks(A, A.slots[last_slot].len);  // every chain live below
+  // Rotation per lane: positions 0..2 of a quad take the three Sigma amounts, 3 repeats 0.
+  const uint32_t am = ahalf ? (k4 == 1 ? 22u : k4 == 2 ? 13u : 2u) : (k4 == 1 ? 11u : k4 == 2 ? 25u : 6u);
+  const uint32_t mk = ahalf ? 0xffffffffu : 0u;
+  const uint32_t one_a = ahalf ? 1u : 0u;
+  uint32_t H[8];
+  if (valid && resumes(A)) {
+    const uint4* sp = reinterpret_cast<const uint4*>(A.state + 8ull * A.out_idx[slot]);
+    const uint4 u = sp[0], v = sp[1];
+    H[0] = u.x; H[1] = u.y; H[2] = u.z; H[3] = u.w; H[4] = v.x; H[5] = v.y; H[6] = v.z; H[7] = v.w;
+  } else {
+    init_state(H);
+  }
+  // Register image before block 0 (parity 0): gen_skew.py init_regs().  The a-quad's two
+  // rounds of the (virtual) previous block compute zeros and its feed-forward adds H.
+  uint32_t e13 = ahalf ? 0u : H[4], e12 = ahalf ? 0u : H[5], e11 = ahalf ? 0u : H[6],
+           e10 = ahalf ? 0u : H[7];
+  uint32_t e03 = ahalf ? H[2] : H[4], e02 = ahalf ? H[3] : 0u, e01 = 0, e00 = 0;
+  uint32_t g11 = ahalf ? H[0] : 0u, g10 = ahalf ? H[1] : 0u, g01 = 0, g00 = 0;
+  uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0, x0, x1 = 0;
+  uint32_t q1, q3, sl, cm, tt;
+  // Per-lane LDS base (buffer 0, block 0, row 0, own column): block and buffer offsets are
+  // immediates of the 16 ds_read_b128 that fetch one block's W+K.
+  const uint4* lbase = &lds_wk[0][0][0][ahalf ? kParts : part];
+  constexpr uint32_t kBlkStride = 16 * kCols, kBufStride = kBps * 16 * kCols;
+  auto load = [&](uint32_t (&w)[64], const uint4* src) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint4 v = src[r * kCols];
+      w[4 * r] = v.x; w[4 * r + 1] = v.y; w[4 * r + 2] = v.z; w[4 * r + 3] = v.w;
+    }
+  };
+  // Final state of chains that end inside the pipeline: captured after the block that
+  // follows their last one (a-half fed forward in its round 1).  Blocks below cap_from
+  // (every chain of the workgroup still live) skip the check with one scalar branch.
+  uint32_t f0 = 0, f1 = 0, f2 = 0, f3 = 0;
+#define S3H_SKEW_CAPTURE(EP3, EP2, EP1, EP0, GQ1, GQ0) \
+  do {                                                 \
+    f0 = ahalf ? GQ1 : EP3;                            \
+    f1 = ahalf ? GQ0 : EP2;                            \
+    f2 = ahalf ? EP3 : EP1;                            \
+    f3 = ahalf ? EP2 : EP0;                            \
+  } while (0)
+
+  const uint32_t it32 = uint32_t(iters);  // < 2^31: the host splits longer launches
+  // first block after which a chain can have ended (>= 1: block 0 ends none)
+  const uint32_t cap_from = __builtin_amdgcn_readfirstlane(
+      uint32_t(live_end > b0 + 1 ? live_end - b0 : 1));
+  const uint32_t nb_rel = nb > b0 ? uint32_t(nb - b0) : 0u;
+
+  uint32_t wa[64], wb[64];
+  __syncthreads();
+  load(wa, lbase);
+  x0 = ahalf ? 0u : H[3] + H[7] + wa[0];
+  // One block: rounds 0-15, then (after the step barrier when the next block lives in the
+  // other LDS buffer, or this is the last block) the next block's 16 rows are read while
+  // rounds 16-63 run; NEXT consumes the next block's first word.  The a-quad lanes read the
+  // ones column, so their NEXT word is 1 even past the last block.
+#define S3H_SKEW_BLOCK(P, CUR, NXT)                                                             \
+  {                                                                                             \
+    const uint32_t bb = j * kBps + i;                                                           \
+    asm volatile(S3H_ALIGN8 S3H_SKEW_ROUNDS_A_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));          \
+    if (i == kBps - 1) {                                                                        \
+      __syncthreads();                                                                          \
+      load(NXT, nbuf);                                                                          \
+    } else {                                                                                    \
+      if (bb + 1 >= it32) __syncthreads();                                                      \
+      load(NXT, buf + (i + 1) * kBlkStride);                                                    \
+    }                                                                                           \
+    asm volatile(S3H_ALIGN8 S3H_SKEW_ROUNDS_B_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));          \
+    if (bb >= cap_from) {                                                                       \
+      asm volatile("; ragged tail: capture check");  /* keeps this branch scalar */           \
+      if (nb_rel == bb) {                                                                       \
+        if (P == 0) S3H_SKEW_CAPTURE(e13, e12, e11, e10, g01, g00);                             \
+        else S3H_SKEW_CAPTURE(e03, e02, e01, e00, g11, g10);                                    \
+      }                                                                                         \
+    }                                                                                           \
+    asm volatile(S3H_ALIGN8 S3H_SKEW_NEXT_##P                                                   \
+                 : S3H_SKEW_STATE : [w0] "v"(NXT[0]), [am] "v"(am), [mk] "v"(mk));              \
+    if (bb + 1 >= it32) goto drain;                                                             \
+  }
+  for (uint32_t j = 0;; ++j) {
+    const uint4* buf = lbase + (j & 1) * kBufStride;
+    const uint4* nbuf = lbase + ((j + 1) & 1) * kBufStride;
+#pragma unroll
+    for (uint32_t h = 0; h < kBps / 2; ++h) {
+      {
+        const uint32_t i = 2 * h;
+        S3H_SKEW_BLOCK(0, wa, wb)
+      }
+      {
+        const uint32_t i = 2 * h + 1;
+        S3H_SKEW_BLOCK(1, wb, wa)
+      }
+    }
+  }
+drain:
+  // The a-quad's last two rounds of the last block (parity (iters-1)&1) run as rounds 0-1
+  // of a virtual block of the other parity (W = 1 in the a-quad); then every chain still
+  // live is captured.
+  {
+    uint32_t wd[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) wd[i] = one_a;
+    if (it32 & 1) {
+      asm volatile(S3H_ALIGN8 S3H_SKEW_DRAIN_1 : S3H_SKEW_STATE : S3H_SKEW_W(wd));
+      if (nb_rel >= it32) S3H_SKEW_CAPTURE(e03, e02, e01, e00, g11, g10);
+    } else {
+      asm volatile(S3H_ALIGN8 S3H_SKEW_DRAIN_0 : S3H_SKEW_STATE : S3H_SKEW_W(wd));
+      if (nb_rel >= it32) S3H_SKEW_CAPTURE(e13, e12, e11, e10, g01, g00);
+    }
+  }
+#undef S3H_SKEW_BLOCK
+#undef S3H_SKEW_CAPTURE
+  if (valid && nb > b0 && k4 == 0) {
+    const uint32_t w0 = ahalf ? 0u : 4u;
+    if (emits(A, nb)) {
+      uint4* o = reinterpret_cast<uint4*>(A.digests + 8ull * A.out_idx[slot] + w0);
+      o[0] = make_uint4(bswap(f0), bswap(f1), bswap(f2), bswap(f3));
+    } else if (A.state) {
+      reinterpret_cast<uint4*>(A.state + 8ull * A.out_idx[slot] + w0)[0] = make_uint4(f0, f1, f2, f3);
+    }
+  }
+}
+
 // ------------------------------------------------------------- MD5 (producer/consumer)
 // Batched MD5 for Content-MD5 / multipart-ETag verification (reference
 // lib/hash/md5.cpp:71-116 for the step function, :158-172 for the padding).  Same

@@ -9,7 +9,7 @@ import s3client_amd as s3
 
 pytestmark = pytest.mark.gpu
 SEED = 20241008
-KERNELS = ["quad", "pair", "pc", "lane"]
+KERNELS = ["skew", "quad", "pair", "pc", "lane"]
 
 
 def _dev_buffer(torch, host: np.ndarray):
@@ -65,7 +65,7 @@ def test_kernels_agree_on_many_small_parts(torch_cuda, oracle):
     """n > 65536 exercises the AUTO switch to the fused kernel; overlapping parts allowed."""
     assert s3.Plan([0] * 70000, [1] * 70000).info()["kernel"] == "lane"
     assert s3.Plan([0] * 40000, [1] * 40000).info()["kernel"] == "pc"
-    assert s3.Plan([0] * 1024, [1] * 1024).info()["kernel"] == "quad"
+    assert s3.Plan([0] * 1024, [1] * 1024).info()["kernel"] == "skew"
     assert s3.Plan([0] * 10000, [1] * 10000).info()["kernel"] == "pair"
     rng = np.random.default_rng(7)
     n = 70000
@@ -74,7 +74,7 @@ def test_kernels_agree_on_many_small_parts(torch_cuda, oracle):
     host = rng.integers(0, 256, (1 << 20) + 256, dtype=np.uint8)
     data = _dev_buffer(torch_cuda, host)
     a = s3.sha256_batch_device(data, offs, lens, kernel="auto").cpu().numpy().view(np.uint32)
-    for k in ("pc", "pair", "quad"):
+    for k in ("pc", "pair", "quad", "skew"):
         b = s3.sha256_batch_device(data, offs, lens, kernel=k).cpu().numpy().view(np.uint32)
         assert np.array_equal(a, b), k
     idx = rng.choice(n, 500, replace=False)
@@ -111,7 +111,7 @@ def test_c2_full_batch_bit_exact(torch_cuda, oracle, golden, kernel):
     txt = s3.digests_to_text(out)
     for e in golden["c2_parts"]:
         assert txt[e["p"]] == e["digest"], e["p"]
-    if kernel in ("quad", "pair"):
+    if kernel in ("skew", "quad", "pair"):
         host = data.cpu().numpy()
         want = oracle.batch(host, offs, lens, threads=16)
         assert np.array_equal(out, want)
@@ -271,15 +271,16 @@ def test_verify_download_parts(torch_cuda, golden):
     assert n == 1 and mask.cpu().tolist() == [False] * 4 + [True, False]
 
 
-def test_quad_two_consumer_waves_ragged(torch_cuda, oracle):
-    """3,000 parts: the quad plan runs two consumer waves per workgroup (grid 188 <= 256)."""
+@pytest.mark.parametrize("kernel", ["quad", "skew"])
+def test_quad_two_consumer_waves_ragged(torch_cuda, oracle, kernel):
+    """3,000 parts: the quad / skew plan runs two consumer waves per workgroup (grid 188)."""
     rng = np.random.default_rng(31)
     n = 3000
-    plan = s3.Plan([0] * n, [1] * n, kernel="quad")
+    plan = s3.Plan([0] * n, [1] * n, kernel=kernel)
     assert plan.info()["grid"] == (n + 15) // 16
     lens = rng.integers(0, 9000, n)
     lens[:4] = [0, 55, 56, 64]
     offs = np.concatenate([[0], np.cumsum(lens + rng.integers(0, 5, n))[:-1]])
     host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 8, dtype=np.uint8)
-    got = _run(torch_cuda, host, offs, lens, "quad")
+    got = _run(torch_cuda, host, offs, lens, kernel)
     assert np.array_equal(got, oracle.batch(host, offs, lens))
