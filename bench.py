@@ -29,13 +29,13 @@ sys.path.insert(0, ROOT)
 SEED = 20241008
 MIB = 1 << 20
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-CLOCK_GHZ = 2.4                 # in-kernel clock measured by tools/ubench (2.39-2.40 GHz)
-LONE_WAVE_CPI = 4.70            # one wave alone, round-shaped VALU stream (tools/ubench_round)
-# Instructions one chain's wave issues per 64-B block (ISA audit: `make isa`, consumer loop;
-# pair = 640 round VALU + state/X bookkeeping + 16 ds_read_b128).  A lone wave issues about
-# one instruction per 5 cycles (profiles/r01_ubench_valu_issue.txt): this, not HBM, bounds
-# each part's chain.
-CHAIN_INSTR_PER_BLOCK = {"skew": 541, "quad": 592, "pair": 672, "pc": 923, "lane": 1425, "md5-pc": 280}
+CLOCK_GHZ = 2.4                 # MI355X peak engine clock (used when no clock probe ran)
+ISSUE_FLOOR_CPI = 4.0           # one wave: <= 1 instruction per 4 cycles (MI355X_MICROARCH.md)
+# Instructions one chain's wave issues per 64-B block (ISA audit of the consumer loop:
+# `make isa` + llvm-objdump; skew = 523 VALU + 16 ds_read_b128 + 2 s_waitcnt + ~2 alignment
+# s_nop + loop control; pair = 640 round VALU + bookkeeping + 16 ds_read_b128).  A wave issues
+# at most one instruction per ~4 cycles: this, not HBM, bounds each part's chain.
+CHAIN_INSTR_PER_BLOCK = {"skew": 544, "quad": 592, "pair": 672, "pc": 923, "lane": 1425, "md5-pc": 280}
 
 
 def parse():
@@ -208,6 +208,25 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)  # max over ranks: the slowest GPU sets the time
     wall, kern_ms_max = float(t[0]), float(t[1])
 
+    # Clock probe (outside the timed region): one more launch on which every consumer wave
+    # records s_memtime / s_memrealtime around its chain loop -> live shader clock and cycles
+    # per block (skew kernel only).
+    probe = None
+    if kname == "skew":
+        clocks = torch.zeros(4 * 4 * info["grid"], dtype=torch.int64, device=dev)
+        waves = plan.set_clock_probe(clocks)
+        plan.launch(data, digests, stream)
+        torch.cuda.synchronize(dev)
+        plan.set_clock_probe(None)
+        c = clocks.view(-1, 4)[:waves].cpu().numpy().astype(np.float64)
+        cyc, rt = c[:, 1] - c[:, 0], c[:, 3] - c[:, 2]
+        ok = rt > 0
+        if ok.any():
+            ghz = float(np.median(cyc[ok] / rt[ok] * 0.1))  # rt ticks at 100 MHz
+            probe = {"clock_GHz": round(ghz, 3),
+                     "cycles_per_block": round(float(np.max(cyc[ok])) / info["max_blocks"], 1),
+                     "waves": int(ok.sum())}
+
     # parity spot-check of the last timed step's digests against the reference fixtures
     gd = digests.cpu().numpy().view(np.uint32)
     with open(os.path.join(ROOT, "tests", "golden", "sha256_golden.json")) as f:
@@ -236,16 +255,22 @@ def main():
     # one part = one sequential chain on one lane: report what one chain sustains and how
     # many of the chip's 256 CU x 4 SIMD x 64 = 65,536 lanes the batch can occupy
     chain_gbps = float(lens.max()) / (kern_ms / 1e3) / 1e9
-    cyc_per_block = kern_ms / 1e3 * CLOCK_GHZ * 1e9 / info["max_blocks"]
+    if probe:
+        cyc_per_block, clock_src = probe["cycles_per_block"], "in-kernel s_memtime probe"
+    else:
+        cyc_per_block = kern_ms / 1e3 * CLOCK_GHZ * 1e9 / info["max_blocks"]
+        clock_src = f"kernel time x assumed {CLOCK_GHZ} GHz"
     cpi = cyc_per_block / CHAIN_INSTR_PER_BLOCK[kname]
     issue = {"bound": "per-wave instruction issue of each part's sequential chain",
              "chain_instr_per_block": CHAIN_INSTR_PER_BLOCK[kname],
-             "cycles_per_block": round(cyc_per_block, 1),
+             "cycles_per_block": round(cyc_per_block, 1), "cycles_source": clock_src,
              "cycles_per_instr": round(cpi, 3),
-             # floor: a lone wave's measured issue rate on a round-shaped stream
-             # (profiles/r01_ubench_pair_round.txt, 4.70 cycles per instruction)
-             "lone_wave_issue_cycles_measured": LONE_WAVE_CPI,
-             "frac": round(LONE_WAVE_CPI / cpi, 4), "clock_GHz_assumed": CLOCK_GHZ,
+             # floor: one wave issues at most one instruction per 4 cycles (MI355X_MICROARCH.md
+             # 'vector-instruction ISSUE cost'; 4.05 measured on an aligned lone-wave stream,
+             # profiles/r01_ubench_alignment.txt)
+             "issue_floor_cycles_per_instr": ISSUE_FLOOR_CPI,
+             "frac": round(ISSUE_FLOOR_CPI / cpi, 4),
+             "clock_GHz": probe["clock_GHz"] if probe else CLOCK_GHZ,
              # chip-wide INT32-VALU roof (256 CU x 64 lanes x clock / VALU per
              # block of the one-lane-per-part kernel x 64 B) and the parallelism ceiling
              "valu_roof_GBps": round(256 * 64 * CLOCK_GHZ * 1e9 / CHAIN_INSTR_PER_BLOCK["lane"]

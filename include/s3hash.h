@@ -86,6 +86,14 @@ int s3h_plan_launch_range(s3h_plan_t plan, const void *d_base, uint32_t *d_diges
 int s3h_plan_info(s3h_plan_t plan, uint64_t *n, uint64_t *total_blocks, uint64_t *max_blocks,
                   int *kernel, uint32_t *grid);
 
+/* Measurement hook (not part of the lib/hash surface): while d_clocks (device memory,
+ * 4 x *waves uint64) is set, every launch of a plan on the skew kernel records, per consumer
+ * wave, the shader-clock counter (s_memtime) and the 100 MHz real-time counter
+ * (s_memrealtime) at the start and end of its chain loop: {clk0, clk1, rt0, rt1}.  *waves
+ * receives the number of consumer waves (0: the plan's kernel does not record).  NULL turns
+ * the probe off.  bench.py uses it to report cycles per block and the live shader clock. */
+int s3h_plan_set_clock_probe(s3h_plan_t plan, uint64_t *d_clocks, uint32_t *waves);
+
 /* One-shot convenience: plan + launch + wait.  Returns when d_digests is complete. */
 int s3h_sha256_batch_device(int device, const void *d_base, const uint64_t *offsets,
                             const uint64_t *lengths, uint64_t n, uint32_t *d_digests,

@@ -29,7 +29,7 @@ C_ABI_SYMBOLS = (
     "s3h_md5_batch_device", "s3h_md5_batch_host", "s3h_verify_batch_device",
     "s3h_verify_batch_host", "s3h_stream_create", "s3h_stream_update_device",
     "s3h_stream_final_device", "s3h_stream_update_host", "s3h_stream_final_host",
-    "s3h_stream_total", "s3h_stream_destroy",
+    "s3h_stream_total", "s3h_stream_destroy", "s3h_plan_set_clock_probe",
 )
 ALGO_SHA256, ALGO_MD5 = 0, 1
 ALGO_IDS = {"sha256": ALGO_SHA256, "md5": ALGO_MD5}
@@ -86,6 +86,8 @@ def lib() -> ctypes.CDLL:
             L.s3h_plan_launch_range.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                 ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                 ctypes.c_void_p]
+            L.s3h_plan_set_clock_probe.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
+                                                   ctypes.POINTER(ctypes.c_uint32)]
             L.s3h_plan_info.argtypes = [ctypes.c_void_p, u64p, u64p, u64p,
                                         ctypes.POINTER(ctypes.c_int), u32p]
             L.s3h_sha256_batch_device.argtypes = [ctypes.c_int, ctypes.c_void_p, u64p, u64p,

@@ -76,6 +76,7 @@ struct s3h_plan_s {
   uint32_t* d_state = nullptr;  // n*8 chaining words, allocated on first ranged launch
   uint8_t* d_zero = nullptr;    // 256 zero bytes: load target for out-of-range lanes
   int quad_waves = 1;           // quad kernel: consumer waves per workgroup (1-4)
+  uint64_t* d_clocks = nullptr; // clock probe buffer (caller-owned), see s3h_plan_set_clock_probe
 };
 
 namespace {
@@ -184,7 +185,8 @@ int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* le
   P->n = n;
   P->total_blocks = total;
   P->max_blocks = s3h::nblocks(slots[0].len);
-  P->quad_waves = kernel == S3H_KERNEL_SKEW && quad_waves(n) > 2 ? 2 : quad_waves(n);
+  // skew: 1, 2 or 4 consumer waves (3 runs as 4)
+  P->quad_waves = kernel == S3H_KERNEL_SKEW && quad_waves(n) == 3 ? 4 : quad_waves(n);
   P->grid = kernel == S3H_KERNEL_PC     ? uint32_t((n + 63) / 64)
             : kernel == S3H_KERNEL_PAIR ? uint32_t((n + s3h::kPairParts - 1) / s3h::kPairParts)
             : kernel == S3H_KERNEL_QUAD || kernel == S3H_KERNEL_SKEW
@@ -226,12 +228,21 @@ int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t
   A.blk_origin = origin;
   A.n = uint32_t(P->n);
   A.flags = flags | prio_flags();
+  A.clocks = P->d_clocks;
   if (P->algo == S3H_ALGO_MD5)
     hipLaunchKernelGGL(s3h::md5_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
+  // The skew kernel counts a launch's blocks in 32 bits: a range of 2^31 blocks (128 GiB of
+  // one part) or more runs on the quad kernel (same plan geometry, 64-bit counters).
+  else if (P->kernel == S3H_KERNEL_SKEW && b1 - b0 >= (1ull << 31) && P->quad_waves == 1)
+    hipLaunchKernelGGL(s3h::sha256_quad_kernel<1>, dim3(P->grid), dim3(128), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_SKEW && b1 - b0 >= (1ull << 31))
+    hipLaunchKernelGGL(s3h::sha256_quad_kernel<2>, dim3(P->grid), dim3(192), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_SKEW && P->quad_waves == 1)
     hipLaunchKernelGGL(s3h::sha256_skew_kernel<1>, dim3(P->grid), dim3(128), 0, stream, A);
-  else if (P->kernel == S3H_KERNEL_SKEW)
+  else if (P->kernel == S3H_KERNEL_SKEW && P->quad_waves == 2)
     hipLaunchKernelGGL(s3h::sha256_skew_kernel<2>, dim3(P->grid), dim3(192), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_SKEW)
+    hipLaunchKernelGGL(s3h::sha256_skew_kernel<4>, dim3(P->grid), dim3(320), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_PC)
     hipLaunchKernelGGL(s3h::sha256_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 1 && quad_shadow())
@@ -570,6 +581,13 @@ int s3h_plan_launch_range(s3h_plan_t P, const void* d_base, uint32_t* d_digests,
   if (origin > b0) return fail(S3H_EINVAL, "blk_origin (%llu) > blk_begin (%llu)",
                                (unsigned long long)origin, (unsigned long long)b0);
   return plan_launch(P, d_base, d_digests, b0, b1, origin, static_cast<hipStream_t>(stream), true);
+}
+
+int s3h_plan_set_clock_probe(s3h_plan_t P, uint64_t* d_clocks, uint32_t* waves) {
+  if (!P) return fail(S3H_EINVAL, "null plan");
+  P->d_clocks = d_clocks;
+  if (waves) *waves = P->kernel == S3H_KERNEL_SKEW ? P->grid * uint32_t(P->quad_waves) : 0u;
+  return S3H_OK;
 }
 
 int s3h_plan_info(s3h_plan_t P, uint64_t* n, uint64_t* total_blocks, uint64_t* max_blocks,

@@ -49,6 +49,9 @@ struct LaunchArgs {
   uint64_t blk_begin, blk_end, blk_origin;
   uint32_t n;
   uint32_t flags;
+  // Clock probe (s3h_plan_set_clock_probe; skew kernel): per consumer wave, shader-clock and
+  // 100 MHz real-time counters at the start and end of its chain loop.  Null: off.
+  uint64_t* clocks;
 };
 
 // Compressions the launch sequence runs for a slot of `len` bytes.
@@ -757,7 +760,7 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_skew_kernel(LaunchArgs A
     f3 = ahalf ? EP2 : EP0;                            \
   } while (0)
 
-  const uint32_t it32 = uint32_t(iters);  // < 2^31: the host splits longer launches
+  const uint32_t it32 = uint32_t(iters);  // < 2^31: capi.hip runs longer ranges on the quad kernel
   // first block after which a chain can have ended (>= 1: block 0 ends none)
   const uint32_t cap_from = __builtin_amdgcn_readfirstlane(
       uint32_t(live_end > b0 + 1 ? live_end - b0 : 1));
@@ -765,23 +768,38 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_skew_kernel(LaunchArgs A
 
   uint32_t wa[64], wb[64];
   __syncthreads();
+  uint64_t clk0 = 0, rt0 = 0;
+  if (A.clocks) {
+    clk0 = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
   load(wa, lbase);
   x0 = ahalf ? 0u : H[3] + H[7] + wa[0];
   // One block: rounds 0-15, then (after the step barrier when the next block lives in the
-  // other LDS buffer, or this is the last block) the next block's 16 rows are read while
-  // rounds 16-63 run; NEXT consumes the next block's first word.  The a-quad lanes read the
-  // ones column, so their NEXT word is 1 even past the last block.
-#define S3H_SKEW_BLOCK(P, CUR, NXT)                                                             \
+  // other LDS buffer) the next block's 16 rows are read while rounds 16-63 run; NEXT
+  // consumes the next block's first word.  The a-quad lanes read the ones column, so their
+  // NEXT word is 1 even past the last block.
+  //
+  // Fast steps -- none of whose blocks can end the launch or a chain -- run fully unrolled
+  // with no per-block test; the remaining blocks (the ragged tail and the launch's last
+  // block) run one at a time with the step barrier, capture and exit checks.
+#define S3H_SKEW_FAST(P, CUR, NXT)                                                              \
+  asm volatile(S3H_ALIGN8 S3H_SKEW_ROUNDS_A_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));            \
+  if (i == kBps - 1) {                                                                          \
+    __syncthreads();                                                                            \
+    load(NXT, nbuf);                                                                            \
+  } else {                                                                                      \
+    load(NXT, buf + (i + 1) * kBlkStride);                                                      \
+  }                                                                                             \
+  asm volatile(S3H_ALIGN8 S3H_SKEW_ROUNDS_B_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));            \
+  asm volatile(S3H_ALIGN8 S3H_SKEW_NEXT_##P                                                     \
+               : S3H_SKEW_STATE : [w0] "v"(NXT[0]), [am] "v"(am), [mk] "v"(mk));
+#define S3H_SKEW_SLOW(P, CUR, NXT)                                                              \
   {                                                                                             \
-    const uint32_t bb = j * kBps + i;                                                           \
     asm volatile(S3H_ALIGN8 S3H_SKEW_ROUNDS_A_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));          \
-    if (i == kBps - 1) {                                                                        \
-      __syncthreads();                                                                          \
-      load(NXT, nbuf);                                                                          \
-    } else {                                                                                    \
-      if (bb + 1 >= it32) __syncthreads();                                                      \
-      load(NXT, buf + (i + 1) * kBlkStride);                                                    \
-    }                                                                                           \
+    const uint32_t nx = bb + 1;                                                                 \
+    if (nx % kBps == 0 || nx >= it32) __syncthreads();                                          \
+    load(NXT, lbase + ((nx / kBps) & 1) * kBufStride + (nx % kBps) * kBlkStride);               \
     asm volatile(S3H_ALIGN8 S3H_SKEW_ROUNDS_B_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));          \
     if (bb >= cap_from) {                                                                       \
       asm volatile("; ragged tail: capture check");  /* keeps this branch scalar */           \
@@ -792,22 +810,30 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_skew_kernel(LaunchArgs A
     }                                                                                           \
     asm volatile(S3H_ALIGN8 S3H_SKEW_NEXT_##P                                                   \
                  : S3H_SKEW_STATE : [w0] "v"(NXT[0]), [am] "v"(am), [mk] "v"(mk));              \
-    if (bb + 1 >= it32) goto drain;                                                             \
+    if (nx >= it32) goto drain;                                                                 \
   }
-  for (uint32_t j = 0;; ++j) {
+  const uint32_t fast_end = cap_from < it32 ? cap_from : it32 - 1;  // blocks < it: no checks
+  const uint32_t nfast = fast_end / kBps;                            // whole fast steps
+  for (uint32_t j = 0; j < nfast; ++j) {
     const uint4* buf = lbase + (j & 1) * kBufStride;
     const uint4* nbuf = lbase + ((j + 1) & 1) * kBufStride;
 #pragma unroll
     for (uint32_t h = 0; h < kBps / 2; ++h) {
       {
         const uint32_t i = 2 * h;
-        S3H_SKEW_BLOCK(0, wa, wb)
+        S3H_SKEW_FAST(0, wa, wb)
       }
       {
         const uint32_t i = 2 * h + 1;
-        S3H_SKEW_BLOCK(1, wb, wa)
+        S3H_SKEW_FAST(1, wb, wa)
       }
     }
+  }
+  for (uint32_t bb = nfast * kBps;; bb += 2) {  // starts at an even block: parity 0
+    S3H_SKEW_SLOW(0, wa, wb)
+    ++bb;
+    S3H_SKEW_SLOW(1, wb, wa)
+    --bb;
   }
 drain:
   // The a-quad's last two rounds of the last block (parity (iters-1)&1) run as rounds 0-1
@@ -825,8 +851,16 @@ drain:
       if (nb_rel >= it32) S3H_SKEW_CAPTURE(e13, e12, e11, e10, g01, g00);
     }
   }
-#undef S3H_SKEW_BLOCK
+#undef S3H_SKEW_FAST
+#undef S3H_SKEW_SLOW
 #undef S3H_SKEW_CAPTURE
+  if (A.clocks) {
+    const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+      uint64_t* c = A.clocks + 4ull * (blockIdx.x * NC + wave);
+      c[0] = clk0; c[1] = clk1; c[2] = rt0; c[3] = rt1;
+    }
+  }
   if (valid && nb > b0 && k4 == 0) {
     const uint32_t w0 = ahalf ? 0u : 4u;
     if (emits(A, nb)) {

@@ -77,6 +77,19 @@ class Plan:
         return {"n": n.value, "total_blocks": tb.value, "max_blocks": mb.value,
                 "kernel": _native.KERNEL_NAMES[k.value], "grid": g.value}
 
+    def set_clock_probe(self, clocks=None) -> int:
+        """Record per-consumer-wave clock counters on later launches (skew kernel only):
+        ``clocks`` is a device int64 tensor of >= 4 x waves entries ({clk0, clk1, rt0, rt1}
+        per wave, s_memtime / s_memrealtime); None switches the probe off.  Returns the
+        number of consumer waves that record (0 if the plan's kernel does not)."""
+        w = ctypes.c_uint32()
+        ptr = ctypes.c_void_p(clocks.data_ptr() if clocks is not None else None)
+        check(lib().s3h_plan_set_clock_probe(self._h, ptr, ctypes.byref(w)))
+        if clocks is not None and clocks.numel() < 4 * w.value:
+            lib().s3h_plan_set_clock_probe(self._h, None, None)
+            raise ValueError(f"clock buffer needs {4 * w.value} int64 entries")
+        return w.value
+
     def _check_buffers(self, data, digests):
         import torch
         if not (data.is_cuda and digests.is_cuda):
