@@ -35,7 +35,7 @@ ISSUE_FLOOR_CPI = 4.0           # one wave: <= 1 instruction per 4 cycles (MI355
 # `make isa` + llvm-objdump; skew = 523 VALU + 16 ds_read_b128 + 2 s_waitcnt + ~2 alignment
 # s_nop + loop control; pair = 640 round VALU + bookkeeping + 16 ds_read_b128).  A wave issues
 # at most one instruction per ~4 cycles: this, not HBM, bounds each part's chain.
-CHAIN_INSTR_PER_BLOCK = {"skew": 544, "quad": 592, "pair": 672, "pc": 923, "lane": 1425, "md5-pc": 280}
+CHAIN_INSTR_PER_BLOCK = {"skew": 544, "skewp": 608, "quad": 592, "pair": 672, "pc": 923, "lane": 1425, "md5-pc": 280}
 
 
 def parse():
@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4"])
     ap.add_argument("--parts-per-gpu", type=int, default=0, help="override batch size")
     ap.add_argument("--part-bytes", type=int, default=0, help="override part size (sweeps)")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "skew", "quad", "pair", "pc", "lane"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "skew", "skewp", "quad", "pair", "pc", "lane"])
     ap.add_argument("--algo", default="sha256", choices=["sha256", "md5"],
                     help="md5: the SURVEY 8(f) Content-MD5/ETag kernel (not the metric)")
     ap.add_argument("--cpu-sample-parts", type=int, default=384)
@@ -212,7 +212,7 @@ def main():
     # records s_memtime / s_memrealtime around its chain loop -> live shader clock and cycles
     # per block (skew kernel only).
     probe = None
-    if kname == "skew":
+    if kname in ("skew", "skewp"):
         clocks = torch.zeros(4 * 4 * info["grid"], dtype=torch.int64, device=dev)
         waves = plan.set_clock_probe(clocks)
         plan.launch(data, digests, stream)

@@ -45,7 +45,8 @@ enum s3h_kernel {
   S3H_KERNEL_PC = 2,   /* producer/consumer: producer wave stages W+K through LDS */
   S3H_KERNEL_PAIR = 3, /* producer/consumer with each chain split over a lane pair (DPP) */
   S3H_KERNEL_QUAD = 4, /* as PAIR, each half-state on a lane quad: 9 instead of 10 VALU/round */
-  S3H_KERNEL_SKEW = 5  /* lane quads with the a-quad two rounds behind: 8 VALU/round */
+  S3H_KERNEL_SKEW = 5, /* lane quads with the a-quad two rounds behind: 8 VALU/round */
+  S3H_KERNEL_SKEWP = 6 /* the same skewed schedule on lane pairs: 9 VALU/round, 32 chains/wave */
 };
 
 enum s3h_algo {

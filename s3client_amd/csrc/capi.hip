@@ -81,14 +81,15 @@ struct s3h_plan_s {
 
 namespace {
 
-// Kernel choice by part count (profiles/r01_sweep_parts_256KiB.jsonl,
-// profiles/r01_sweep_quad_waves.jsonl): while every consumer wave can own a SIMD, per-chain
-// latency rules and the lane-quad kernel (9 VALU/round, 8 chains per wave) wins -- one
-// consumer wave per workgroup up to 2,048 parts, two up to 4,096 (256 workgroups = one per
-// CU); then the lane-pair kernel (10 VALU/round, 32 chains per wave) until consumer+producer
-// waves fill every SIMD and total instruction count rules: producer/consumer up to 64K parts,
-// then the fused one-lane-per-part kernel.
-constexpr uint64_t kQuadMaxParts = 4096;
+// Kernel choice by part count (profiles/r01_sweep_skew*.jsonl, r01_sweep_parts_256KiB.jsonl):
+// while every consumer wave can own a SIMD, per-chain latency rules and the skewed lane-octet
+// kernel (8 VALU/round, 8 chains per wave) wins -- one consumer wave per workgroup up to 2,048
+// parts, two up to 4,096 (256 workgroups = one per CU); then the skewed lane-pair kernel
+// (9 VALU/round, 32 chains per wave: 1.17x the pair kernel at 8K parts, 1.97x at 16K), then
+// the pair kernel until consumer+producer waves fill every SIMD and total instruction count
+// rules: producer/consumer up to 64K parts, then the fused one-lane-per-part kernel.
+constexpr uint64_t kQuadMaxParts = 4096;   // skew (lane octets), 1-2 consumer waves per WG
+constexpr uint64_t kSkewpMaxParts = 24576; // skewp (lane pairs, 32 chains per consumer wave)
 constexpr uint64_t kPairMaxParts = 32768;
 constexpr uint64_t kPcMaxParts = 65536;
 constexpr uint64_t kMaxParts = 1ull << 31;
@@ -166,12 +167,13 @@ int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* le
     kernel = S3H_KERNEL_PC;
   }
   if (kernel == S3H_KERNEL_AUTO)
-    kernel = n <= kQuadMaxParts ? S3H_KERNEL_SKEW
-             : n <= kPairMaxParts ? S3H_KERNEL_PAIR
+    kernel = n <= kQuadMaxParts    ? S3H_KERNEL_SKEW
+             : n <= kSkewpMaxParts ? S3H_KERNEL_SKEWP
+             : n <= kPairMaxParts  ? S3H_KERNEL_PAIR
              : n <= kPcMaxParts   ? S3H_KERNEL_PC
                                   : S3H_KERNEL_LANE;
   if (kernel != S3H_KERNEL_PC && kernel != S3H_KERNEL_LANE && kernel != S3H_KERNEL_PAIR &&
-      kernel != S3H_KERNEL_QUAD && kernel != S3H_KERNEL_SKEW)
+      kernel != S3H_KERNEL_QUAD && kernel != S3H_KERNEL_SKEW && kernel != S3H_KERNEL_SKEWP)
     return fail(S3H_EINVAL, "plan: unknown kernel %d", kernel);
 
   std::vector<uint32_t> order(n);
@@ -188,7 +190,8 @@ int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* le
   // skew: 1, 2 or 4 consumer waves (3 runs as 4)
   P->quad_waves = kernel == S3H_KERNEL_SKEW && quad_waves(n) == 3 ? 4 : quad_waves(n);
   P->grid = kernel == S3H_KERNEL_PC     ? uint32_t((n + 63) / 64)
-            : kernel == S3H_KERNEL_PAIR ? uint32_t((n + s3h::kPairParts - 1) / s3h::kPairParts)
+            : kernel == S3H_KERNEL_PAIR || kernel == S3H_KERNEL_SKEWP
+                ? uint32_t((n + s3h::kPairParts - 1) / s3h::kPairParts)
             : kernel == S3H_KERNEL_QUAD || kernel == S3H_KERNEL_SKEW
                 ? uint32_t((n + 8 * P->quad_waves - 1) / (8 * P->quad_waves))
                                         : uint32_t((n + 255) / 256);
@@ -237,6 +240,10 @@ int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t
     hipLaunchKernelGGL(s3h::sha256_quad_kernel<1>, dim3(P->grid), dim3(128), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_SKEW && b1 - b0 >= (1ull << 31))
     hipLaunchKernelGGL(s3h::sha256_quad_kernel<2>, dim3(P->grid), dim3(192), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_SKEWP && b1 - b0 >= (1ull << 31))
+    hipLaunchKernelGGL(s3h::sha256_pair_kernel, dim3(P->grid), dim3(s3h::kPairThreads), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_SKEWP)
+    hipLaunchKernelGGL((s3h::sha256_skew_kernel<1, true>), dim3(P->grid), dim3(128), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_SKEW && P->quad_waves == 1)
     hipLaunchKernelGGL(s3h::sha256_skew_kernel<1>, dim3(P->grid), dim3(128), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_SKEW && P->quad_waves == 2)
@@ -586,7 +593,10 @@ int s3h_plan_launch_range(s3h_plan_t P, const void* d_base, uint32_t* d_digests,
 int s3h_plan_set_clock_probe(s3h_plan_t P, uint64_t* d_clocks, uint32_t* waves) {
   if (!P) return fail(S3H_EINVAL, "null plan");
   P->d_clocks = d_clocks;
-  if (waves) *waves = P->kernel == S3H_KERNEL_SKEW ? P->grid * uint32_t(P->quad_waves) : 0u;
+  if (waves)
+    *waves = P->kernel == S3H_KERNEL_SKEW    ? P->grid * uint32_t(P->quad_waves)
+             : P->kernel == S3H_KERNEL_SKEWP ? P->grid
+                                             : 0u;
   return S3H_OK;
 }
 

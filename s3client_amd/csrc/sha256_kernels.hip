@@ -638,7 +638,7 @@ __global__ __launch_bounds__(64 * (NC * (1 + SH) + 1)) void sha256_quad_kernel(L
       [e0_1] "+v"(e01), [e0_2] "+v"(e02), [e0_3] "+v"(e03), [e1_0] "+v"(e10), [e1_1] "+v"(e11), \
       [e1_2] "+v"(e12), [e1_3] "+v"(e13), [n0] "+v"(n0), [n1] "+v"(n1), [n2] "+v"(n2),          \
       [n3] "+v"(n3), [x0] "+v"(x0), [x1] "+v"(x1), [q1] "=&v"(q1), [q3] "=&v"(q3),               \
-      [sl] "=&v"(sl), [cm] "=&v"(cm), [t] "=&v"(tt)
+      [sl] "=&v"(sl), [cm] "=&v"(cm), [t] "=&v"(tt), [q2] "=&v"(q2)
 #define S3H_SKEW_W(W)                                                                           \
   [w1] "v"(W[1]), [w2] "v"(W[2]), [w3] "v"(W[3]), [w4] "v"(W[4]), [w5] "v"(W[5]), [w6] "v"(W[6]), \
       [w7] "v"(W[7]), [w8] "v"(W[8]), [w9] "v"(W[9]), [w10] "v"(W[10]), [w11] "v"(W[11]),         \
@@ -652,14 +652,21 @@ __global__ __launch_bounds__(64 * (NC * (1 + SH) + 1)) void sha256_quad_kernel(L
       [w47] "v"(W[47]), [w48] "v"(W[48]), [w49] "v"(W[49]), [w50] "v"(W[50]), [w51] "v"(W[51]),   \
       [w52] "v"(W[52]), [w53] "v"(W[53]), [w54] "v"(W[54]), [w55] "v"(W[55]), [w56] "v"(W[56]),   \
       [w57] "v"(W[57]), [w58] "v"(W[58]), [w59] "v"(W[59]), [w60] "v"(W[60]), [w61] "v"(W[61]),   \
-      [w62] "v"(W[62]), [w63] "v"(W[63]), [am] "v"(am), [mk] "v"(mk)
+      [w62] "v"(W[62]), [w63] "v"(W[63]), [am] "v"(am), [mk] "v"(mk), [am2] "v"(am2), [am3] "v"(am3)
 
-template <int NC>
+// PAIR: the lane-pair layout of the same schedule (S3H_SKEWP_*, 9 VALU per round): a chain on
+// e-lane k and a-lane 7-k of a half-row, 32 chains per consumer wave.
+template <int NC, bool PAIR = false>
 __global__ __launch_bounds__(64 * (NC + 1)) void sha256_skew_kernel(LaunchArgs A) {
-  constexpr uint32_t kParts = kQuadChainsPerWave * NC;
-  constexpr uint32_t kBps = 64 / kParts >= 2 ? 64 / kParts : 2;  // blocks per producer step
+  constexpr uint32_t kCpw = PAIR ? 32 : kQuadChainsPerWave;  // chains per consumer wave
+  constexpr uint32_t kParts = kCpw * NC;
+  // Blocks per producer step: 8 when the producer's lanes make at most two (part, block)
+  // items per step (one step of prefetch = ~8 blocks of chain time, one barrier per 8
+  // blocks); fewer for wider workgroups, whose producer would spill.
+  constexpr uint32_t kBps = PAIR ? 4 : NC >= 4 ? 2 : 8;
   constexpr uint32_t kLanes = kParts * kBps;
-  constexpr uint32_t kCols = kParts + 1;  // column kParts holds ones (read by the a-quads)
+  constexpr uint32_t kItems = kLanes / 64;  // == NC
+  constexpr uint32_t kCols = kParts + 1;    // column kParts holds ones (read by the a-quads)
   __shared__ uint4 lds_wk[2][kBps][16][kCols];
 
   const uint32_t lane = threadIdx.x & 63u;
@@ -673,35 +680,58 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_skew_kernel(LaunchArgs A
   const uint64_t steps = (iters + kBps - 1) / kBps;
 
   if (wave == NC) {
-    // ---------------------------------------------------------------- producer (as quad)
+    // ---------------------------------------------------------------- producer
     for (uint32_t i = lane; i < 2 * kBps * 16; i += 64)
       lds_wk[i / (kBps * 16)][(i / 16) % kBps][i % 16][kParts] = make_uint4(1u, 1u, 1u, 1u);
-    const uint32_t pl = lane % kLanes;
-    const uint32_t part = pl / kBps, h = pl % kBps;
-    const uint32_t slot = slot0 + part;
-    Slot s = {0, 0};
-    if (slot < A.n) s = A.slots[slot];
-    const uint8_t* p = A.base + s.off + 64ull * (b0 + h - A.blk_origin);
-    const uint32_t sel = be_selector(uint32_t(reinterpret_cast<uintptr_t>(A.base + s.off) & 3));
-    const uint64_t fend = fetch_end(s.len, A.blk_end);
-    const uint64_t bh = b0 + h;
-    const uint64_t bits = slot < A.n ? msg_bits(A, slot, s.len) : 0;
+    // Item r of this lane = (part, block h of the step); consecutive lanes take consecutive
+    // blocks of one part (coalesced 512-byte runs).
+    const uint8_t* p[kItems];
+    uint32_t sel[kItems], part[kItems], h[kItems];
+    uint64_t len[kItems], fend[kItems], bh[kItems], bits[kItems];
+#pragma unroll
+    for (uint32_t r = 0; r < kItems; ++r) {
+      const uint32_t it = lane + 64u * r;
+      part[r] = it / kBps;
+      h[r] = it % kBps;
+      const uint32_t slot = slot0 + part[r];
+      Slot s = {0, 0};
+      if (slot < A.n) s = A.slots[slot];
+      p[r] = A.base + s.off + 64ull * (b0 + h[r] - A.blk_origin);
+      sel[r] = be_selector(uint32_t(reinterpret_cast<uintptr_t>(A.base + s.off) & 3));
+      len[r] = s.len;
+      fend[r] = fetch_end(s.len, A.blk_end);
+      bh[r] = b0 + h[r];
+      bits[r] = slot < A.n ? msg_bits(A, slot, s.len) : 0;
+    }
     constexpr uint64_t kStride = 64ull * kBps;
-    RawBlock ra, rb;
-    fetch_full(p, bh < fend, A.zero, ra);
-    fetch_full(p + kStride, bh + kBps < fend, A.zero, rb);
-    produce_block(ra, sel, p, s.len, bits, bh, A.blk_end, lds_wk[0][h], part);
+    RawBlock ra[kItems], rb[kItems];
+#pragma unroll
+    for (uint32_t r = 0; r < kItems; ++r) {
+      fetch_full(p[r], bh[r] < fend[r], A.zero, ra[r]);
+      fetch_full(p[r] + kStride, bh[r] + kBps < fend[r], A.zero, rb[r]);
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kItems; ++r)
+      produce_block(ra[r], sel[r], p[r], len[r], bits[r], bh[r], A.blk_end, lds_wk[0][h[r]], part[r]);
     __syncthreads();
     for (uint64_t k = 1; k <= steps; k += 2) {
       if (k < steps) {
-        fetch_full(p + kStride * (k + 1), bh + kBps * (k + 1) < fend, A.zero, ra);
-        produce_block(rb, sel, p + kStride * k, s.len, bits, bh + kBps * k, A.blk_end, lds_wk[1][h], part);
+#pragma unroll
+        for (uint32_t r = 0; r < kItems; ++r) {
+          fetch_full(p[r] + kStride * (k + 1), bh[r] + kBps * (k + 1) < fend[r], A.zero, ra[r]);
+          produce_block(rb[r], sel[r], p[r] + kStride * k, len[r], bits[r], bh[r] + kBps * k,
+                        A.blk_end, lds_wk[1][h[r]], part[r]);
+        }
       }
       __syncthreads();
       if (k + 1 > steps) break;
       if (k + 1 < steps) {
-        fetch_full(p + kStride * (k + 2), bh + kBps * (k + 2) < fend, A.zero, rb);
-        produce_block(ra, sel, p + kStride * (k + 1), s.len, bits, bh + kBps * (k + 1), A.blk_end, lds_wk[0][h], part);
+#pragma unroll
+        for (uint32_t r = 0; r < kItems; ++r) {
+          fetch_full(p[r] + kStride * (k + 2), bh[r] + kBps * (k + 2) < fend[r], A.zero, rb[r]);
+          produce_block(ra[r], sel[r], p[r] + kStride * (k + 1), len[r], bits[r],
+                        bh[r] + kBps * (k + 1), A.blk_end, lds_wk[0][h[r]], part[r]);
+        }
       }
       __syncthreads();
     }
@@ -709,16 +739,22 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_skew_kernel(LaunchArgs A
   }
   // ------------------------------------------------------------------ consumer
   if (!(A.flags & kPrioNone)) __builtin_amdgcn_s_setprio(3);
-  const uint32_t part = kQuadChainsPerWave * wave + (lane >> 3);
   const bool ahalf = (lane >> 2) & 1u;
   const uint32_t k4 = lane & 3u;
+  // quad: lanes 8c..8c+7 = chain c; pair: half-row h holds chains 4h..4h+3 (e-lane k, a-lane 7-k)
+  const uint32_t part = kCpw * wave + (PAIR ? 4 * (lane >> 3) + (ahalf ? 3 - k4 : k4) : lane >> 3);
   const uint32_t slot = slot0 + part;
   const bool valid = slot < A.n;
   const uint64_t nb = valid ? slot_blocks(A, A.slots[slot].len) : 0;
   const uint32_t last_slot = (slot0 + kParts <= A.n ? slot0 + kParts : A.n) - 1;
   const uint64_t live_end = slot_blocks(A, A.slots[last_slot].len);  // every chain live below
   // Rotation per lane: positions 0..2 of a quad take the three Sigma amounts, 3 repeats 0.
-  const uint32_t am = ahalf ? (k4 == 1 ? 22u : k4 == 2 ? 13u : 2u) : (k4 == 1 ? 11u : k4 == 2 ? 25u : 6u);
+  // quad: one rotation per lane (positions 0..2 of a quad take the three Sigma amounts, 3
+  // repeats 0); pair: all three in every lane
+  const uint32_t am = PAIR ? (ahalf ? 2u : 6u)
+                           : ahalf ? (k4 == 1 ? 22u : k4 == 2 ? 13u : 2u)
+                                   : (k4 == 1 ? 11u : k4 == 2 ? 25u : 6u);
+  const uint32_t am2 = ahalf ? 13u : 11u, am3 = ahalf ? 22u : 25u;
   const uint32_t mk = ahalf ? 0xffffffffu : 0u;
   const uint32_t one_a = ahalf ? 1u : 0u;
   uint32_t H[8];
@@ -736,7 +772,7 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_skew_kernel(LaunchArgs A
   uint32_t e03 = ahalf ? H[2] : H[4], e02 = ahalf ? H[3] : 0u, e01 = 0, e00 = 0;
   uint32_t g11 = ahalf ? H[0] : 0u, g10 = ahalf ? H[1] : 0u, g01 = 0, g00 = 0;
   uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0, x0, x1 = 0;
-  uint32_t q1, q3, sl, cm, tt;
+  uint32_t q1, q2, q3, sl, cm, tt;
   // Per-lane LDS base (buffer 0, block 0, row 0, own column): block and buffer offsets are
   // immediates of the 16 ds_read_b128 that fetch one block's W+K.
   const uint4* lbase = &lds_wk[0][0][0][ahalf ? kParts : part];
@@ -783,24 +819,24 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_skew_kernel(LaunchArgs A
   // Fast steps -- none of whose blocks can end the launch or a chain -- run fully unrolled
   // with no per-block test; the remaining blocks (the ragged tail and the launch's last
   // block) run one at a time with the step barrier, capture and exit checks.
-#define S3H_SKEW_FAST(P, CUR, NXT)                                                              \
-  asm volatile(S3H_ALIGN8 S3H_SKEW_ROUNDS_A_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));            \
+#define S3H_SKEW_FAST(L, P, CUR, NXT)                                                           \
+  asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_A_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));           \
   if (i == kBps - 1) {                                                                          \
     __syncthreads();                                                                            \
     load(NXT, nbuf);                                                                            \
   } else {                                                                                      \
     load(NXT, buf + (i + 1) * kBlkStride);                                                      \
   }                                                                                             \
-  asm volatile(S3H_ALIGN8 S3H_SKEW_ROUNDS_B_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));            \
-  asm volatile(S3H_ALIGN8 S3H_SKEW_NEXT_##P                                                     \
+  asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_B_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));           \
+  asm volatile(S3H_ALIGN8 S3H_##L##_NEXT_##P                                                    \
                : S3H_SKEW_STATE : [w0] "v"(NXT[0]), [am] "v"(am), [mk] "v"(mk));
-#define S3H_SKEW_SLOW(P, CUR, NXT)                                                              \
+#define S3H_SKEW_SLOW(L, P, CUR, NXT)                                                           \
   {                                                                                             \
-    asm volatile(S3H_ALIGN8 S3H_SKEW_ROUNDS_A_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));          \
+    asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_A_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));         \
     const uint32_t nx = bb + 1;                                                                 \
     if (nx % kBps == 0 || nx >= it32) __syncthreads();                                          \
     load(NXT, lbase + ((nx / kBps) & 1) * kBufStride + (nx % kBps) * kBlkStride);               \
-    asm volatile(S3H_ALIGN8 S3H_SKEW_ROUNDS_B_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));          \
+    asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_B_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));         \
     if (bb >= cap_from) {                                                                       \
       asm volatile("; ragged tail: capture check");  /* keeps this branch scalar */           \
       if (nb_rel == bb) {                                                                       \
@@ -808,32 +844,37 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_skew_kernel(LaunchArgs A
         else S3H_SKEW_CAPTURE(e03, e02, e01, e00, g11, g10);                                    \
       }                                                                                         \
     }                                                                                           \
-    asm volatile(S3H_ALIGN8 S3H_SKEW_NEXT_##P                                                   \
+    asm volatile(S3H_ALIGN8 S3H_##L##_NEXT_##P                                                  \
                  : S3H_SKEW_STATE : [w0] "v"(NXT[0]), [am] "v"(am), [mk] "v"(mk));              \
     if (nx >= it32) goto drain;                                                                 \
   }
   const uint32_t fast_end = cap_from < it32 ? cap_from : it32 - 1;  // blocks < it: no checks
   const uint32_t nfast = fast_end / kBps;                            // whole fast steps
-  for (uint32_t j = 0; j < nfast; ++j) {
-    const uint4* buf = lbase + (j & 1) * kBufStride;
-    const uint4* nbuf = lbase + ((j + 1) & 1) * kBufStride;
-#pragma unroll
-    for (uint32_t h = 0; h < kBps / 2; ++h) {
-      {
-        const uint32_t i = 2 * h;
-        S3H_SKEW_FAST(0, wa, wb)
-      }
-      {
-        const uint32_t i = 2 * h + 1;
-        S3H_SKEW_FAST(1, wb, wa)
-      }
-    }
+#define S3H_SKEW_LOOPS(L)                                                                       \
+  for (uint32_t j = 0; j < nfast; ++j) {                                                        \
+    const uint4* buf = lbase + (j & 1) * kBufStride;                                            \
+    const uint4* nbuf = lbase + ((j + 1) & 1) * kBufStride;                                     \
+    _Pragma("unroll") for (uint32_t h = 0; h < kBps / 2; ++h) {                                 \
+      {                                                                                         \
+        const uint32_t i = 2 * h;                                                               \
+        S3H_SKEW_FAST(L, 0, wa, wb)                                                             \
+      }                                                                                         \
+      {                                                                                         \
+        const uint32_t i = 2 * h + 1;                                                           \
+        S3H_SKEW_FAST(L, 1, wb, wa)                                                             \
+      }                                                                                         \
+    }                                                                                           \
+  }                                                                                             \
+  for (uint32_t bb = nfast * kBps;; bb += 2) { /* starts at an even block: parity 0 */          \
+    S3H_SKEW_SLOW(L, 0, wa, wb)                                                                 \
+    ++bb;                                                                                       \
+    S3H_SKEW_SLOW(L, 1, wb, wa)                                                                 \
+    --bb;                                                                                       \
   }
-  for (uint32_t bb = nfast * kBps;; bb += 2) {  // starts at an even block: parity 0
-    S3H_SKEW_SLOW(0, wa, wb)
-    ++bb;
-    S3H_SKEW_SLOW(1, wb, wa)
-    --bb;
+  if constexpr (PAIR) {
+    S3H_SKEW_LOOPS(SKEWP)
+  } else {
+    S3H_SKEW_LOOPS(SKEW)
   }
 drain:
   // The a-quad's last two rounds of the last block (parity (iters-1)&1) run as rounds 0-1
@@ -844,15 +885,22 @@ drain:
 #pragma unroll
     for (int i = 0; i < 64; ++i) wd[i] = one_a;
     if (it32 & 1) {
-      asm volatile(S3H_ALIGN8 S3H_SKEW_DRAIN_1 : S3H_SKEW_STATE : S3H_SKEW_W(wd));
+      if constexpr (PAIR)
+        asm volatile(S3H_ALIGN8 S3H_SKEWP_DRAIN_1 : S3H_SKEW_STATE : S3H_SKEW_W(wd));
+      else
+        asm volatile(S3H_ALIGN8 S3H_SKEW_DRAIN_1 : S3H_SKEW_STATE : S3H_SKEW_W(wd));
       if (nb_rel >= it32) S3H_SKEW_CAPTURE(e03, e02, e01, e00, g11, g10);
     } else {
-      asm volatile(S3H_ALIGN8 S3H_SKEW_DRAIN_0 : S3H_SKEW_STATE : S3H_SKEW_W(wd));
+      if constexpr (PAIR)
+        asm volatile(S3H_ALIGN8 S3H_SKEWP_DRAIN_0 : S3H_SKEW_STATE : S3H_SKEW_W(wd));
+      else
+        asm volatile(S3H_ALIGN8 S3H_SKEW_DRAIN_0 : S3H_SKEW_STATE : S3H_SKEW_W(wd));
       if (nb_rel >= it32) S3H_SKEW_CAPTURE(e13, e12, e11, e10, g01, g00);
     }
   }
 #undef S3H_SKEW_FAST
 #undef S3H_SKEW_SLOW
+#undef S3H_SKEW_LOOPS
 #undef S3H_SKEW_CAPTURE
   if (A.clocks) {
     const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
@@ -861,7 +909,7 @@ drain:
       c[0] = clk0; c[1] = clk1; c[2] = rt0; c[3] = rt1;
     }
   }
-  if (valid && nb > b0 && k4 == 0) {
+  if (valid && nb > b0 && (PAIR || k4 == 0)) {  // quad: one lane per quad writes its half
     const uint32_t w0 = ahalf ? 0u : 4u;
     if (emits(A, nb)) {
       uint4* o = reinterpret_cast<uint4*>(A.digests + 8ull * A.out_idx[slot] + w0);

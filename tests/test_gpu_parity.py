@@ -2,6 +2,8 @@
 
 Bar: bit-exact digests (integer work).  Sizes are chosen so the CPU oracle finishes in
 seconds; the full C2 batch (1024 x 8 MiB) is checked part-by-part against the oracle too."""
+import os
+
 import numpy as np
 import pytest
 
@@ -9,7 +11,7 @@ import s3client_amd as s3
 
 pytestmark = pytest.mark.gpu
 SEED = 20241008
-KERNELS = ["skew", "quad", "pair", "pc", "lane"]
+KERNELS = ["skew", "skewp", "quad", "pair", "pc", "lane"]
 
 
 def _dev_buffer(torch, host: np.ndarray):
@@ -66,7 +68,8 @@ def test_kernels_agree_on_many_small_parts(torch_cuda, oracle):
     assert s3.Plan([0] * 70000, [1] * 70000).info()["kernel"] == "lane"
     assert s3.Plan([0] * 40000, [1] * 40000).info()["kernel"] == "pc"
     assert s3.Plan([0] * 1024, [1] * 1024).info()["kernel"] == "skew"
-    assert s3.Plan([0] * 10000, [1] * 10000).info()["kernel"] == "pair"
+    assert s3.Plan([0] * 10000, [1] * 10000).info()["kernel"] == "skewp"
+    assert s3.Plan([0] * 30000, [1] * 30000).info()["kernel"] == "pair"
     rng = np.random.default_rng(7)
     n = 70000
     lens = rng.integers(0, 200, n)
@@ -74,7 +77,7 @@ def test_kernels_agree_on_many_small_parts(torch_cuda, oracle):
     host = rng.integers(0, 256, (1 << 20) + 256, dtype=np.uint8)
     data = _dev_buffer(torch_cuda, host)
     a = s3.sha256_batch_device(data, offs, lens, kernel="auto").cpu().numpy().view(np.uint32)
-    for k in ("pc", "pair", "quad", "skew"):
+    for k in ("pc", "pair", "quad", "skew", "skewp"):
         b = s3.sha256_batch_device(data, offs, lens, kernel=k).cpu().numpy().view(np.uint32)
         assert np.array_equal(a, b), k
     idx = rng.choice(n, 500, replace=False)
@@ -111,7 +114,7 @@ def test_c2_full_batch_bit_exact(torch_cuda, oracle, golden, kernel):
     txt = s3.digests_to_text(out)
     for e in golden["c2_parts"]:
         assert txt[e["p"]] == e["digest"], e["p"]
-    if kernel in ("skew", "quad", "pair"):
+    if kernel in ("skew", "skewp", "quad", "pair"):
         host = data.cpu().numpy()
         want = oracle.batch(host, offs, lens, threads=16)
         assert np.array_equal(out, want)
@@ -277,7 +280,8 @@ def test_quad_two_consumer_waves_ragged(torch_cuda, oracle, kernel):
     rng = np.random.default_rng(31)
     n = 3000
     plan = s3.Plan([0] * n, [1] * n, kernel=kernel)
-    assert plan.info()["grid"] == (n + 15) // 16
+    if "S3H_QUAD_WAVES" not in os.environ:  # sweeps force the consumer-wave count
+        assert plan.info()["grid"] == (n + 15) // 16
     lens = rng.integers(0, 9000, n)
     lens[:4] = [0, 55, 56, 64]
     offs = np.concatenate([[0], np.cumsum(lens + rng.integers(0, 5, n))[:-1]])

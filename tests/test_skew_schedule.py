@@ -24,6 +24,15 @@ def test_schedule_matches_hashlib(n):
     assert got == list(struct.unpack(">8I", hashlib.sha256(msg).digest()))
 
 
+@pytest.mark.parametrize("n", [0, 55, 56, 64, 200, 1000])
+def test_pair_layout_four_chains(n):
+    """Lane-pair layout: four independent chains per half-row (e-lane k, a-lane 7-k)."""
+    rng = random.Random(100 + n)
+    msgs = [bytes(rng.randrange(256) for _ in range(n)) for _ in range(4)]
+    got = gen_skew.simulate_chains([gen_skew.IV] * 4, [gen_skew.pad_words(m) for m in msgs], "pair")
+    assert got == [list(struct.unpack(">8I", hashlib.sha256(m).digest())) for m in msgs]
+
+
 def test_schedule_from_arbitrary_state():
     """Resumed launches start from a loaded chaining state, not the IV."""
     rng = random.Random(5)
@@ -34,14 +43,16 @@ def test_schedule_from_arbitrary_state():
 
 
 def test_instruction_counts():
-    # 8 VALU per round; feed-forward (8) and boundary corrections (3) per block
+    # 8 (quad) / 9 (pair) VALU per round; feed-forward (8) and boundary corrections (3) per block
     assert len(gen_skew.rounds_ops(0)) + len(gen_skew.next_ops(0)) == 64 * 8 + 11
+    assert len(gen_skew.rounds_ops(0, layout="pair")) + len(gen_skew.next_ops(0)) == 64 * 9 + 11
 
 
+@pytest.mark.parametrize("layout", ["quad", "pair"])
 @pytest.mark.parametrize("p", [0, 1])
-def test_no_dpp_hazards(p):
-    assert gen_skew.dpp_hazards(gen_skew.block_stream(p)) == []
-    assert gen_skew.dpp_hazards(gen_skew.rounds_ops(p, 0, 2)) == []
+def test_no_dpp_hazards(p, layout):
+    assert gen_skew.dpp_hazards(gen_skew.block_stream(p, layout)) == []
+    assert gen_skew.dpp_hazards(gen_skew.rounds_ops(p, 0, 2, layout)) == []
 
 
 def test_committed_inc_is_generated(tmp_path):

@@ -78,13 +78,22 @@ def R(r, p):
     return f"e{p}_{r - 60}"
 
 
-def round_ops(r, p, wreg):
+def round_ops(r, p, wreg, layout="quad"):
     """Instructions of round r (0..63) of a block of parity p.  wreg: W+K register of round r+1
-    (None at r = 63: the next block's first word is consumed by next_ops)."""
+    (None at r = 63: the next block's first word is consumed by next_ops).
+
+    layout "quad": a chain on 8 lanes (e-quad + a-quad), Sigma = one per-lane rotation folded
+    by two quad_perm xor_dpp.  layout "pair": a chain on 2 lanes (e-lane k, a-lane 7-k of a
+    half-row: the same row_half_mirror partner), Sigma = three per-lane rotations + xor3, four
+    chains per half-row (9 VALU per round)."""
     q = 1 - p
     s0, s1, s2 = R(r - 1, p), R(r - 2, p), R(r - 3, p)
     xc, xn = f"x{r % 2}", f"x{(r + 1) % 2}"
-    ops = [("align", "q1", s0, "am"), ("sel", "sl", s0, s1, "mk")]
+    pair = layout == "pair"
+    ops = [("align", "q1", s0, "am")]
+    if pair:
+        ops += [("align", "q2", s0, "am2"), ("align", "q3", s0, "am3")]
+    ops.append(("sel", "sl", s0, s1, "mk"))
     if r == 1:
         # a-feed-forward of the previous block's raw a63 (s0 here) once SEL has read it, so that
         # P1 below already hands the e-quad H_b.
@@ -100,12 +109,17 @@ def round_ops(r, p, wreg):
     if r == 1:
         ops.append(("ffa", f"e{q}_3", f"e{p}_3"))   # raw a62 -> H_c (s1: last read by BFI)
         ops.append(("ffa", f"e{q}_2", f"e{p}_2"))   # raw a61 -> H_d (read by P2 below)
-    ops.append(("xor1", "q3", "q1"))
-    if wreg is not None:
-        ops.append(("p1", "t", s0, wreg))
-    ops.append(("xor2", "q3", "q1"))
-    if wreg is not None:
-        ops.append(("p2", xn, s2, "mk", "t"))
+    if pair:
+        ops.append(("xor3", "q3", "q1", "q2", "q3"))
+        if wreg is not None:
+            ops += [("p1", "t", s0, wreg), ("p2", xn, s2, "mk", "t")]
+    else:
+        ops.append(("xor1", "q3", "q1"))
+        if wreg is not None:
+            ops.append(("p1", "t", s0, wreg))
+        ops.append(("xor2", "q3", "q1"))
+        if wreg is not None:
+            ops.append(("p2", xn, s2, "mk", "t"))
     if r == 0:
         # C2: the e-quad's cross term was the previous block's raw a62: add its H_c.
         ops.append(("adde", xn, f"e{p}_3"))
@@ -118,9 +132,9 @@ def round_ops(r, p, wreg):
     return ops
 
 
-def rounds_ops(p, first=0, last=64):
+def rounds_ops(p, first=0, last=64, layout="quad"):
     return [op for r in range(first, last)
-            for op in round_ops(r, p, f"w{r + 1}" if r < 63 else None)]
+            for op in round_ops(r, p, f"w{r + 1}" if r < 63 else None, layout)]
 
 
 def next_ops(p, wreg="w0"):
@@ -155,6 +169,9 @@ def simulate_ops(ops, regs):
         elif op == "bfi":
             _, d, s, a, b = ins
             regs[d] = [(regs[s][i] & regs[a][i] | ~regs[s][i] & regs[b][i]) & M32 for i in range(8)]
+        elif op == "xor3":
+            _, d, a, b, c = ins
+            regs[d] = [regs[a][i] ^ regs[b][i] ^ regs[c][i] for i in range(8)]
         elif op in ("xor1", "xor2"):
             _, d, s = ins
             perm = PERM1 if op == "xor1" else PERM2
@@ -198,53 +215,79 @@ def schedule(block_words):
     return out
 
 
-def init_regs(H, wk0):
-    """Kernel prologue: register contents before block 0 (parity 0), per lane.  H = 8-word
-    state (a..h), wk0 = W[0]+K[0] of block 0."""
-    Ha, Hb, Hc, Hd, He, Hf, Hg, Hh = H
+def lane_chain(i, layout):
+    """Chain index of lane i (0..7) of a half-row: quad = one chain, pair = four (e-lane k and
+    a-lane 7-k)."""
+    if layout == "quad":
+        return 0
+    return i if i < 4 else 7 - i
 
-    def lanes(e, a):
-        return [e] * 4 + [a] * 4
-    regs = {n: lanes(0, 0) for n in
-            ["g0_0", "g0_1", "g1_0", "g1_1", "n0", "n1", "n2", "n3", "x1", "q1", "q3", "sl", "cm", "t"]
-            + [f"e{p}_{i}" for p in (0, 1) for i in range(4)]}
-    regs["am"] = [6, 11, 25, 6, 2, 22, 13, 2]  # lanes 4-7 mirror lanes 3-0: any order works
-    regs["mk"] = lanes(0, M32)
-    regs["e1_3"], regs["e1_2"], regs["e1_1"], regs["e1_0"] = (lanes(He, 0), lanes(Hf, 0),
-                                                             lanes(Hg, 0), lanes(Hh, 0))
-    regs["e0_3"] = lanes(He, Hc)    # C4 / C2 of block 0 read the "previous" H_e / H_c here
-    regs["e0_2"] = lanes(0, Hd)     # a-feed-forward source for H_d
-    regs["g1_1"] = lanes(0, Ha)
-    regs["g1_0"] = lanes(0, Hb)
-    regs["x0"] = lanes((Hd + Hh + wk0) & M32, 0)
+
+def init_regs(Hs, wk0s, layout="quad"):
+    """Kernel prologue: register contents before block 0 (parity 0), per lane.  Hs[c] = 8-word
+    state (a..h) of chain c, wk0s[c] = W[0]+K[0] of its block 0."""
+    def lanes(f):  # f(chain state, ahalf, wk0) -> value
+        return [f(Hs[lane_chain(i, layout)], i >= 4, wk0s[lane_chain(i, layout)]) & M32
+                for i in range(8)]
+    regs = {n: [0] * 8 for n in
+            ["g0_0", "g0_1", "g1_0", "g1_1", "n0", "n1", "n2", "n3", "x1", "q1", "q2", "q3", "sl",
+             "cm", "t"] + [f"e{p}_{i}" for p in (0, 1) for i in range(4)]}
+    if layout == "quad":
+        regs["am"] = [6, 11, 25, 6, 2, 22, 13, 2]  # lanes 4-7 mirror lanes 3-0: any order works
+    else:
+        regs["am"], regs["am2"], regs["am3"] = [6] * 4 + [2] * 4, [11] * 4 + [13] * 4, [25] * 4 + [22] * 4
+    regs["mk"] = [0] * 4 + [M32] * 4
+    regs["e1_3"] = lanes(lambda H, a, w: 0 if a else H[4])
+    regs["e1_2"] = lanes(lambda H, a, w: 0 if a else H[5])
+    regs["e1_1"] = lanes(lambda H, a, w: 0 if a else H[6])
+    regs["e1_0"] = lanes(lambda H, a, w: 0 if a else H[7])
+    regs["e0_3"] = lanes(lambda H, a, w: H[2] if a else H[4])  # C4 / C2 of block 0: old H_e / H_c
+    regs["e0_2"] = lanes(lambda H, a, w: H[3] if a else 0)     # a-feed-forward source for H_d
+    regs["g1_1"] = lanes(lambda H, a, w: H[0] if a else 0)
+    regs["g1_0"] = lanes(lambda H, a, w: H[1] if a else 0)
+    regs["x0"] = lanes(lambda H, a, w: 0 if a else H[3] + H[7] + w)
     return regs
 
 
-def extract(regs, p_last):
-    """Final state after the drain (rounds 0-1 of a virtual block of parity 1 - p_last)."""
+def extract(regs, p_last, chain=0, layout="quad"):
+    """Final state of a chain after the drain (rounds 0-1 of a virtual block of parity
+    1 - p_last)."""
     q = 1 - p_last
-    e = [regs[f"e{p_last}_{i}"][0] for i in (3, 2, 1, 0)]
-    a = [regs[f"g{q}_1"][4], regs[f"g{q}_0"][4], regs[f"e{p_last}_3"][4], regs[f"e{p_last}_2"][4]]
+    el = chain if layout == "pair" else 0
+    al = 7 - chain if layout == "pair" else 4
+    e = [regs[f"e{p_last}_{i}"][el] for i in (3, 2, 1, 0)]
+    a = [regs[f"g{q}_1"][al], regs[f"g{q}_0"][al], regs[f"e{p_last}_3"][al], regs[f"e{p_last}_2"][al]]
     return a + e
 
 
-def simulate_chain(H, blocks_words):
-    """Run the generated schedule over a message's 16-word blocks; return the final state."""
-    wks = schedule(blocks_words)
-    regs = init_regs(H, wks[0][0])
-    nb = len(wks)
+def simulate_chains(Hs, blocks, layout="quad"):
+    """Run the generated schedule lane by lane over the chains of one half-row (1 for quad, 4 for
+    pair; all with the same block count); return their final states."""
+    nchains = 1 if layout == "quad" else 4
+    wks = [schedule(b) for b in blocks]
+    nb = len(wks[0])
+    assert all(len(w) == nb for w in wks)
+    regs = init_regs(Hs, [w[0][0] for w in wks], layout)
+
+    def wreg(k, r):
+        return [wks[lane_chain(i, layout)][k][r] if i < 4 else 1 for i in range(8)]
     for k in range(nb):
         p = k & 1
         for r in range(64):
-            regs[f"w{r}"] = [wks[k][r]] * 4 + [1] * 4
-        simulate_ops(rounds_ops(p), regs)
-        regs["w0"] = [wks[k + 1][0] if k + 1 < nb else 0] * 4 + [1] * 4
+            regs[f"w{r}"] = wreg(k, r)
+        simulate_ops(rounds_ops(p, layout=layout), regs)
+        regs["w0"] = wreg(k + 1, 0) if k + 1 < nb else [0] * 4 + [1] * 4
         simulate_ops(next_ops(p), regs)
-    # drain: the a-quad's last two rounds (+ its feed-forward) in a virtual block
+    # drain: the a-half's last two rounds (+ its feed-forward) in a virtual block
     p = nb & 1
-    regs["w1"] = [0] * 4 + [1] * 4
-    simulate_ops(rounds_ops(p, 0, 2), regs)
-    return extract(regs, 1 - p)
+    regs["w1"] = regs["w2"] = [0] * 4 + [1] * 4
+    simulate_ops(rounds_ops(p, 0, 2, layout), regs)
+    return [extract(regs, 1 - p, c, layout) for c in range(nchains)]
+
+
+def simulate_chain(H, blocks_words):
+    """Quad layout, one chain."""
+    return simulate_chains([H], [blocks_words])[0]
 
 
 def ref_compress(H, blocks_words):
@@ -288,9 +331,9 @@ def dpp_hazards(ops, wait_states=2):
     return bad
 
 
-def block_stream(p):
+def block_stream(p, layout="quad"):
     """Instruction order of one block of parity p followed by the next block's first rounds."""
-    return rounds_ops(p) + next_ops(p) + rounds_ops(1 - p, 0, 4)
+    return rounds_ops(p, layout=layout) + next_ops(p) + rounds_ops(1 - p, 0, 4, layout)
 
 
 # ----------------------------------------------------------------------------- asm emission
@@ -303,6 +346,8 @@ def asm_of(ins):
         return f"v_bitop3_b32 {r(ins[1])}, {r(ins[2])}, {r(ins[3])}, {r(ins[4])} bitop3:0xd2"
     if op == "bfi":
         return f"v_bfi_b32 {r(ins[1])}, {r(ins[2])}, {r(ins[3])}, {r(ins[4])}"
+    if op == "xor3":
+        return f"v_bitop3_b32 {r(ins[1])}, {r(ins[2])}, {r(ins[3])}, {r(ins[4])} bitop3:0x96"
     if op == "xor1":
         return (f"v_xor_b32_dpp {r(ins[1])}, {r(ins[2])}, {r(ins[2])} quad_perm:[1,2,0,1] "
                 "row_mask:0xf bank_mask:0xf")
@@ -337,22 +382,24 @@ def c_string(ops):
 
 
 def emit_inc(path):
-    out = ["// GENERATED by tools/gen_skew.py -- do not edit.  Skewed lane-octet SHA-256 rounds",
-           "// (8 VALU per round); see the generator's docstring for the schedule.", ""]
-    for p in (0, 1):
-        # split after round SPLIT-1: the next block's W+K reads are issued between the halves
-        out.append(f"#define S3H_SKEW_ROUNDS_A_{p} \\")
-        out.append(c_string(rounds_ops(p, 0, SPLIT)).replace("\n", " \\\n"))
-        out.append("")
-        out.append(f"#define S3H_SKEW_ROUNDS_B_{p} \\")
-        out.append(c_string(rounds_ops(p, SPLIT, 64)).replace("\n", " \\\n"))
-        out.append("")
-        out.append(f"#define S3H_SKEW_NEXT_{p} \\")
-        out.append(c_string(next_ops(p)).replace("\n", " \\\n"))
-        out.append("")
-        out.append(f"#define S3H_SKEW_DRAIN_{p} \\")
-        out.append(c_string(rounds_ops(p, 0, 2)).replace("\n", " \\\n"))
-        out.append("")
+    out = ["// GENERATED by tools/gen_skew.py -- do not edit.  Skewed SHA-256 rounds: S3H_SKEW_*",
+           "// lane-octet layout (8 VALU per round), S3H_SKEWP_* lane-pair layout (9 VALU per",
+           "// round); see the generator's docstring for the schedule.", ""]
+    for layout, tag in (("quad", "SKEW"), ("pair", "SKEWP")):
+        for p in (0, 1):
+            # split after round SPLIT-1: the next block's W+K reads are issued between the halves
+            out.append(f"#define S3H_{tag}_ROUNDS_A_{p} \\")
+            out.append(c_string(rounds_ops(p, 0, SPLIT, layout)).replace("\n", " \\\n"))
+            out.append("")
+            out.append(f"#define S3H_{tag}_ROUNDS_B_{p} \\")
+            out.append(c_string(rounds_ops(p, SPLIT, 64, layout)).replace("\n", " \\\n"))
+            out.append("")
+            out.append(f"#define S3H_{tag}_NEXT_{p} \\")
+            out.append(c_string(next_ops(p)).replace("\n", " \\\n"))
+            out.append("")
+            out.append(f"#define S3H_{tag}_DRAIN_{p} \\")
+            out.append(c_string(rounds_ops(p, 0, 2, layout)).replace("\n", " \\\n"))
+            out.append("")
     with open(path, "w") as f:
         f.write("\n".join(out))
 
@@ -371,10 +418,16 @@ def main():
             msg = bytes(rng.randrange(256) for _ in range(n))
             got = simulate_chain(IV, pad_words(msg))
             want = list(struct.unpack(">8I", hashlib.sha256(msg).digest()))
-            print(n, "ok" if got == want else f"MISMATCH {got} {want}")
+            print(n, "quad ok" if got == want else f"MISMATCH {got} {want}")
+            msgs = [bytes(rng.randrange(256) for _ in range(n)) for _ in range(4)]
+            got = simulate_chains([IV] * 4, [pad_words(m) for m in msgs], "pair")
+            want = [list(struct.unpack(">8I", hashlib.sha256(m).digest())) for m in msgs]
+            print(n, "pair ok" if got == want else "PAIR MISMATCH")
     emit_inc(a.out)
-    n = len(rounds_ops(0)) + len(next_ops(0))
-    print(f"wrote {a.out}: {n} VALU per block ({len(rounds_ops(0))} rounds + {len(next_ops(0))} next)")
+    for layout in ("quad", "pair"):
+        n = len(rounds_ops(0, layout=layout)) + len(next_ops(0))
+        print(f"{layout}: {n} VALU per block")
+    print(f"wrote {a.out}")
 
 
 if __name__ == "__main__":
