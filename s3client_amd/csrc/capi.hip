@@ -89,7 +89,7 @@ namespace {
 // the pair kernel until consumer+producer waves fill every SIMD and total instruction count
 // rules: producer/consumer up to 64K parts, then the fused one-lane-per-part kernel.
 constexpr uint64_t kQuadMaxParts = 4096;   // skew (lane octets), 1-2 consumer waves per WG
-constexpr uint64_t kSkewpMaxParts = 24576; // skewp (lane pairs, 32 chains per consumer wave)
+constexpr uint64_t kSkewpMaxParts = 28672; // skewp (lane pairs, 32 chains per consumer wave)
 constexpr uint64_t kPairMaxParts = 32768;
 constexpr uint64_t kPcMaxParts = 65536;
 constexpr uint64_t kMaxParts = 1ull << 31;

@@ -39,8 +39,12 @@ and R(-1..-4) = E[q][3..0] with q = 1 - p (the previous block's last four).  Aft
 e-feed-forward E[p][3..0] (e-lanes) are H_e..H_h; after the next block's a-feed-forward the
 a-half H_a..H_d are (G[q][1], G[q][0], E[p][3], E[p][2]) (a-lanes).
 
+The same schedule runs on a lane-PAIR layout (layout="pair"): a chain on e-lane k and a-lane
+7-k of a half-row -- the same row_half_mirror partner -- with Sigma as three per-lane rotations
+and one xor3 (9 VALU per round, four chains per half-row, 32 per wave).
+
 This module emits the asm text (`emit_inc`) consumed by s3client_amd/csrc/sha256_kernels.hip
-and simulates the same instruction lists lane by lane (`simulate_chain`), which
+and simulates the same instruction lists lane by lane (`simulate_chains`), which
 tests/test_skew_schedule.py checks against hashlib on multi-block messages.
 """
 import argparse
