@@ -52,9 +52,11 @@ def parse():
     ap.add_argument("--cpu-sample-parts", type=int, default=384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--slice-bytes", type=int, default=0, help="host mode: bytes per part per slice")
-    ap.add_argument("--mode", default="device", choices=["device", "host", "stream"],
+    ap.add_argument("--mode", default="device",
+                    choices=["device", "host", "stream", "dual", "host-dual"],
                     help="host: H2D-inclusive rate from pinned host memory; stream: the parts "
-                         "appended chunk by chunk through s3h_stream_* (neither is the metric)")
+                         "appended chunk by chunk through s3h_stream_*; dual / host-dual: "
+                         "SHA-256 + MD5 of every part in one pass (none of these is the metric)")
     ap.add_argument("--chunk-bytes", type=int, default=MIB, help="stream mode: bytes per append")
     return ap.parse_args()
 
@@ -178,10 +180,12 @@ def main():
     info = plan.info()
     kname = "md5-pc" if args.algo == "md5" else info["kernel"]
 
-    if args.mode == "host":
+    if args.mode in ("host", "host-dual"):
         return host_mode(args, s3, torch, dist, data, ids, lens, offs, world, rank, name)
     if args.mode == "stream":
         return stream_mode(args, s3, torch, data, ids, lens, offs, rank, name, stream)
+    if args.mode == "dual":
+        return dual_mode(args, s3, torch, data, ids, lens, offs, rank, name, stream)
 
     for _ in range(args.warmup):
         plan.launch(data, digests, stream)
@@ -323,24 +327,63 @@ def host_mode(args, s3, torch, dist, data, ids, lens, offs, world, rank, name):
     torch.cuda.empty_cache()
     h = host.numpy()
     views = [h[int(o):int(o) + int(L)] for o, L in zip(offs, lens)]
-    out = s3.sha256_batch_host(views, ndevices=1, slice_bytes=args.slice_bytes)
+    dual = args.mode == "host-dual"
+
+    def run():
+        if dual:
+            return s3.sha256_md5_batch_host(views, ndevices=1, slice_bytes=args.slice_bytes)
+        return s3.sha256_batch_host(views, ndevices=1, slice_bytes=args.slice_bytes), None
+
+    out, m5 = run()
     times = []
     for _ in range(max(1, args.steps)):
         t0 = time.perf_counter()
-        out = s3.sha256_batch_host(views, ndevices=1, slice_bytes=args.slice_bytes)
+        out, m5 = run()
         times.append(time.perf_counter() - t0)
     wall = float(np.mean(times))
-    with open(os.path.join(ROOT, "tests", "golden", "sha256_golden.json")) as f:
-        gold = json.load(f)
-    fixtures = {e["p"]: e["digest"] for e in gold["c2_parts"]}
-    bad = sum(s3.hash_to_text(out[s]) != fixtures[int(p)] for s, p in enumerate(ids)
-              if int(p) in fixtures)
+    bad = _fixture_mismatches(s3, ids, out, m5)
     if rank == 0:
-        print(json.dumps({"metric": "host-resident (H2D-inclusive) SHA-256 GiB/s", "value":
+        what = "SHA-256 + MD5 (one H2D pass)" if dual else "SHA-256"
+        print(json.dumps({"metric": f"host-resident (H2D-inclusive) {what} GiB/s", "value":
                           round(float(lens.sum()) / 2**30 / wall, 3), "unit": "GiB/s",
                           "n_gpus": 1, "steps": args.steps,
                           "config": {"workload": name, "slice_bytes": args.slice_bytes or "auto"},
                           "fixture_mismatches": int(bad), "ms_per_batch": round(wall * 1e3, 2)}))
+    return 0
+
+
+def _fixture_mismatches(s3, ids, sha, m5=None) -> int:
+    """Digests of the C2 parts that have committed golden fixtures, compared with them."""
+    with open(os.path.join(ROOT, "tests", "golden", "sha256_golden.json")) as f:
+        gold = json.load(f)
+    fixtures = {e["p"]: e["digest"] for e in gold["c2_parts"]}
+    bad = sum(s3.hash_to_text(sha[s]) != fixtures[int(p)] for s, p in enumerate(ids)
+              if int(p) in fixtures)
+    if m5 is not None:
+        mf = {e["p"]: e["digest"] for e in gold["md5"]["c2_parts"]}
+        bad += sum(s3.digests_to_text(m5[s:s + 1], 4)[0] != mf[int(p)] for s, p in enumerate(ids)
+                   if int(p) in mf)
+    return int(bad)
+
+
+def dual_mode(args, s3, torch, data, ids, lens, offs, rank, name, stream):
+    """Device-resident SHA-256 + MD5 of every part (s3h_sha256_md5_batch_device: the MD5
+    kernel on a side stream beside the SHA-256 one), wall time per batch incl. the join."""
+    sha, m5 = s3.sha256_md5_batch_device(data, offs, lens, stream=stream)
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(max(1, args.steps)):
+        t0 = time.perf_counter()
+        sha, m5 = s3.sha256_md5_batch_device(data, offs, lens, stream=stream)
+        times.append(time.perf_counter() - t0)
+    wall = float(np.mean(times))
+    bad = _fixture_mismatches(s3, ids, sha.cpu().numpy().view(np.uint32),
+                              m5.cpu().numpy().view(np.uint32))
+    if rank == 0:
+        print(json.dumps({"metric": "device-resident SHA-256 + MD5 GiB/s (both digests)",
+                          "value": round(float(lens.sum()) / 2**30 / wall, 3), "unit": "GiB/s",
+                          "n_gpus": 1, "steps": args.steps, "config": {"workload": name},
+                          "fixture_mismatches": bad, "ms_per_batch": round(wall * 1e3, 2)}))
     return 0
 
 

@@ -118,6 +118,21 @@ int s3h_sha256_batch_host(const uint8_t *const *parts, const uint64_t *lengths, 
 int s3h_md5_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                        uint32_t *digests, int ndevices, uint64_t slice_bytes);
 
+/* ---------------------------------------------------------------- dual digest
+ * x-amz-content-sha256 AND Content-MD5 of every part in one call (an upload that sends both
+ * headers; the MD5s also give the multipart ETag).  Replaces a sha256::sha256 plus an
+ * md5::md5 call per part (lib/hash/sha256.cpp:147-160, lib/hash/md5.cpp:71-180).
+ * Host form: each slice crosses PCIe ONCE and is hashed by both kernels on two streams, so
+ * the pair costs one H2D pass (the host path is PCIe-bound).  Device form: the MD5 kernel
+ * runs on a side stream forked from and joined back into `stream`.  Blocking.
+ * sha256_digests: n x 8 words (lib/hash layout); md5_digests: n x 4 words (memory order). */
+int s3h_sha256_md5_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
+                              uint32_t *sha256_digests, uint32_t *md5_digests, int ndevices,
+                              uint64_t slice_bytes);
+int s3h_sha256_md5_batch_device(int device, const void *d_base, const uint64_t *offsets,
+                                const uint64_t *lengths, uint64_t n, uint32_t *d_sha256,
+                                uint32_t *d_md5, void *stream);
+
 /* ---------------------------------------------------------------- verification
  * Download-side check of parts against known digests (ranged GETs of
  * lib/src/download.cpp:88-103; expected = the uploader's x-amz-content-sha256 / Content-MD5).

@@ -5,7 +5,8 @@ Drop-in for uv-cpp/s3client's lib/hash on the payload-hashing path; see DESIGN.m
 from .hashing import (Plan, device_count, digests_to_text, generate_parts, hash_to_text,
                       hmac256, nblocks, sha256, sha256_batch_device, sha256_batch_host,
                       cpu_backend, md5, md5_batch_device, md5_batch_host, multipart_etag,
-                      verify_batch_device, verify_batch_host, Stream)
+                      verify_batch_device, verify_batch_host, Stream,
+                      sha256_md5_batch_device, sha256_md5_batch_host)
 from .upload import upload_parts_geometry, UploadPart
 from ._native import S3HashError, LIB_PATH
 
@@ -13,4 +14,5 @@ __all__ = ["Plan", "device_count", "digests_to_text", "generate_parts", "hash_to
            "hmac256", "nblocks", "sha256", "sha256_batch_device", "sha256_batch_host",
            "cpu_backend", "md5", "md5_batch_device", "md5_batch_host", "multipart_etag",
            "verify_batch_device", "verify_batch_host", "Stream",
+           "sha256_md5_batch_device", "sha256_md5_batch_host",
            "upload_parts_geometry", "UploadPart", "S3HashError", "LIB_PATH"]

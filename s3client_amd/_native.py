@@ -30,6 +30,7 @@ C_ABI_SYMBOLS = (
     "s3h_verify_batch_host", "s3h_stream_create", "s3h_stream_update_device",
     "s3h_stream_final_device", "s3h_stream_update_host", "s3h_stream_final_host",
     "s3h_stream_total", "s3h_stream_destroy", "s3h_plan_set_clock_probe",
+    "s3h_sha256_md5_batch_host", "s3h_sha256_md5_batch_device",
 )
 ALGO_SHA256, ALGO_MD5 = 0, 1
 ALGO_IDS = {"sha256": ALGO_SHA256, "md5": ALGO_MD5}
@@ -96,6 +97,13 @@ def lib() -> ctypes.CDLL:
                 getattr(L, name).argtypes = [ctypes.POINTER(ctypes.c_void_p), u64p,
                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
                                              ctypes.c_uint64]
+            L.s3h_sha256_md5_batch_host.argtypes = [ctypes.POINTER(ctypes.c_void_p), u64p,
+                                                    ctypes.c_uint64, ctypes.c_void_p,
+                                                    ctypes.c_void_p, ctypes.c_int,
+                                                    ctypes.c_uint64]
+            L.s3h_sha256_md5_batch_device.argtypes = [ctypes.c_int, ctypes.c_void_p, u64p, u64p,
+                                                      ctypes.c_uint64, ctypes.c_void_p,
+                                                      ctypes.c_void_p, ctypes.c_void_p]
             L.s3h_verify_batch_host.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), u64p,
                                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                                 u64p, ctypes.c_int]

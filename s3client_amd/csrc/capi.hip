@@ -215,9 +215,9 @@ int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* le
 }
 
 // One launch of P's kernel over blocks [b0, b1) (caller holds the device guard).
-int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t* d_state,
-                uint64_t b0, uint64_t b1, uint64_t origin, uint32_t flags, const uint64_t* d_bits,
-                hipStream_t stream) {
+s3h::LaunchArgs make_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests,
+                          uint32_t* d_state, uint64_t b0, uint64_t b1, uint64_t origin,
+                          uint32_t flags, const uint64_t* d_bits) {
   s3h::LaunchArgs A;
   A.base = static_cast<const uint8_t*>(d_base);
   A.slots = P->d_slots;
@@ -232,6 +232,13 @@ int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t
   A.n = uint32_t(P->n);
   A.flags = flags | prio_flags();
   A.clocks = P->d_clocks;
+  return A;
+}
+
+int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t* d_state,
+                uint64_t b0, uint64_t b1, uint64_t origin, uint32_t flags, const uint64_t* d_bits,
+                hipStream_t stream) {
+  const s3h::LaunchArgs A = make_args(P, d_base, d_digests, d_state, b0, b1, origin, flags, d_bits);
   if (P->algo == S3H_ALGO_MD5)
     hipLaunchKernelGGL(s3h::md5_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
   // The skew kernel counts a launch's blocks in 32 bits: a range of 2^31 blocks (128 GiB of
@@ -286,15 +293,58 @@ int plan_launch(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint64_t
                      nullptr, stream);
 }
 
+// SHA-256 (plan S) and MD5 (plan M, same parts) in ONE grid (sha256_md5_dual_kernel) when S
+// runs a 128-thread skew body; returns S3H_EINVAL without launching otherwise (the caller
+// then launches the two plans on two streams).
+// The fused grid must fit one workgroup per CU: beyond that its MD5 workgroups (the grid's
+// tail) would only start as SHA-256 ones retire, i.e. run after them.
+int device_cus(int device) {
+  hipDeviceProp_t prop;
+  return hipGetDeviceProperties(&prop, device) == hipSuccess ? prop.multiProcessorCount : 0;
+}
+
+bool dual_eligible(const s3h_plan_s* S, const s3h_plan_s* M, uint64_t b0, uint64_t b1) {
+  return M->algo == S3H_ALGO_MD5 && S->algo == S3H_ALGO_SHA256 && b1 - b0 < (1ull << 31) &&
+         ((S->kernel == S3H_KERNEL_SKEW && S->quad_waves == 1) || S->kernel == S3H_KERNEL_SKEWP) &&
+         S->grid + M->grid <= uint64_t(device_cus(S->device));
+}
+
+int dual_launch(s3h_plan_s* S, s3h_plan_s* M, const void* d_base, uint32_t* d_sha,
+                uint32_t* d_md5, uint64_t b0, uint64_t b1, uint64_t origin, bool ranged,
+                hipStream_t stream) {
+  if (!dual_eligible(S, M, b0, b1)) return S3H_EINVAL;
+  if (b1 <= b0) return S3H_OK;
+  DeviceGuard g(S->device);
+  if (ranged && !S->d_state) HIP_TRY(hipMalloc(&S->d_state, S->n * 8 * sizeof(uint32_t)));
+  if (ranged && !M->d_state) HIP_TRY(hipMalloc(&M->d_state, M->n * 8 * sizeof(uint32_t)));
+  const s3h::LaunchArgs A = make_args(S, d_base, d_sha, ranged ? S->d_state : nullptr, b0, b1,
+                                      origin, 0, nullptr);
+  const s3h::LaunchArgs B = make_args(M, d_base, d_md5, ranged ? M->d_state : nullptr, b0, b1,
+                                      origin, 0, nullptr);
+  const dim3 grid(S->grid + M->grid);
+  if (S->kernel == S3H_KERNEL_SKEWP)
+    hipLaunchKernelGGL(s3h::sha256_md5_dual_kernel<true>, grid, dim3(128), 0, stream, A, B,
+                       uint32_t(S->grid));
+  else
+    hipLaunchKernelGGL(s3h::sha256_md5_dual_kernel<false>, grid, dim3(128), 0, stream, A, B,
+                       uint32_t(S->grid));
+  HIP_TRY(hipGetLastError());
+  return S3H_OK;
+}
+
 // ------------------------------------------------------------------ host streaming path
 struct HostShard {
   int device;
   std::vector<uint64_t> parts;  // global part indices on this device
 };
 
-int run_host_shard(const HostShard& sh, int algo, const uint8_t* const* parts,
-                   const uint64_t* lengths, uint32_t* digests, uint64_t slice) {
-  const uint32_t dw = digest_words(algo);
+// Streams one device's parts through a 3-slot HBM ring; every slice is copied ONCE and
+// hashed by each requested algorithm (SHA-256 and/or MD5) on its own stream, so a dual
+// digest costs one PCIe pass.  digests[a] receives algo[a]'s digests (global part order).
+int run_host_shard(const HostShard& sh, const int* algos, int nalgo, const uint8_t* const* parts,
+                   const uint64_t* lengths, uint32_t* const* digests, uint64_t slice) {
+  constexpr int kMaxAlgo = 2;
+  if (nalgo < 1 || nalgo > kMaxAlgo) return fail(S3H_EINVAL, "host shard: %d algorithms", nalgo);
   const uint64_t n = sh.parts.size();
   if (n == 0) return S3H_OK;
   DeviceGuard g(sh.device);
@@ -316,48 +366,71 @@ int run_host_shard(const HostShard& sh, int algo, const uint8_t* const* parts,
   const uint64_t budget = std::min<uint64_t>(16ull << 30, free_b / 4);
   if (3 * n * slice > budget) slice = std::max<uint64_t>(64, budget / (3 * n) / 64 * 64);
   for (uint64_t j = 0; j < n; ++j) offs[j] = j * slice;
-  s3h_plan_s* P = nullptr;
-  if (int rc = plan_build(sh.device, algo, offs.data(), lens.data(), n, S3H_KERNEL_AUTO, &P)) return rc;
-  struct Cleanup {
-    s3h_plan_s* P;
-    ~Cleanup() { s3h_plan_destroy(P); }
-  } cleanup{P};
 
+  struct Res {  // owns every device resource of this call
+    s3h_plan_s* plan[kMaxAlgo] = {};
+    uint32_t* d_dig[kMaxAlgo] = {};
+    uint8_t* ring = nullptr;
+    hipStream_t copy_s = nullptr, hash_s[kMaxAlgo] = {};
+    std::vector<hipEvent_t> events;
+    ~Res() {
+      if (copy_s) (void)hipStreamSynchronize(copy_s);
+      for (hipStream_t s : hash_s)
+        if (s) (void)hipStreamSynchronize(s);
+      for (hipEvent_t e : events) (void)hipEventDestroy(e);
+      if (copy_s) (void)hipStreamDestroy(copy_s);
+      for (hipStream_t s : hash_s)
+        if (s) (void)hipStreamDestroy(s);
+      for (uint32_t* d : d_dig)
+        if (d) (void)hipFree(d);
+      if (ring) (void)hipFree(ring);
+      for (s3h_plan_s* p : plan)
+        if (p) s3h_plan_destroy(p);
+    }
+    hipEvent_t event() {
+      hipEvent_t e = nullptr;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+      events.push_back(e);
+      return e;
+    }
+  } R;
+  uint64_t max_blocks = 0;
+  for (int a = 0; a < nalgo; ++a) {
+    if (int rc = plan_build(sh.device, algos[a], offs.data(), lens.data(), n, S3H_KERNEL_AUTO,
+                            &R.plan[a]))
+      return rc;
+    max_blocks = std::max(max_blocks, R.plan[a]->max_blocks);
+    HIP_TRY(hipMalloc(&R.d_dig[a], n * digest_words(algos[a]) * sizeof(uint32_t)));
+    HIP_TRY(hipStreamCreateWithFlags(&R.hash_s[a], hipStreamNonBlocking));
+  }
   constexpr int kRing = 3;
-  uint8_t* ring = nullptr;
-  uint32_t* d_dig = nullptr;
-  hipStream_t copy_s = nullptr, hash_s = nullptr;
-  hipEvent_t copied[kRing], hashed[kRing];
-  HIP_TRY(hipMalloc(&ring, kRing * n * slice));
-  struct Free {
-    void* p;
-    ~Free() { (void)hipFree(p); }
-  } f1{ring};
-  HIP_TRY(hipMalloc(&d_dig, n * dw * sizeof(uint32_t)));
-  Free f2{d_dig};
-  HIP_TRY(hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&hash_s, hipStreamNonBlocking));
+  HIP_TRY(hipMalloc(&R.ring, kRing * n * slice));
+  HIP_TRY(hipStreamCreateWithFlags(&R.copy_s, hipStreamNonBlocking));
+  hipEvent_t copied[kRing], hashed[kRing][kMaxAlgo];
   for (int r = 0; r < kRing; ++r) {
-    HIP_TRY(hipEventCreateWithFlags(&copied[r], hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&hashed[r], hipEventDisableTiming));
+    if (!(copied[r] = R.event())) return fail(S3H_EHIP, "event create failed");
+    for (int a = 0; a < nalgo; ++a)
+      if (!(hashed[r][a] = R.event())) return fail(S3H_EHIP, "event create failed");
   }
   const uint64_t bps = slice / 64;  // blocks per slice
+  const bool fused = nalgo == 2 && R.plan[0]->max_blocks == R.plan[1]->max_blocks &&
+                     dual_eligible(R.plan[0], R.plan[1], 0, bps);
   int rc = S3H_OK;
   uint64_t k = 0;
-  for (uint64_t b0 = 0; b0 < P->max_blocks; b0 += bps, ++k) {
+  for (uint64_t b0 = 0; b0 < max_blocks && rc == S3H_OK; b0 += bps, ++k) {
     const int r = int(k % kRing);
-    uint8_t* slot_base = ring + uint64_t(r) * n * slice;
-    if (k >= kRing) {
-      hipError_t e = hipStreamWaitEvent(copy_s, hashed[r], 0);
-      if (e != hipSuccess) { rc = fail(S3H_EHIP, "wait: %s", hipGetErrorString(e)); break; }
-    }
+    uint8_t* slot_base = R.ring + uint64_t(r) * n * slice;
+    hipError_t e = hipSuccess;
+    for (int a = 0; a < nalgo && k >= kRing && e == hipSuccess; ++a)
+      e = hipStreamWaitEvent(R.copy_s, hashed[r][a], 0);  // slot reusable once all hashed it
+    if (e != hipSuccess) { rc = fail(S3H_EHIP, "wait: %s", hipGetErrorString(e)); break; }
     const uint64_t byte0 = b0 * 64;
     if (uniform) {
       // equal-length parts at a constant host stride (file chunks): one 2-D copy per slice
       if (byte0 < lens[0]) {
         const uint64_t cnt = std::min(slice, lens[0] - byte0);
-        hipError_t e = hipMemcpy2DAsync(slot_base, slice, parts[sh.parts[0]] + byte0, stride, cnt,
-                                        n, hipMemcpyHostToDevice, copy_s);
+        e = hipMemcpy2DAsync(slot_base, slice, parts[sh.parts[0]] + byte0, stride, cnt, n,
+                             hipMemcpyHostToDevice, R.copy_s);
         if (e != hipSuccess) rc = fail(S3H_EHIP, "H2D 2D: %s", hipGetErrorString(e));
       }
     } else {
@@ -365,37 +438,40 @@ int run_host_shard(const HostShard& sh, int algo, const uint8_t* const* parts,
         const uint64_t len = lens[j];
         if (byte0 >= len) continue;
         const uint64_t cnt = std::min(slice, len - byte0);
-        hipError_t e = hipMemcpyAsync(slot_base + j * slice, parts[sh.parts[j]] + byte0, cnt,
-                                      hipMemcpyHostToDevice, copy_s);
+        e = hipMemcpyAsync(slot_base + j * slice, parts[sh.parts[j]] + byte0, cnt,
+                           hipMemcpyHostToDevice, R.copy_s);
         if (e != hipSuccess) rc = fail(S3H_EHIP, "H2D: %s", hipGetErrorString(e));
       }
     }
     if (rc) break;
-    hipError_t e = hipEventRecord(copied[r], copy_s);
-    if (e == hipSuccess) e = hipStreamWaitEvent(hash_s, copied[r], 0);
-    if (e != hipSuccess) { rc = fail(S3H_EHIP, "event: %s", hipGetErrorString(e)); break; }
-    rc = plan_launch(P, slot_base, d_dig, b0, b0 + bps, b0, hash_s, true);
-    if (rc) break;
-    e = hipEventRecord(hashed[r], hash_s);
-    if (e != hipSuccess) { rc = fail(S3H_EHIP, "event: %s", hipGetErrorString(e)); break; }
+    e = hipEventRecord(copied[r], R.copy_s);
+    if (fused) {  // both digests from one grid on one stream
+      if (e == hipSuccess) e = hipStreamWaitEvent(R.hash_s[0], copied[r], 0);
+      if (e != hipSuccess) { rc = fail(S3H_EHIP, "event: %s", hipGetErrorString(e)); break; }
+      rc = dual_launch(R.plan[0], R.plan[1], slot_base, R.d_dig[0], R.d_dig[1], b0, b0 + bps, b0,
+                       true, R.hash_s[0]);
+      if (rc == S3H_OK) e = hipEventRecord(hashed[r][0], R.hash_s[0]);
+      if (e == hipSuccess) e = hipEventRecord(hashed[r][1], R.hash_s[0]);
+    }
+    for (int a = 0; a < nalgo && rc == S3H_OK && !fused; ++a) {
+      if (e == hipSuccess) e = hipStreamWaitEvent(R.hash_s[a], copied[r], 0);
+      if (e != hipSuccess) { rc = fail(S3H_EHIP, "event: %s", hipGetErrorString(e)); break; }
+      if (b0 < R.plan[a]->max_blocks)  // both pad 9 B, so equal block counts; guard anyway
+        rc = plan_launch(R.plan[a], slot_base, R.d_dig[a], b0, b0 + bps, b0, R.hash_s[a], true);
+      if (rc == S3H_OK) e = hipEventRecord(hashed[r][a], R.hash_s[a]);
+    }
+    if (rc == S3H_OK && e != hipSuccess) rc = fail(S3H_EHIP, "event: %s", hipGetErrorString(e));
   }
-  std::vector<uint32_t> local(n * dw);
-  if (rc == S3H_OK) {
-    hipError_t e = hipMemcpyAsync(local.data(), d_dig, n * dw * 4, hipMemcpyDeviceToHost, hash_s);
-    if (e == hipSuccess) e = hipStreamSynchronize(hash_s);
-    if (e != hipSuccess) rc = fail(S3H_EHIP, "D2H digests: %s", hipGetErrorString(e));
-  }
-  (void)hipStreamSynchronize(copy_s);
-  (void)hipStreamSynchronize(hash_s);
-  for (int r = 0; r < kRing; ++r) {
-    (void)hipEventDestroy(copied[r]);
-    (void)hipEventDestroy(hashed[r]);
-  }
-  (void)hipStreamDestroy(copy_s);
-  (void)hipStreamDestroy(hash_s);
-  if (rc == S3H_OK)
+  for (int a = 0; a < nalgo && rc == S3H_OK; ++a) {
+    const uint32_t dw = digest_words(algos[a]);
+    std::vector<uint32_t> local(n * dw);
+    hipStream_t hs = R.hash_s[fused ? 0 : a];
+    hipError_t e = hipMemcpyAsync(local.data(), R.d_dig[a], n * dw * 4, hipMemcpyDeviceToHost, hs);
+    if (e == hipSuccess) e = hipStreamSynchronize(hs);
+    if (e != hipSuccess) { rc = fail(S3H_EHIP, "D2H digests: %s", hipGetErrorString(e)); break; }
     for (uint64_t j = 0; j < n; ++j)
-      std::memcpy(digests + dw * sh.parts[j], &local[dw * j], dw * 4);
+      std::memcpy(digests[a] + dw * sh.parts[j], &local[dw * j], dw * 4);
+  }
   return rc;
 }
 
@@ -636,9 +712,12 @@ int s3h_md5_batch_device(int device, const void* d_base, const uint64_t* offsets
   return batch_device(device, S3H_ALGO_MD5, d_base, offsets, lengths, n, d_digests, stream);
 }
 
-static int batch_host(int algo, const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
-                      uint32_t* digests, int ndevices, uint64_t slice_bytes) {
-  if (!parts || !lengths || !digests || n == 0) return fail(S3H_EINVAL, "batch_host: bad arguments");
+static int batch_host(const int* algos, int nalgo, const uint8_t* const* parts,
+                      const uint64_t* lengths, uint64_t n, uint32_t* const* digests, int ndevices,
+                      uint64_t slice_bytes) {
+  if (!parts || !lengths || n == 0) return fail(S3H_EINVAL, "batch_host: bad arguments");
+  for (int a = 0; a < nalgo; ++a)
+    if (!digests[a]) return fail(S3H_EINVAL, "batch_host: null digest array");
   int count = 0;
   if (int rc = s3h_device_count(&count)) return rc;
   if (ndevices <= 0 || ndevices > count) ndevices = count;
@@ -653,13 +732,19 @@ static int batch_host(int algo, const uint8_t* const* parts, const uint64_t* len
   std::vector<std::thread> pool;
   for (int d = 0; d < ndevices; ++d)
     pool.emplace_back([&, d] {
-      rcs[d] = run_host_shard(shards[d], algo, parts, lengths, digests, slice_bytes);
+      rcs[d] = run_host_shard(shards[d], algos, nalgo, parts, lengths, digests, slice_bytes);
       if (rcs[d]) errs[d] = g_err;
     });
   for (auto& t : pool) t.join();
   for (int d = 0; d < ndevices; ++d)
     if (rcs[d]) return fail(rcs[d], "device %d: %s", d, errs[d].c_str());
   return S3H_OK;
+}
+
+static int batch_host(int algo, const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
+                      uint32_t* digests, int ndevices, uint64_t slice_bytes) {
+  uint32_t* const out[1] = {digests};
+  return batch_host(&algo, 1, parts, lengths, n, out, ndevices, slice_bytes);
 }
 
 int s3h_sha256_batch_host(const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
@@ -670,6 +755,58 @@ int s3h_sha256_batch_host(const uint8_t* const* parts, const uint64_t* lengths, 
 int s3h_md5_batch_host(const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
                        uint32_t* digests, int ndevices, uint64_t slice_bytes) {
   return batch_host(S3H_ALGO_MD5, parts, lengths, n, digests, ndevices, slice_bytes);
+}
+
+int s3h_sha256_md5_batch_host(const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
+                              uint32_t* sha256_digests, uint32_t* md5_digests, int ndevices,
+                              uint64_t slice_bytes) {
+  static const int algos[2] = {S3H_ALGO_SHA256, S3H_ALGO_MD5};
+  uint32_t* const out[2] = {sha256_digests, md5_digests};
+  return batch_host(algos, 2, parts, lengths, n, out, ndevices, slice_bytes);
+}
+
+int s3h_sha256_md5_batch_device(int device, const void* d_base, const uint64_t* offsets,
+                                const uint64_t* lengths, uint64_t n, uint32_t* d_sha256,
+                                uint32_t* d_md5, void* stream) {
+  if (!d_base || !d_sha256 || !d_md5) return fail(S3H_EINVAL, "dual batch: null pointer");
+  s3h_plan_s* P[2] = {};
+  struct Cleanup {
+    s3h_plan_s** P;
+    hipStream_t side = nullptr;
+    hipEvent_t ev[2] = {};
+    ~Cleanup() {
+      if (side) (void)hipStreamSynchronize(side);
+      for (hipEvent_t e : ev)
+        if (e) (void)hipEventDestroy(e);
+      if (side) (void)hipStreamDestroy(side);
+      s3h_plan_destroy(P[0]);
+      s3h_plan_destroy(P[1]);
+    }
+  } C{P};
+  if (int rc = plan_build(device, S3H_ALGO_SHA256, offsets, lengths, n, S3H_KERNEL_AUTO, &P[0])) return rc;
+  if (int rc = plan_build(device, S3H_ALGO_MD5, offsets, lengths, n, S3H_KERNEL_AUTO, &P[1])) return rc;
+  DeviceGuard g(device);
+  hipStream_t main_s = static_cast<hipStream_t>(stream);
+  if (dual_eligible(P[0], P[1], 0, P[0]->max_blocks)) {  // one grid: both digests
+    if (int rc = dual_launch(P[0], P[1], d_base, d_sha256, d_md5, 0, P[0]->max_blocks, 0, false,
+                             main_s))
+      return rc;
+    HIP_TRY(hipStreamSynchronize(main_s));
+    return S3H_OK;
+  }
+  // Otherwise MD5 runs on a side stream forked from and joined back into the caller's: the two
+  // kernels occupy different CUs, so both digests take about the SHA-256 time.
+  HIP_TRY(hipStreamCreateWithFlags(&C.side, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&C.ev[0], hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&C.ev[1], hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(C.ev[0], main_s));
+  HIP_TRY(hipStreamWaitEvent(C.side, C.ev[0], 0));
+  if (int rc = plan_launch(P[1], d_base, d_md5, 0, P[1]->max_blocks, 0, C.side, false)) return rc;
+  if (int rc = plan_launch(P[0], d_base, d_sha256, 0, P[0]->max_blocks, 0, main_s, false)) return rc;
+  HIP_TRY(hipEventRecord(C.ev[1], C.side));
+  HIP_TRY(hipStreamWaitEvent(main_s, C.ev[1], 0));
+  HIP_TRY(hipStreamSynchronize(main_s));
+  return S3H_OK;
 }
 
 int s3h_verify_batch_device(int device, int algo, const void* d_base, const uint64_t* offsets,

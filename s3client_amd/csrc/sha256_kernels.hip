@@ -656,8 +656,10 @@ __global__ __launch_bounds__(64 * (NC * (1 + SH) + 1)) void sha256_quad_kernel(L
 
 // PAIR: the lane-pair layout of the same schedule (S3H_SKEWP_*, 9 VALU per round): a chain on
 // e-lane k and a-lane 7-k of a half-row, 32 chains per consumer wave.
-template <int NC, bool PAIR = false>
-__global__ __launch_bounds__(64 * (NC + 1)) void sha256_skew_kernel(LaunchArgs A) {
+// The kernel body takes its workgroup index as `blk` so sha256_md5_dual_kernel can run it
+// beside MD5 workgroups in one grid.
+template <int NC, bool PAIR>
+__device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t blk) {
   constexpr uint32_t kCpw = PAIR ? 32 : kQuadChainsPerWave;  // chains per consumer wave
   constexpr uint32_t kParts = kCpw * NC;
   // Blocks per producer step: 8 when the producer's lanes make at most two (part, block)
@@ -671,7 +673,7 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_skew_kernel(LaunchArgs A
 
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t slot0 = blockIdx.x * kParts;
+  const uint32_t slot0 = blk * kParts;
   const uint64_t b0 = A.blk_begin;
   const uint64_t wg_nb = slot_blocks(A, A.slots[slot0].len);
   const uint64_t wg_end = wg_nb < A.blk_end ? wg_nb : A.blk_end;
@@ -905,7 +907,7 @@ drain:
   if (A.clocks) {
     const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
-      uint64_t* c = A.clocks + 4ull * (blockIdx.x * NC + wave);
+      uint64_t* c = A.clocks + 4ull * (blk * NC + wave);
       c[0] = clk0; c[1] = clk1; c[2] = rt0; c[3] = rt1;
     }
   }
@@ -918,6 +920,11 @@ drain:
       reinterpret_cast<uint4*>(A.state + 8ull * A.out_idx[slot] + w0)[0] = make_uint4(f0, f1, f2, f3);
     }
   }
+}
+
+template <int NC, bool PAIR = false>
+__global__ __launch_bounds__(64 * (NC + 1)) void sha256_skew_kernel(LaunchArgs A) {
+  skew_body<NC, PAIR>(A, blockIdx.x);
 }
 
 // ------------------------------------------------------------- MD5 (producer/consumer)
@@ -1031,11 +1038,11 @@ __device__ __forceinline__ void md5_produce(const RawBlock& r, uint32_t sel, con
     buf[q][lane] = make_uint4(km[4 * q], km[4 * q + 1], km[4 * q + 2], km[4 * q + 3]);
 }
 
-__global__ __launch_bounds__(kPcThreads) void md5_pc_kernel(LaunchArgs A) {
+__device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t blk) {
   __shared__ uint4 lds_km[2][16][64];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t slot0 = blockIdx.x * 64u;
+  const uint32_t slot0 = blk * 64u;
   const uint32_t slot = slot0 + lane;
   const bool valid = slot < A.n;
   Slot s = {0, 0};
@@ -1107,6 +1114,26 @@ __global__ __launch_bounds__(kPcThreads) void md5_pc_kernel(LaunchArgs A) {
             make_uint4(st[0], st[1], st[2], st[3]);
     }
   }
+}
+
+__global__ __launch_bounds__(kPcThreads) void md5_pc_kernel(LaunchArgs A) { md5_pc_body(A, blockIdx.x); }
+
+// ------------------------------------------------------------- dual digest (SHA-256 + MD5)
+// One grid for x-amz-content-sha256 AND Content-MD5 of the same parts: workgroups
+// [0, sha_grid) run the skew SHA-256 body (PAIR: skewp), the rest the MD5 body.  Two
+// separate concurrent launches let the dispatcher stack MD5 workgroups onto CUs already
+// running SHA-256 ones, where the two consumers share a SIMD's issue and both chains slow
+// ~1.4-2.2x (kernel trace, profiles/r01_dual_kernel_trace.txt); one grid of <= 256
+// workgroups is placed one per CU (profiles/r01_placement.txt).  Both bodies are 128-thread
+// (1 consumer + 1 producer wave).
+static_assert(kPcThreads == 128, "dual kernel assumes 128-thread MD5 workgroups");
+template <bool PAIR>
+__global__ __launch_bounds__(128) void sha256_md5_dual_kernel(LaunchArgs S, LaunchArgs M,
+                                                              uint32_t sha_grid) {
+  if (blockIdx.x < sha_grid)
+    skew_body<1, PAIR>(S, blockIdx.x);
+  else
+    md5_pc_body(M, blockIdx.x - sha_grid);
 }
 
 // ------------------------------------------------------------- verification

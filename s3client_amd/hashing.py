@@ -8,6 +8,8 @@ and adds the batched GPU entry points that the parallel upload uses for per-part
 hashes (lib/src/upload.cpp:89-110 -> S3Api::UploadFilePart(..., payloadHash)):
   * ``Plan`` / ``sha256_batch_device``  -- parts already resident in HBM (torch tensors)
   * ``sha256_batch_host``               -- parts in host memory, sharded over GPUs
+  * ``sha256_md5_batch_{host,device}``  -- both digests (x-amz-content-sha256 + Content-MD5)
+                                           from one pass over the parts
 
 Device memory, streams and events come from PyTorch (plumbing only); all hashing is done by
 the HIP kernels in s3client_amd/csrc.  Nothing here falls back to the CPU for a batch.
@@ -154,15 +156,52 @@ def md5_batch_device(data, offsets, lengths, device: int | None = None, stream=N
     return sha256_batch_device(data, offsets, lengths, device, "auto", stream, algo="md5")
 
 
-def _host_batch(fn, words, parts, ndevices, slice_bytes):
+def _host_parts(parts):
     arrs = [np.frombuffer(p, dtype=np.uint8) if isinstance(p, (bytes, bytearray, memoryview))
             else np.ascontiguousarray(p, dtype=np.uint8).reshape(-1) for p in parts]
     n = len(arrs)
     ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data if a.size else 0 for a in arrs])
-    lens = _u64([a.size for a in arrs])
+    return arrs, ptrs, _u64([a.size for a in arrs])
+
+
+def _host_batch(fn, words, parts, ndevices, slice_bytes):
+    arrs, ptrs, lens = _host_parts(parts)
+    n = len(arrs)
     out = np.zeros((n, words), dtype=np.uint32)
     check(fn(ptrs, _p64(lens), n, out.ctypes.data, ndevices, slice_bytes))
     return out
+
+
+def sha256_md5_batch_host(parts: Sequence, ndevices: int = 0,
+                          slice_bytes: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """SHA-256 (n, 8) and MD5 (n, 4) uint32 digests of host-resident parts, each part crossing
+    PCIe once (s3h_sha256_md5_batch_host)."""
+    arrs, ptrs, lens = _host_parts(parts)
+    n = len(arrs)
+    sha = np.zeros((n, 8), dtype=np.uint32)
+    m5 = np.zeros((n, 4), dtype=np.uint32)
+    check(lib().s3h_sha256_md5_batch_host(ptrs, _p64(lens), n, sha.ctypes.data, m5.ctypes.data,
+                                          ndevices, slice_bytes))
+    return sha, m5
+
+
+def sha256_md5_batch_device(data, offsets, lengths, device: int | None = None, stream=None):
+    """SHA-256 (n, 8) and MD5 (n, 4) int32 device tensors of device-resident parts; the MD5
+    kernel runs concurrently on a side stream (s3h_sha256_md5_batch_device)."""
+    import torch
+    dev = data.device.index if device is None else device
+    offs, lens = _u64(offsets), _u64(lengths)
+    if offs.shape != lens.shape:
+        raise ValueError("offsets and lengths differ in length")
+    n = int(lens.size)
+    if n and int((offs + lens).max()) > data.numel() * data.element_size():
+        raise ValueError("a part extends past the end of the data tensor")
+    sha = torch.empty((n, 8), dtype=torch.int32, device=data.device)
+    m5 = torch.empty((n, 4), dtype=torch.int32, device=data.device)
+    check(lib().s3h_sha256_md5_batch_device(dev, data.data_ptr(), _p64(offs), _p64(lens), n,
+                                            sha.data_ptr(), m5.data_ptr(),
+                                            _stream_handle(stream)))
+    return sha, m5
 
 
 def md5_batch_host(parts: Sequence, ndevices: int = 0, slice_bytes: int = 0) -> np.ndarray:

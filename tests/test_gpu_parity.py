@@ -288,3 +288,55 @@ def test_quad_two_consumer_waves_ragged(torch_cuda, oracle, kernel):
     host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 8, dtype=np.uint8)
     got = _run(torch_cuda, host, offs, lens, kernel)
     assert np.array_equal(got, oracle.batch(host, offs, lens))
+
+
+# ------------------------------------------------------------------ dual digest (SHA-256 + MD5)
+def test_dual_digest_host_transfer_and_ragged(torch_cuda, oracle, golden):
+    """s3h_sha256_md5_batch_host: one H2D pass, both digests bit-exact (reference transfer
+    parts: SHA-256 goldens, MD5 goldens + ETag; ragged random parts vs the oracle)."""
+    t = golden["transfer"]
+    data = (np.arange(t["size"], dtype=np.uint64) % 128).astype(np.uint8)
+    views = [data[p["offset"]:p["offset"] + p["size"]] for p in t["parts"]]
+    for sl in (0, 64 << 10):
+        sha, m5 = s3.sha256_md5_batch_host(views, slice_bytes=sl)
+        assert s3.digests_to_text(sha) == [p["digest"] for p in t["parts"]]
+        assert s3.digests_to_text(m5, 4) == [p["digest"] for p in golden["md5"]["transfer"]]
+        assert s3.multipart_etag(m5) == golden["md5"]["transfer_etag"]
+    rng = np.random.default_rng(31)
+    lens = [0, 1, 55, 56, 63, 64, 65, 119, 4087, 4088, 300001, (1 << 20) + 13] * 6
+    parts = [rng.integers(0, 256, L, dtype=np.uint8) for L in lens]
+    sha, m5 = s3.sha256_md5_batch_host(parts, slice_bytes=64 << 10)
+    assert np.array_equal(sha, np.stack([oracle.sha256(p.tobytes()) for p in parts]))
+    assert np.array_equal(m5, np.stack([oracle.md5(p.tobytes()) for p in parts]))
+
+
+def test_dual_digest_device_c2_subset(torch_cuda, oracle, golden):
+    """s3h_sha256_md5_batch_device on C2 parts: SHA-256 and MD5 goldens, and every part vs
+    the single-algorithm batch entry points."""
+    data, offs, lens = _c2(torch_cuda, 256)
+    sha, m5 = s3.sha256_md5_batch_device(data, offs, lens)
+    sha = sha.cpu().numpy().view(np.uint32)
+    m5 = m5.cpu().numpy().view(np.uint32)
+    txt = s3.digests_to_text(sha)
+    for e in golden["c2_parts"]:
+        if e["p"] < 256:
+            assert txt[e["p"]] == e["digest"], e["p"]
+    m5txt = s3.digests_to_text(m5, 4)
+    for e in golden["md5"]["c2_parts"]:
+        if e["p"] < 256:
+            assert m5txt[e["p"]] == e["digest"], e["p"]
+    assert np.array_equal(sha, s3.sha256_batch_device(data, offs, lens).cpu().numpy().view(np.uint32))
+    assert np.array_equal(m5, s3.md5_batch_device(data, offs, lens).cpu().numpy().view(np.uint32))
+
+
+def test_dual_digest_device_fallback_and_fused_ragged(torch_cuda, oracle):
+    """Ragged batches on both dual-digest routes: 300 parts (fused grid, skew) and 2,500 parts
+    (skew NC=2 is not fused: MD5 on a forked side stream), each vs the oracle."""
+    rng = np.random.default_rng(33)
+    for n in (300, 2500):
+        rl = rng.integers(0, 9000, n)
+        ro = np.cumsum(rng.integers(0, 70, n) + np.concatenate([[0], rl[:-1]]))
+        host = rng.integers(0, 256, int(ro[-1] + rl[-1]) + 8, dtype=np.uint8)
+        sha, m5 = s3.sha256_md5_batch_device(_dev_buffer(torch_cuda, host), ro, rl)
+        assert np.array_equal(sha.cpu().numpy().view(np.uint32), oracle.batch(host, ro, rl)), n
+        assert np.array_equal(m5.cpu().numpy().view(np.uint32), oracle.md5_batch(host, ro, rl)), n
