@@ -59,6 +59,24 @@ inline std::vector<std::string> payload_hashes(const std::vector<const uint8_t*>
   return out;
 }
 
+// Both upload headers per part from one pass (s3h_sha256_md5_batch_host): `sha256` gets the
+// x-amz-content-sha256 hex, `md5` the 16 digest bytes of Content-MD5 (base64 them for the
+// header) -- the replacement for one sha256::sha256 + one md5::md5 call per part.
+struct DualDigests {
+  std::vector<uint32_t> sha256;  // 8 words per part, lib/hash layout
+  std::vector<uint32_t> md5;     // 4 words per part, digest bytes in memory order
+};
+inline DualDigests sha256_md5_batch(const std::vector<const uint8_t*>& parts,
+                                    const std::vector<uint64_t>& lengths, int ndevices = 0,
+                                    uint64_t slice_bytes = 0) {
+  if (parts.size() != lengths.size()) throw std::invalid_argument("parts/lengths size mismatch");
+  DualDigests d{std::vector<uint32_t>(8 * parts.size()), std::vector<uint32_t>(4 * parts.size())};
+  if (!parts.empty())
+    batch_check(s3h_sha256_md5_batch_host(parts.data(), lengths.data(), parts.size(),
+                                          d.sha256.data(), d.md5.data(), ndevices, slice_bytes));
+  return d;
+}
+
 // n objects hashed as their bodies arrive (s3h_stream_*): append() one chunk per object
 // (any length, 0 allowed), finish() -> n digests of everything appended since the last
 // finish(), after which the object restarts with n empty messages.  The batched, on-device

@@ -133,6 +133,16 @@ int main(int argc, char** argv) {
     bool ok = true;
     for (size_t i = 0; i < msgs.size(); ++i) ok &= hex[i] == digest(msgs[i]);
     report("gpu batch payload_hashes", ok);
+    // both upload headers in one pass == the single-buffer drop-ins
+    const sha256::DualDigests dd = sha256::sha256_md5_batch(ptrs, lens);
+    bool dual_ok = true;
+    for (size_t i = 0; i < msgs.size(); ++i) {
+      uint32_t h[8], m5[4];
+      sha256::sha256(ptrs[i], lens[i], h);
+      md5::md5(ptrs[i], lens[i], m5);
+      dual_ok &= std::memcmp(h, &dd.sha256[8 * i], 32) == 0 && std::memcmp(m5, &dd.md5[4 * i], 16) == 0;
+    }
+    report("gpu sha256_md5_batch", dual_ok);
     // the same messages streamed in ragged chunks through sha256::stream_batch
     sha256::stream_batch sb(msgs.size());
     std::vector<size_t> pos(msgs.size(), 0);
