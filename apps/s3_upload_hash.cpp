@@ -62,7 +62,7 @@ void usage() {
   std::fprintf(stderr,
                "usage: s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--cpu] [--verify]\n"
                "       [--print-headers] [--endpoint URL --bucket B --key K --access A\n"
-               "        --secret S --upload-id ID] [--devices N]\n");
+               "        --secret S --upload-id ID] [--devices N] [--repeat R]\n");
 }
 
 }  // namespace
@@ -70,7 +70,7 @@ void usage() {
 int main(int argc, char** argv) {
   std::string file, endpoint = "http://127.0.0.1:9000", bucket = "bucket1", key = "key1";
   std::string access = "ACCESS", secret = "SECRET", upload_id = "UPLOAD-ID";
-  int jobs = 1, ppj = 1, devices = 0;
+  int jobs = 1, ppj = 1, devices = 0, repeat = 1;
   bool cpu = false, verify = false, print_headers = false;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
@@ -91,9 +91,10 @@ int main(int argc, char** argv) {
     else if (a == "--secret") secret = next();
     else if (a == "--upload-id") upload_id = next();
     else if (a == "--devices") devices = std::atoi(next().c_str());
+    else if (a == "--repeat") repeat = std::atoi(next().c_str());
     else { usage(); return 2; }
   }
-  if (file.empty() || jobs < 1 || ppj < 1) { usage(); return 2; }
+  if (file.empty() || jobs < 1 || ppj < 1 || repeat < 1) { usage(); return 2; }
 
   const int fd = open(file.c_str(), O_RDONLY);
   if (fd < 0) { std::perror(file.c_str()); return 1; }
@@ -113,28 +114,54 @@ int main(int argc, char** argv) {
   }
 
   std::vector<std::string> hex(parts.size());
-  double t0 = now();
-  if (cpu) {  // lib/hash drop-in on the host cores, one std::thread per job as upload.cpp does
-    std::vector<std::thread> pool;
-    for (int j = 0; j < jobs; ++j)
-      pool.emplace_back([&, j] {
-        for (size_t i = 0; i < parts.size(); ++i)
-          if (parts[i].job == j) {
-            uint32_t h[8];
-            sha256::sha256(ptrs[i], lens[i], h);
-            char t[65];
-            sha256::hash_to_text(h, t);
-            hex[i] = t;
-          }
-      });
-    for (auto& t : pool) t.join();
-  } else {
+  // GPU runtime start-up (device discovery, code-object load) happens once per process in a
+  // real uploader: do it before the timed hash stage with a one-part warm-up batch.
+  double init_s = 0;
+  if (!cpu) {
+    const double ti = now();
     try {
-      hex = sha256::payload_hashes(ptrs, lens, devices);
+      static const uint8_t warm[64] = {};
+      (void)sha256::payload_hashes({warm}, {64}, devices);
     } catch (const std::exception& e) {
       std::fprintf(stderr, "%s\n", e.what());
       return 1;
     }
+    init_s = now() - ti;
+  }
+  // One hash pass over all parts: the CPU drop-in on one std::thread per job (as upload.cpp
+  // runs its jobs), or one batched GPU call.
+  auto hash_pass = [&]() -> bool {
+    if (cpu) {
+      std::vector<std::thread> pool;
+      for (int j = 0; j < jobs; ++j)
+        pool.emplace_back([&, j] {
+          for (size_t i = 0; i < parts.size(); ++i)
+            if (parts[i].job == j) {
+              uint32_t h[8];
+              sha256::sha256(ptrs[i], lens[i], h);
+              char t[65];
+              sha256::hash_to_text(h, t);
+              hex[i] = t;
+            }
+        });
+      for (auto& t : pool) t.join();
+      return true;
+    }
+    try {
+      hex = sha256::payload_hashes(ptrs, lens, devices);
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "%s\n", e.what());
+      return false;
+    }
+    return true;
+  };
+  // --repeat R: R passes (an uploader's steady state, buffers cached); the last pass is
+  // reported, the first beside it.
+  double t0 = 0, first = 0;
+  for (int rep = 0; rep < repeat; ++rep) {
+    t0 = now();
+    if (!hash_pass()) return 1;
+    if (rep == 0) first = now() - t0;
   }
   const double dt = now() - t0;
 
@@ -168,10 +195,13 @@ int main(int argc, char** argv) {
       for (const auto& kv : s3h::sigv4::SignHeaders(c))
         std::printf("# part %d %s: %s\n", parts[i].number, kv.first.c_str(), kv.second.c_str());
     }
-  std::fprintf(stderr, "%s: %zu parts, %.3f GiB in %.3f s = %.3f GiB/s%s\n",
+  std::fprintf(stderr, "%s: %zu parts, %.3f GiB in %.3f s = %.3f GiB/s%s",
                cpu ? "cpu lib/hash drop-in" : "gpu batch (H2D included)", parts.size(),
                double(size) / (1 << 30), dt, double(size) / (1 << 30) / dt,
                verify ? (mismatches ? ", VERIFY FAILED" : ", verified vs CPU") : "");
+  if (repeat > 1) std::fprintf(stderr, " (pass %d of %d; first pass %.3f s)", repeat, repeat, first);
+  if (!cpu) std::fprintf(stderr, " (GPU runtime start-up before it: %.3f s)", init_s);
+  std::fprintf(stderr, "\n");
   munmap(const_cast<uint8_t*>(data), size);
   close(fd);
   return mismatches ? 1 : 0;

@@ -57,6 +57,9 @@ enum s3h_algo {
 /* Last error message of the calling thread ("" if none). */
 const char *s3h_last_error(void);
 int s3h_api_version(void);
+/* Free the host path's cached buffers (its HBM ring and pinned staging ring are kept per
+ * device between s3h_*_batch_host / s3h_verify_batch_host calls). */
+int s3h_trim(void);
 /* Number of visible HIP devices; S3H_ENODEV (and *count = 0) when there is none. */
 int s3h_device_count(int *count);
 
@@ -109,9 +112,11 @@ int s3h_md5_batch_device(int device, const void *d_base, const uint64_t *offsets
  * parts[i] (host memory, pinned or pageable) of lengths[i] bytes -> digests (host, n*8).
  * Parts are sharded round-robin over `ndevices` GPUs (0 = all visible), part i on device
  * i % ndevices; each device streams its parts through HBM in slices of `slice_bytes` per
- * part (0 = auto: 256 KiB when the parts are equal-length chunks at a constant host stride,
- * copied with one 2-D copy per slice; 2 MiB otherwise) with copies overlapped with hashing.
- * Blocking. */
+ * part with copies overlapped with hashing.  slice_bytes 0 = auto: pinned parts are DMA'd
+ * directly (256 KiB slices and one 2-D copy per slice when they are equal-length chunks at a
+ * constant host stride, 2 MiB per-part copies otherwise); pageable parts (e.g. an mmap'd
+ * file) are first copied by host threads into a pinned staging ring (32 MiB per slot) and
+ * DMA'd from there.  The HBM and staging rings are cached per device (s3h_trim).  Blocking. */
 int s3h_sha256_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                           uint32_t *digests, int ndevices, uint64_t slice_bytes);
 
@@ -122,9 +127,10 @@ int s3h_md5_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uin
  * x-amz-content-sha256 AND Content-MD5 of every part in one call (an upload that sends both
  * headers; the MD5s also give the multipart ETag).  Replaces a sha256::sha256 plus an
  * md5::md5 call per part (lib/hash/sha256.cpp:147-160, lib/hash/md5.cpp:71-180).
- * Host form: each slice crosses PCIe ONCE and is hashed by both kernels on two streams, so
- * the pair costs one H2D pass (the host path is PCIe-bound).  Device form: the MD5 kernel
- * runs on a side stream forked from and joined back into `stream`.  Blocking.
+ * Both forms launch ONE grid whose workgroups run either the SHA-256 or the MD5 chain
+ * (sha256_md5_dual_kernel) while it fits one workgroup per CU, so both digests take the
+ * SHA-256 time; larger batches run the two kernels on two streams.  Host form: each slice
+ * crosses PCIe ONCE for both digests (the host path is PCIe-bound).  Blocking.
  * sha256_digests: n x 8 words (lib/hash layout); md5_digests: n x 4 words (memory order). */
 int s3h_sha256_md5_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                               uint32_t *sha256_digests, uint32_t *md5_digests, int ndevices,

@@ -30,7 +30,7 @@ C_ABI_SYMBOLS = (
     "s3h_verify_batch_host", "s3h_stream_create", "s3h_stream_update_device",
     "s3h_stream_final_device", "s3h_stream_update_host", "s3h_stream_final_host",
     "s3h_stream_total", "s3h_stream_destroy", "s3h_plan_set_clock_probe",
-    "s3h_sha256_md5_batch_host", "s3h_sha256_md5_batch_device",
+    "s3h_sha256_md5_batch_host", "s3h_sha256_md5_batch_device", "s3h_trim",
 )
 ALGO_SHA256, ALGO_MD5 = 0, 1
 ALGO_IDS = {"sha256": ALGO_SHA256, "md5": ALGO_MD5}

@@ -8,6 +8,11 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -333,8 +338,157 @@ int dual_launch(s3h_plan_s* S, s3h_plan_s* M, const void* d_base, uint32_t* d_sh
 }
 
 // ------------------------------------------------------------------ host streaming path
+// Host threads that fill a pinned staging slot from pageable part memory (one task per part
+// slice).  DMA straight from pageable memory goes through the runtime's bounce buffer and
+// serialises with the host; staging keeps the copy engine fed from pinned memory.
+class CopyPool {
+ public:
+  explicit CopyPool(unsigned workers) {
+    for (unsigned i = 0; i < workers; ++i) threads_.emplace_back([this] { loop(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : threads_) t.join();
+  }
+  // fn(i) for every i in [0, n), on the workers and the calling thread; returns when done.
+  void run(uint64_t n, const std::function<void(uint64_t)>& fn) {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      fn_ = &fn;
+      n_ = n;
+      next_ = 0;
+      busy_ = threads_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> l(m_);
+    done_.wait(l, [this] { return busy_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (uint64_t i; (i = next_.fetch_add(1)) < n_;) (*fn_)(i);
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+      std::lock_guard<std::mutex> l(m_);
+      if (--busy_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> threads_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(uint64_t)>* fn_ = nullptr;
+  std::atomic<uint64_t> next_{0};
+  uint64_t n_ = 0, gen_ = 0;
+  size_t busy_ = 0;
+  bool stop_ = false;
+};
+
+// Per-device cache of the host path's big buffers (the HBM ring and the pinned staging
+// ring): an uploader calls the batch once per file, and allocating ~100 MiB of pinned memory
+// costs tens of milliseconds per call.  One cached buffer per (device, kind), grown on demand;
+// s3h_trim() frees them.
+struct BufferCache {
+  struct Entry {
+    void* p = nullptr;
+    size_t bytes = 0;
+    bool busy = false;
+  };
+  std::mutex m;
+  std::vector<Entry> dev, host;  // indexed by device
+
+  // A buffer of >= bytes, or nullptr (and *err) on failure.  Never shared by two callers.
+  void* acquire(int device, bool pinned, size_t bytes, hipError_t* err) {
+    std::lock_guard<std::mutex> l(m);
+    auto& v = pinned ? host : dev;
+    if (v.size() <= size_t(device)) v.resize(device + 1);
+    Entry& e = v[device];
+    *err = hipSuccess;
+    if (e.busy) {  // a concurrent call on this device: give it a private buffer
+      void* p = nullptr;
+      *err = pinned ? hipHostMalloc(&p, bytes, hipHostMallocDefault) : hipMalloc(&p, bytes);
+      return *err == hipSuccess ? p : nullptr;
+    }
+    if (e.bytes < bytes) {
+      if (e.p) (void)(pinned ? hipHostFree(e.p) : hipFree(e.p));
+      e.p = nullptr;
+      e.bytes = 0;
+      *err = pinned ? hipHostMalloc(&e.p, bytes, hipHostMallocDefault) : hipMalloc(&e.p, bytes);
+      if (*err != hipSuccess) return nullptr;
+      e.bytes = bytes;
+    }
+    e.busy = true;
+    return e.p;
+  }
+  void release(int device, bool pinned, void* p) {
+    std::lock_guard<std::mutex> l(m);
+    auto& v = pinned ? host : dev;
+    if (size_t(device) < v.size() && v[device].p == p) {
+      v[device].busy = false;
+      return;
+    }
+    (void)(pinned ? hipHostFree(p) : hipFree(p));  // a private buffer
+  }
+  void trim() {
+    std::lock_guard<std::mutex> l(m);
+    for (int pinned = 0; pinned < 2; ++pinned)
+      for (Entry& e : pinned ? host : dev)
+        if (e.p && !e.busy) {
+          (void)(pinned ? hipHostFree(e.p) : hipFree(e.p));
+          e = Entry{};
+        }
+  }
+};
+
+BufferCache& buffer_cache() {
+  static BufferCache* c = new BufferCache();  // never destroyed: HIP may be gone at exit
+  return *c;
+}
+
+// S3H_TRACE_HOST=1: per-shard phase times of the host path on stderr (setup, pipeline, drain).
+bool trace_host() {
+  static const bool on = [] {
+    const char* e = std::getenv("S3H_TRACE_HOST");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
+
+double wall_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+bool all_pinned(const uint8_t* const* parts, const uint64_t* lengths,
+                const std::vector<uint64_t>& idx) {
+  for (uint64_t i : idx) {
+    if (!lengths[i]) continue;
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, parts[i]) != hipSuccess || a.type != hipMemoryTypeHost) {
+      (void)hipGetLastError();  // an unregistered pointer may leave a sticky error
+      return false;
+    }
+  }
+  return true;
+}
+
 struct HostShard {
   int device;
+  int ndevices;  // shards running concurrently (host threads are split between them)
   std::vector<uint64_t> parts;  // global part indices on this device
 };
 
@@ -359,7 +513,17 @@ int run_host_shard(const HostShard& sh, const int* algos, int nalgo, const uint8
   for (uint64_t j = 1; j < n && uniform; ++j)
     uniform = lens[j] == lens[0] && parts[sh.parts[j]] - parts[sh.parts[j - 1]] == stride;
   uniform = uniform && stride >= intptr_t(lens[0]) && lens[0] > 0;
-  if (slice == 0) slice = uniform ? (256ull << 10) : (2ull << 20);
+  // Pageable parts are staged through a pinned host ring filled by host threads, one
+  // contiguous DMA per slice; its slots are capped at kStageSlot bytes, so slices shrink
+  // with n (a 3-slot ring of n*slice bytes each side).
+  const double t_start = wall_s();
+  const bool staged = !all_pinned(parts, lengths, sh.parts);
+  constexpr uint64_t kStageSlot = 32ull << 20;
+  if (slice == 0)
+    slice = staged ? std::max<uint64_t>(4096, kStageSlot / n / 64 * 64)
+            : uniform ? (256ull << 10) : (2ull << 20);
+  const uint64_t longest = *std::max_element(lens.begin(), lens.end());
+  slice = std::min(slice, std::max<uint64_t>(64, (longest + 63) / 64 * 64));  // no idle slot bytes
   // The 3-slot ring holds 3*n*slice bytes: keep it within min(16 GiB, free/4) of HBM.
   size_t free_b = 0, total_b = 0;
   HIP_TRY(hipMemGetInfo(&free_b, &total_b));
@@ -370,7 +534,9 @@ int run_host_shard(const HostShard& sh, const int* algos, int nalgo, const uint8
   struct Res {  // owns every device resource of this call
     s3h_plan_s* plan[kMaxAlgo] = {};
     uint32_t* d_dig[kMaxAlgo] = {};
-    uint8_t* ring = nullptr;
+    int device = 0;
+    uint8_t* ring = nullptr;   // HBM ring (buffer cache)
+    uint8_t* stage = nullptr;  // pinned host ring, staged mode (buffer cache)
     hipStream_t copy_s = nullptr, hash_s[kMaxAlgo] = {};
     std::vector<hipEvent_t> events;
     ~Res() {
@@ -383,7 +549,8 @@ int run_host_shard(const HostShard& sh, const int* algos, int nalgo, const uint8
         if (s) (void)hipStreamDestroy(s);
       for (uint32_t* d : d_dig)
         if (d) (void)hipFree(d);
-      if (ring) (void)hipFree(ring);
+      if (ring) buffer_cache().release(device, false, ring);
+      if (stage) buffer_cache().release(device, true, stage);
       for (s3h_plan_s* p : plan)
         if (p) s3h_plan_destroy(p);
     }
@@ -394,6 +561,7 @@ int run_host_shard(const HostShard& sh, const int* algos, int nalgo, const uint8
       return e;
     }
   } R;
+  R.device = sh.device;
   uint64_t max_blocks = 0;
   for (int a = 0; a < nalgo; ++a) {
     if (int rc = plan_build(sh.device, algos[a], offs.data(), lens.data(), n, S3H_KERNEL_AUTO,
@@ -404,7 +572,18 @@ int run_host_shard(const HostShard& sh, const int* algos, int nalgo, const uint8
     HIP_TRY(hipStreamCreateWithFlags(&R.hash_s[a], hipStreamNonBlocking));
   }
   constexpr int kRing = 3;
-  HIP_TRY(hipMalloc(&R.ring, kRing * n * slice));
+  hipError_t ce = hipSuccess;
+  R.ring = static_cast<uint8_t*>(buffer_cache().acquire(sh.device, false, kRing * n * slice, &ce));
+  if (!R.ring) return fail(S3H_ENOMEM, "host ring (%llu B): %s",
+                           (unsigned long long)(kRing * n * slice), hipGetErrorString(ce));
+  std::unique_ptr<CopyPool> pool;
+  if (staged) {
+    R.stage = static_cast<uint8_t*>(buffer_cache().acquire(sh.device, true, kRing * n * slice, &ce));
+    if (!R.stage) return fail(S3H_ENOMEM, "pinned staging (%llu B): %s",
+                              (unsigned long long)(kRing * n * slice), hipGetErrorString(ce));
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    pool.reset(new CopyPool(std::min(15u, std::max(1u, hw / unsigned(sh.ndevices)) - 1)));
+  }
   HIP_TRY(hipStreamCreateWithFlags(&R.copy_s, hipStreamNonBlocking));
   hipEvent_t copied[kRing], hashed[kRing][kMaxAlgo];
   for (int r = 0; r < kRing; ++r) {
@@ -417,6 +596,7 @@ int run_host_shard(const HostShard& sh, const int* algos, int nalgo, const uint8
                      dual_eligible(R.plan[0], R.plan[1], 0, bps);
   int rc = S3H_OK;
   uint64_t k = 0;
+  const double t_setup = wall_s();
   for (uint64_t b0 = 0; b0 < max_blocks && rc == S3H_OK; b0 += bps, ++k) {
     const int r = int(k % kRing);
     uint8_t* slot_base = R.ring + uint64_t(r) * n * slice;
@@ -425,7 +605,19 @@ int run_host_shard(const HostShard& sh, const int* algos, int nalgo, const uint8
       e = hipStreamWaitEvent(R.copy_s, hashed[r][a], 0);  // slot reusable once all hashed it
     if (e != hipSuccess) { rc = fail(S3H_EHIP, "wait: %s", hipGetErrorString(e)); break; }
     const uint64_t byte0 = b0 * 64;
-    if (uniform) {
+    if (staged) {
+      // host slot r is free once the DMA that last read it (copied[r]) has finished
+      uint8_t* hslot = R.stage + uint64_t(r) * n * slice;
+      if (k >= kRing) e = hipEventSynchronize(copied[r]);
+      if (e != hipSuccess) { rc = fail(S3H_EHIP, "stage wait: %s", hipGetErrorString(e)); break; }
+      pool->run(n, [&](uint64_t j) {
+        const uint64_t len = lens[j];
+        if (byte0 < len)
+          std::memcpy(hslot + j * slice, parts[sh.parts[j]] + byte0, std::min(slice, len - byte0));
+      });
+      e = hipMemcpyAsync(slot_base, hslot, n * slice, hipMemcpyHostToDevice, R.copy_s);
+      if (e != hipSuccess) rc = fail(S3H_EHIP, "H2D staged: %s", hipGetErrorString(e));
+    } else if (uniform) {
       // equal-length parts at a constant host stride (file chunks): one 2-D copy per slice
       if (byte0 < lens[0]) {
         const uint64_t cnt = std::min(slice, lens[0] - byte0);
@@ -462,6 +654,7 @@ int run_host_shard(const HostShard& sh, const int* algos, int nalgo, const uint8
     }
     if (rc == S3H_OK && e != hipSuccess) rc = fail(S3H_EHIP, "event: %s", hipGetErrorString(e));
   }
+  const double t_issue = wall_s();
   for (int a = 0; a < nalgo && rc == S3H_OK; ++a) {
     const uint32_t dw = digest_words(algos[a]);
     std::vector<uint32_t> local(n * dw);
@@ -472,6 +665,14 @@ int run_host_shard(const HostShard& sh, const int* algos, int nalgo, const uint8
     for (uint64_t j = 0; j < n; ++j)
       std::memcpy(digests[a] + dw * sh.parts[j], &local[dw * j], dw * 4);
   }
+  if (trace_host())
+    std::fprintf(stderr,
+                 "[s3h host] dev %d: %llu parts, slice %llu B, %s, %llu slices: setup %.2f ms, "
+                 "issue %.2f ms, drain %.2f ms\n",
+                 sh.device, (unsigned long long)n, (unsigned long long)slice,
+                 staged ? "staged (pageable)" : uniform ? "pinned 2-D" : "pinned per-part",
+                 (unsigned long long)k, 1e3 * (t_setup - t_start), 1e3 * (t_issue - t_setup),
+                 1e3 * (wall_s() - t_issue));
   return rc;
 }
 
@@ -619,6 +820,11 @@ extern "C" {
 const char* s3h_last_error(void) { return g_err.c_str(); }
 int s3h_api_version(void) { return S3H_API_VERSION; }
 
+int s3h_trim(void) {
+  buffer_cache().trim();
+  return S3H_OK;
+}
+
 int s3h_device_count(int* count) {
   if (!count) return fail(S3H_EINVAL, "null count");
   *count = 0;
@@ -725,7 +931,7 @@ static int batch_host(const int* algos, int nalgo, const uint8_t* const* parts,
   for (uint64_t i = 0; i < n; ++i)
     if (!parts[i] && lengths[i]) return fail(S3H_EINVAL, "batch_host: part %llu is null", (unsigned long long)i);
   std::vector<HostShard> shards(ndevices);
-  for (int d = 0; d < ndevices; ++d) shards[d].device = d;
+  for (int d = 0; d < ndevices; ++d) shards[d] = {d, ndevices, {}};
   for (uint64_t i = 0; i < n; ++i) shards[i % ndevices].parts.push_back(i);
   std::vector<int> rcs(ndevices, S3H_OK);
   std::vector<std::string> errs(ndevices);
