@@ -460,6 +460,137 @@ BufferCache& buffer_cache() {
   return *c;
 }
 
+// Per-device cache of the host path's small resources: streams, ring events, the copy-thread
+// pool, and the last call's plans and digest buffers (reused when the next call has the same
+// part count and algorithms: the slots are re-sorted and re-uploaded in place).  An uploader
+// hashes file after file with one geometry; creating and freeing these per call cost about as
+// much as the pipeline itself (hipFree synchronises the device), profiles/r01_app_upload_hash.txt.
+constexpr int kHostRing = 3;
+constexpr int kHostMaxAlgo = 2;
+
+struct HostCtx {
+  int device = 0;
+  bool busy = false;
+  hipStream_t copy_s = nullptr, hash_s[kHostMaxAlgo] = {};
+  hipEvent_t copied[kHostRing] = {}, hashed[kHostRing][kHostMaxAlgo] = {};
+  std::unique_ptr<CopyPool> pool;
+  unsigned pool_workers = 0;
+  s3h_plan_s* plan[kHostMaxAlgo] = {};
+  uint32_t* d_dig[kHostMaxAlgo] = {};
+  uint64_t dig_bytes[kHostMaxAlgo] = {};
+
+  hipError_t ensure_streams() {
+    hipError_t e = hipSuccess;
+    if (!copy_s) e = hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking);
+    for (hipStream_t& s : hash_s)
+      if (e == hipSuccess && !s) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    for (int r = 0; r < kHostRing && e == hipSuccess; ++r) {
+      if (!copied[r]) e = hipEventCreateWithFlags(&copied[r], hipEventDisableTiming);
+      for (hipEvent_t& h : hashed[r])
+        if (e == hipSuccess && !h) e = hipEventCreateWithFlags(&h, hipEventDisableTiming);
+    }
+    return e;
+  }
+  hipError_t ensure_digests(int a, uint64_t bytes) {
+    if (dig_bytes[a] >= bytes) return hipSuccess;
+    if (d_dig[a]) (void)hipFree(d_dig[a]);
+    d_dig[a] = nullptr;
+    dig_bytes[a] = 0;
+    const hipError_t e = hipMalloc(&d_dig[a], bytes);
+    if (e == hipSuccess) dig_bytes[a] = bytes;
+    return e;
+  }
+  CopyPool* ensure_pool(unsigned workers) {
+    if (!pool || pool_workers != workers) {
+      pool.reset(new CopyPool(workers));
+      pool_workers = workers;
+    }
+    return pool.get();
+  }
+  void sync() {
+    if (copy_s) (void)hipStreamSynchronize(copy_s);
+    for (hipStream_t s : hash_s)
+      if (s) (void)hipStreamSynchronize(s);
+  }
+  ~HostCtx() {
+    DeviceGuard g(device);
+    sync();
+    pool.reset();
+    for (hipEvent_t e : copied)
+      if (e) (void)hipEventDestroy(e);
+    for (auto& row : hashed)
+      for (hipEvent_t e : row)
+        if (e) (void)hipEventDestroy(e);
+    if (copy_s) (void)hipStreamDestroy(copy_s);
+    for (hipStream_t s : hash_s)
+      if (s) (void)hipStreamDestroy(s);
+    for (uint32_t* d : d_dig)
+      if (d) (void)hipFree(d);
+    for (s3h_plan_s* p : plan)
+      if (p) s3h_plan_destroy(p);
+  }
+};
+
+struct HostCtxCache {
+  std::mutex m;
+  std::vector<HostCtx*> v;  // indexed by device
+  // The device's cached context, or a private one while another call holds it.
+  HostCtx* acquire(int device) {
+    std::lock_guard<std::mutex> l(m);
+    if (v.size() <= size_t(device)) v.resize(device + 1, nullptr);
+    HostCtx*& c = v[device];
+    if (!c) {
+      c = new HostCtx();
+      c->device = device;
+    }
+    if (c->busy) {
+      auto* p = new HostCtx();
+      p->device = device;
+      return p;
+    }
+    c->busy = true;
+    return c;
+  }
+  void release(HostCtx* c, bool keep) {
+    {
+      std::lock_guard<std::mutex> l(m);
+      if (size_t(c->device) < v.size() && v[c->device] == c) {
+        if (keep) {
+          c->busy = false;
+          return;
+        }
+        v[c->device] = nullptr;  // failed call: drop its resources
+      }
+    }
+    delete c;
+  }
+  void trim() {
+    std::lock_guard<std::mutex> l(m);
+    for (HostCtx*& c : v)
+      if (c && !c->busy) {
+        delete c;
+        c = nullptr;
+      }
+  }
+};
+
+HostCtxCache& host_ctx_cache() {
+  static HostCtxCache* c = new HostCtxCache();  // never destroyed: HIP may be gone at exit
+  return *c;
+}
+
+// Re-sort a cached plan's slots for a new geometry with the same part count (same kernel,
+// grid and state buffer) and upload them.
+int plan_reuse(s3h_plan_s* P, const uint64_t* offsets, const uint64_t* lengths) {
+  std::vector<uint32_t> order(P->n);
+  std::vector<s3h::Slot> slots(P->n);
+  P->total_blocks = sort_slots(offsets, lengths, P->n, false, slots.data(), order.data());
+  P->max_blocks = s3h::nblocks(slots[0].len);
+  HIP_TRY(hipMemcpy(P->d_slots, slots.data(), P->n * sizeof(s3h::Slot), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(P->d_out_idx, order.data(), P->n * sizeof(uint32_t), hipMemcpyHostToDevice));
+  return S3H_OK;
+}
+
 // S3H_TRACE_HOST=1: per-shard phase times of the host path on stderr (setup, pipeline, drain).
 bool trace_host() {
   static const bool on = [] {
