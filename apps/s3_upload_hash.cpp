@@ -9,7 +9,20 @@
 // x-amz-content-sha256.  No network I/O (libcurl headers, Lyra and MinIO are not available
 // in this environment): `--print-headers` shows what would be sent.
 //
-//   s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--cpu] [--verify] [--print-headers]
+// Part sources (how the bytes reach the hash, mirroring the reference's two upload paths):
+//   --source file    UploadFile (upload.cpp:113-149): parts are (file, offset, size) ranges as
+//                    UploadFilePart sends them; s3h_sha256_file_parts preads each slice
+//                    straight into pinned staging (default).
+//   --source mmap    the file mmap'd, parts = pointers into the mapping (pageable memory).
+//   --source memory  UploadData (upload.cpp:152-184): the object is a memory buffer (cfg.data)
+//                    and parts go through S3Api::UploadPart -> DoUploadPart, which in the
+//                    reference drops payloadHash (multipart_upload.cpp:131-136); here the digest
+//                    is forwarded into the signature as DoUploadFilePart does (:81-86).
+//   --per-job        one batch call per job thread at the same time (std::async per job, as
+//                    upload.cpp:136-140 runs UploadParts), instead of one call for all parts.
+//
+//   s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory] [--per-job]
+//                  [--cpu] [--verify] [--print-headers] [--devices N] [--repeat R]
 //                  [--endpoint URL --bucket B --key K --access A --secret S --upload-id ID]
 #include <fcntl.h>
 #include <sys/mman.h>
@@ -17,6 +30,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <future>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -60,9 +74,9 @@ double now() {
 
 void usage() {
   std::fprintf(stderr,
-               "usage: s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--cpu] [--verify]\n"
-               "       [--print-headers] [--endpoint URL --bucket B --key K --access A\n"
-               "        --secret S --upload-id ID] [--devices N] [--repeat R]\n");
+               "usage: s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory]\n"
+               "       [--per-job] [--cpu] [--verify] [--print-headers] [--endpoint URL --bucket B\n"
+               "        --key K --access A --secret S --upload-id ID] [--devices N] [--repeat R]\n");
 }
 
 }  // namespace
@@ -70,8 +84,9 @@ void usage() {
 int main(int argc, char** argv) {
   std::string file, endpoint = "http://127.0.0.1:9000", bucket = "bucket1", key = "key1";
   std::string access = "ACCESS", secret = "SECRET", upload_id = "UPLOAD-ID";
+  std::string source = "file";
   int jobs = 1, ppj = 1, devices = 0, repeat = 1;
-  bool cpu = false, verify = false, print_headers = false;
+  bool cpu = false, verify = false, print_headers = false, per_job = false;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -92,9 +107,12 @@ int main(int argc, char** argv) {
     else if (a == "--upload-id") upload_id = next();
     else if (a == "--devices") devices = std::atoi(next().c_str());
     else if (a == "--repeat") repeat = std::atoi(next().c_str());
+    else if (a == "--source") source = next();
+    else if (a == "--per-job") per_job = true;
     else { usage(); return 2; }
   }
-  if (file.empty() || jobs < 1 || ppj < 1 || repeat < 1) { usage(); return 2; }
+  if (file.empty() || jobs < 1 || ppj < 1 || repeat < 1 ||
+      (source != "file" && source != "mmap" && source != "memory")) { usage(); return 2; }
 
   const int fd = open(file.c_str(), O_RDONLY);
   if (fd < 0) { std::perror(file.c_str()); return 1; }
@@ -102,15 +120,30 @@ int main(int argc, char** argv) {
   fstat(fd, &st);
   const uint64_t size = uint64_t(st.st_size);
   if (size == 0) { std::fprintf(stderr, "empty file\n"); return 1; }
+  // The object's bytes as the chosen upload path holds them: a private mapping (mmap), a
+  // heap buffer read from the file (memory: the cfg.data of UploadData), or only the file
+  // name (file: UploadFilePart reads by offset).  The CPU drop-in and --verify read the mapping.
   auto* data = static_cast<const uint8_t*>(mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0));
   if (data == MAP_FAILED) { std::perror("mmap"); return 1; }
+  std::vector<uint8_t> object;
+  const uint8_t* base = data;
+  if (source == "memory") {
+    object.resize(size);
+    for (uint64_t got = 0; got < size;) {
+      const ssize_t r = pread(fd, object.data() + got, size - got, off_t(got));
+      if (r <= 0) { std::perror("read"); return 1; }
+      got += uint64_t(r);
+    }
+    base = object.data();
+  }
 
   const std::vector<Part> parts = geometry(size, jobs, ppj);
   std::vector<const uint8_t*> ptrs;
-  std::vector<uint64_t> lens;
+  std::vector<uint64_t> lens, offs;
   for (const auto& p : parts) {
-    ptrs.push_back(data + p.offset);
+    ptrs.push_back(base + p.offset);
     lens.push_back(p.size);
+    offs.push_back(p.offset);
   }
 
   std::vector<std::string> hex(parts.size());
@@ -147,8 +180,35 @@ int main(int argc, char** argv) {
       for (auto& t : pool) t.join();
       return true;
     }
+    // GPU: the parts of `idx` through the chosen source, hex digests into hex[idx[k]]
+    auto gpu = [&](const std::vector<size_t>& idx) {
+      std::vector<const uint8_t*> p;
+      std::vector<uint64_t> l, o;
+      for (size_t i : idx) {
+        p.push_back(ptrs[i]);
+        l.push_back(lens[i]);
+        o.push_back(offs[i]);
+      }
+      const std::vector<std::string> h = source == "file"
+                                             ? sha256::file_part_hashes(file, o, l, devices)
+                                             : sha256::payload_hashes(p, l, devices);
+      for (size_t k = 0; k < idx.size(); ++k) hex[idx[k]] = h[k];
+    };
     try {
-      hex = sha256::payload_hashes(ptrs, lens, devices);
+      if (per_job) {  // one concurrent batch call per job, like upload.cpp:136-140
+        std::vector<std::future<void>> fut;
+        for (int j = 0; j < jobs; ++j) {
+          std::vector<size_t> idx;
+          for (size_t i = 0; i < parts.size(); ++i)
+            if (parts[i].job == j) idx.push_back(i);
+          if (!idx.empty()) fut.push_back(std::async(std::launch::async, gpu, idx));
+        }
+        for (auto& f : fut) f.get();
+      } else {
+        std::vector<size_t> all(parts.size());
+        for (size_t i = 0; i < all.size(); ++i) all[i] = i;
+        gpu(all);
+      }
     } catch (const std::exception& e) {
       std::fprintf(stderr, "%s\n", e.what());
       return false;
@@ -189,14 +249,19 @@ int main(int argc, char** argv) {
       c.method = "PUT";
       c.bucket = bucket;
       c.key = key;
-      c.payloadHash = hex[i];  // instead of UNSIGNED-PAYLOAD (aws_sign.cpp:236-237)
-      c.parameters = {{"partNumber", std::to_string(parts[i].number)}, {"uploadId", upload_id}};
+      // instead of UNSIGNED-PAYLOAD (aws_sign.cpp:236-237); the memory path forwards it too,
+      // where the reference's DoUploadPart drops it (multipart_upload.cpp:131-136)
+      c.payloadHash = hex[i];
+      // partNumber = i + 1 (multipart_upload.cpp:79, :126)
+      c.parameters = {{"partNumber", std::to_string(parts[i].number + 1)}, {"uploadId", upload_id}};
       c.headers = {{"content-length", std::to_string(parts[i].size)}};
       for (const auto& kv : s3h::sigv4::SignHeaders(c))
         std::printf("# part %d %s: %s\n", parts[i].number, kv.first.c_str(), kv.second.c_str());
     }
-  std::fprintf(stderr, "%s: %zu parts, %.3f GiB in %.3f s = %.3f GiB/s%s",
-               cpu ? "cpu lib/hash drop-in" : "gpu batch (H2D included)", parts.size(),
+  const std::string what = cpu ? std::string("cpu lib/hash drop-in")
+                               : "gpu batch (H2D included, source " + source +
+                                     (per_job ? ", one call per job" : ", one call") + ")";
+  std::fprintf(stderr, "%s: %zu parts, %.3f GiB in %.3f s = %.3f GiB/s%s", what.c_str(), parts.size(),
                double(size) / (1 << 30), dt, double(size) / (1 << 30) / dt,
                verify ? (mismatches ? ", VERIFY FAILED" : ", verified vs CPU") : "");
   if (repeat > 1) std::fprintf(stderr, " (pass %d of %d; first pass %.3f s)", repeat, repeat, first);

@@ -57,8 +57,10 @@ enum s3h_algo {
 /* Last error message of the calling thread ("" if none). */
 const char *s3h_last_error(void);
 int s3h_api_version(void);
-/* Free the host path's cached buffers (its HBM ring and pinned staging ring are kept per
- * device between s3h_*_batch_host / s3h_verify_batch_host calls). */
+/* Free the host path's cached per-device contexts.  Between s3h_*_batch_host /
+ * s3h_sha256_file_parts / s3h_verify_batch_host calls each device keeps its streams, plans,
+ * digest buffers, at most 1 GiB of HBM ring (larger rings are freed when the call returns)
+ * and at most 96 MiB of pinned staging; s3h_trim releases all of it for idle devices. */
 int s3h_trim(void);
 /* Number of visible HIP devices; S3H_ENODEV (and *count = 0) when there is none. */
 int s3h_device_count(int *count);
@@ -115,13 +117,25 @@ int s3h_md5_batch_device(int device, const void *d_base, const uint64_t *offsets
  * part with copies overlapped with hashing.  slice_bytes 0 = auto: pinned parts are DMA'd
  * directly (256 KiB slices and one 2-D copy per slice when they are equal-length chunks at a
  * constant host stride, 2 MiB per-part copies otherwise); pageable parts (e.g. an mmap'd
- * file) are first copied by host threads into a pinned staging ring (32 MiB per slot) and
- * DMA'd from there.  The HBM and staging rings are cached per device (s3h_trim).  Blocking. */
+ * file) are first copied by host threads into a pinned staging ring (at most 32 MiB per
+ * slot: slices of 32 MiB / n bytes, down to 64 B) and DMA'd from there; beyond 524,288
+ * pageable parts, or when pinned memory is unavailable, each part is DMA'd from pageable memory.
+ * Everything is cached per device between calls (s3h_trim).  Safe to call from concurrent
+ * threads (a call that finds the device busy builds private resources).  Blocking. */
 int s3h_sha256_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                           uint32_t *digests, int ndevices, uint64_t slice_bytes);
 
 int s3h_md5_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                        uint32_t *digests, int ndevices, uint64_t slice_bytes);
+
+/* Parts given as byte ranges of a file: part i = [offsets[i], offsets[i] + lengths[i]) of
+ * `path` -- the (file, offset, size) parts that S3Api::UploadFilePart sends
+ * (lib/src/api/multipart_upload.cpp:216-223 -> WebClient::UploadFile, webclient.cpp:331-355),
+ * i.e. a batched sha256::sha256_file (lib/hash/sha256.cpp:183-233) over ranges.  Host threads
+ * pread each slice straight into the pinned staging ring (no mmap, no intermediate copy).
+ * S3H_EINVAL when the file cannot be opened or is shorter than a part.  Blocking. */
+int s3h_sha256_file_parts(const char *path, const uint64_t *offsets, const uint64_t *lengths,
+                          uint64_t n, uint32_t *digests, int ndevices, uint64_t slice_bytes);
 
 /* ---------------------------------------------------------------- dual digest
  * x-amz-content-sha256 AND Content-MD5 of every part in one call (an upload that sends both

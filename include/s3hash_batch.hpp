@@ -59,6 +59,29 @@ inline std::vector<std::string> payload_hashes(const std::vector<const uint8_t*>
   return out;
 }
 
+// Digests of byte ranges of a file -- the (file, offset, size) parts UploadFilePart sends --
+// read by host threads straight into pinned staging (s3h_sha256_file_parts), as hex.
+inline std::vector<std::string> file_part_hashes(const std::string& path,
+                                                 const std::vector<uint64_t>& offsets,
+                                                 const std::vector<uint64_t>& lengths,
+                                                 int ndevices = 0) {
+  if (offsets.size() != lengths.size()) throw std::invalid_argument("offsets/lengths size mismatch");
+  std::vector<uint32_t> d(8 * offsets.size());
+  if (!offsets.empty())
+    batch_check(s3h_sha256_file_parts(path.c_str(), offsets.data(), lengths.data(), offsets.size(),
+                                      d.data(), ndevices, 0));
+  std::vector<std::string> out(offsets.size());
+  for (size_t i = 0; i < offsets.size(); ++i) {
+    char t[65];
+    hash_to_text(&d[8 * i], t);
+    out[i] = t;
+  }
+  return out;
+}
+
+// Release the host path's cached per-device buffers (s3h_trim).
+inline void trim() { batch_check(s3h_trim()); }
+
 // Both upload headers per part from one pass (s3h_sha256_md5_batch_host): `sha256` gets the
 // x-amz-content-sha256 hex, `md5` the 16 digest bytes of Content-MD5 (base64 them for the
 // header) -- the replacement for one sha256::sha256 + one md5::md5 call per part.

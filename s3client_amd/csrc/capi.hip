@@ -6,6 +6,11 @@
 // with no HIP device every call fails with S3H_ENODEV.
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <cerrno>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -73,6 +78,7 @@ struct s3h_plan_s {
   int algo = S3H_ALGO_SHA256;
   int kernel = S3H_KERNEL_PC;
   uint64_t n = 0;
+  uint64_t cap = 0;             // parts the device arrays hold (host path: reused plans)
   uint64_t total_blocks = 0;
   uint64_t max_blocks = 0;
   uint32_t grid = 0;
@@ -80,7 +86,7 @@ struct s3h_plan_s {
   uint32_t* d_out_idx = nullptr;
   uint32_t* d_state = nullptr;  // n*8 chaining words, allocated on first ranged launch
   uint8_t* d_zero = nullptr;    // 256 zero bytes: load target for out-of-range lanes
-  int quad_waves = 1;           // quad kernel: consumer waves per workgroup (1-4)
+  int quad_waves = 1;           // skew / quad kernels: consumer waves per workgroup (1-2)
   uint64_t* d_clocks = nullptr; // clock probe buffer (caller-owned), see s3h_plan_set_clock_probe
 };
 
@@ -101,46 +107,9 @@ constexpr uint64_t kMaxParts = 1ull << 31;
 
 uint32_t digest_words(int algo) { return algo == S3H_ALGO_MD5 ? 4u : 8u; }
 
-// Blocks-per-step experiment knob for the NC = 1 quad kernel (S3H_QUAD_BPS=2|4; default 8).
-int quad_bps() {
-  static const int v = [] {
-    const char* e = std::getenv("S3H_QUAD_BPS");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
-
-// Shadow-consumer experiment knob (S3H_QUAD_SHADOW=1).
-bool quad_shadow() {
-  static const bool on = [] {
-    const char* e = std::getenv("S3H_QUAD_SHADOW");
-    return e && std::atoi(e) == 1;
-  }();
-  return on;
-}
-
-// Wave-priority experiment knob for the quad kernel (S3H_PRIO=1: no s_setprio, 2: producer
-// at priority 3 as well); default: consumers at 3.
-uint32_t prio_flags() {
-  static const uint32_t f = [] {
-    const char* e = std::getenv("S3H_PRIO");
-    const int v = e ? std::atoi(e) : 0;
-    return v == 1 ? s3h::kPrioNone : v == 2 ? s3h::kPrioAll : 0u;
-  }();
-  return f;
-}
-
-// Quad kernel: consumer waves per workgroup -- the fewest that keep the grid within one
-// workgroup per CU (256); S3H_QUAD_WAVES=1..4 overrides (sweeps).
-int quad_waves(uint64_t n) {
-  static const int forced = [] {
-    const char* e = std::getenv("S3H_QUAD_WAVES");
-    const int v = e ? std::atoi(e) : 0;
-    return v >= 1 && v <= 4 ? v : 0;
-  }();
-  if (forced) return forced;
-  return n <= 256ull * s3h::kQuadChainsPerWave ? 1 : 2;
-}
+// Skew / quad kernels: consumer waves per workgroup -- the fewest that keep the grid within
+// one workgroup per CU (256): one up to 2,048 parts, two up to 4,096 (kQuadMaxParts).
+int quad_waves(uint64_t n) { return n <= 256ull * s3h::kQuadChainsPerWave ? 1 : 2; }
 
 // Slots in descending length order (so block counts descend too, padded or not: the kernels
 // bound a workgroup's loop by its first slot); returns the total compressions.
@@ -156,64 +125,89 @@ uint64_t sort_slots(const uint64_t* offsets, const uint64_t* lengths, uint64_t n
   return total;
 }
 
-int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* lengths, uint64_t n,
-               int kernel, s3h_plan_s** out) {
-  *out = nullptr;
+int resolve_kernel(int algo, uint64_t n, int kernel) {
+  if (algo == S3H_ALGO_MD5) return S3H_KERNEL_PC;  // MD5 has one kernel (4 VALU per step)
+  if (kernel != S3H_KERNEL_AUTO) return kernel;
+  return n <= kQuadMaxParts    ? S3H_KERNEL_SKEW
+         : n <= kSkewpMaxParts ? S3H_KERNEL_SKEWP
+         : n <= kPairMaxParts  ? S3H_KERNEL_PAIR
+         : n <= kPcMaxParts    ? S3H_KERNEL_PC
+                               : S3H_KERNEL_LANE;
+}
+
+int check_plan_args(int device, int algo, uint64_t n, int kernel) {
   if (algo != S3H_ALGO_SHA256 && algo != S3H_ALGO_MD5)
     return fail(S3H_EINVAL, "plan: unknown algorithm %d", algo);
-  if (!offsets || !lengths || n == 0 || n > kMaxParts)
-    return fail(S3H_EINVAL, "plan: need offsets, lengths and 0 < n <= 2^31 (n=%llu)",
-                (unsigned long long)n);
-  if (int rc = check_device(device)) return rc;
-  if (algo == S3H_ALGO_MD5) {
-    // MD5 has one kernel (producer/consumer, 4 VALU per step on the chain)
-    if (kernel != S3H_KERNEL_AUTO && kernel != S3H_KERNEL_PC)
-      return fail(S3H_EINVAL, "plan: MD5 supports only the producer/consumer kernel");
-    kernel = S3H_KERNEL_PC;
-  }
-  if (kernel == S3H_KERNEL_AUTO)
-    kernel = n <= kQuadMaxParts    ? S3H_KERNEL_SKEW
-             : n <= kSkewpMaxParts ? S3H_KERNEL_SKEWP
-             : n <= kPairMaxParts  ? S3H_KERNEL_PAIR
-             : n <= kPcMaxParts   ? S3H_KERNEL_PC
-                                  : S3H_KERNEL_LANE;
-  if (kernel != S3H_KERNEL_PC && kernel != S3H_KERNEL_LANE && kernel != S3H_KERNEL_PAIR &&
-      kernel != S3H_KERNEL_QUAD && kernel != S3H_KERNEL_SKEW && kernel != S3H_KERNEL_SKEWP)
+  if (n == 0 || n > kMaxParts)
+    return fail(S3H_EINVAL, "plan: need 0 < n <= 2^31 (n=%llu)", (unsigned long long)n);
+  if (algo == S3H_ALGO_MD5 && kernel != S3H_KERNEL_AUTO && kernel != S3H_KERNEL_PC)
+    return fail(S3H_EINVAL, "plan: MD5 supports only the producer/consumer kernel");
+  if (kernel < S3H_KERNEL_AUTO || kernel > S3H_KERNEL_SKEWP)
     return fail(S3H_EINVAL, "plan: unknown kernel %d", kernel);
+  return check_device(device);
+}
 
-  std::vector<uint32_t> order(n);
-  std::vector<s3h::Slot> slots(n);
-  const uint64_t total = sort_slots(offsets, lengths, n, false, slots.data(), order.data());
-
+// Device arrays of a plan for up to `cap` parts (no geometry yet).  Caller holds the guard.
+int plan_alloc(int device, int algo, uint64_t cap, s3h_plan_s** out) {
   auto* P = new s3h_plan_s();
   P->device = device;
   P->algo = algo;
-  P->kernel = kernel;
-  P->n = n;
-  P->total_blocks = total;
-  P->max_blocks = s3h::nblocks(slots[0].len);
-  // skew: 1, 2 or 4 consumer waves (3 runs as 4)
-  P->quad_waves = kernel == S3H_KERNEL_SKEW && quad_waves(n) == 3 ? 4 : quad_waves(n);
-  P->grid = kernel == S3H_KERNEL_PC     ? uint32_t((n + 63) / 64)
-            : kernel == S3H_KERNEL_PAIR || kernel == S3H_KERNEL_SKEWP
-                ? uint32_t((n + s3h::kPairParts - 1) / s3h::kPairParts)
-            : kernel == S3H_KERNEL_QUAD || kernel == S3H_KERNEL_SKEW
-                ? uint32_t((n + 8 * P->quad_waves - 1) / (8 * P->quad_waves))
-                                        : uint32_t((n + 255) / 256);
-
-  DeviceGuard g(device);
-  hipError_t e = hipMalloc(&P->d_slots, n * sizeof(s3h::Slot));
-  if (e == hipSuccess) e = hipMalloc(&P->d_out_idx, n * sizeof(uint32_t));
+  P->cap = cap;
+  hipError_t e = hipMalloc(&P->d_slots, cap * sizeof(s3h::Slot));
+  if (e == hipSuccess) e = hipMalloc(&P->d_out_idx, cap * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&P->d_zero, 256);
   if (e == hipSuccess) e = hipMemset(P->d_zero, 0, 256);
-  if (e == hipSuccess) e = hipMemcpy(P->d_slots, slots.data(), n * sizeof(s3h::Slot), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(P->d_out_idx, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     (void)hipFree(P->d_slots);
     (void)hipFree(P->d_out_idx);
     (void)hipFree(P->d_zero);
     delete P;
-    return fail(e == hipErrorOutOfMemory ? S3H_ENOMEM : S3H_EHIP, "plan upload: %s", hipGetErrorString(e));
+    *out = nullptr;
+    return fail(e == hipErrorOutOfMemory ? S3H_ENOMEM : S3H_EHIP, "plan alloc: %s", hipGetErrorString(e));
+  }
+  *out = P;
+  return S3H_OK;
+}
+
+// Set n parts of geometry: kernel (AUTO by n), grid and the slots sorted by block count into
+// h_slots / h_order (n entries each), then copy them to the device on `s` (asynchronous when
+// the host arrays are pinned; the caller keeps them alive until `s` passes the copy).
+int plan_geometry(s3h_plan_s* P, const uint64_t* offsets, const uint64_t* lengths, uint64_t n,
+                  int kernel, s3h::Slot* h_slots, uint32_t* h_order, hipStream_t s) {
+  if (n > P->cap) return fail(S3H_EINVAL, "plan: %llu parts exceed capacity %llu",
+                              (unsigned long long)n, (unsigned long long)P->cap);
+  P->n = n;
+  P->kernel = resolve_kernel(P->algo, n, kernel);
+  P->total_blocks = sort_slots(offsets, lengths, n, false, h_slots, h_order);
+  P->max_blocks = s3h::nblocks(h_slots[0].len);
+  P->quad_waves = quad_waves(n);
+  P->grid = P->kernel == S3H_KERNEL_PC ? uint32_t((n + 63) / 64)
+            : P->kernel == S3H_KERNEL_PAIR || P->kernel == S3H_KERNEL_SKEWP
+                ? uint32_t((n + s3h::kPairParts - 1) / s3h::kPairParts)
+            : P->kernel == S3H_KERNEL_QUAD || P->kernel == S3H_KERNEL_SKEW
+                ? uint32_t((n + 8 * P->quad_waves - 1) / (8 * P->quad_waves))
+                : uint32_t((n + 255) / 256);
+  HIP_TRY(hipMemcpyAsync(P->d_slots, h_slots, n * sizeof(s3h::Slot), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(P->d_out_idx, h_order, n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  return S3H_OK;
+}
+
+int plan_build(int device, int algo, const uint64_t* offsets, const uint64_t* lengths, uint64_t n,
+               int kernel, s3h_plan_s** out) {
+  *out = nullptr;
+  if (!offsets || !lengths) return fail(S3H_EINVAL, "plan: need offsets and lengths");
+  if (int rc = check_plan_args(device, algo, n, kernel)) return rc;
+  DeviceGuard g(device);
+  s3h_plan_s* P = nullptr;
+  if (int rc = plan_alloc(device, algo, n, &P)) return rc;
+  std::vector<uint32_t> order(n);
+  std::vector<s3h::Slot> slots(n);
+  int rc = plan_geometry(P, offsets, lengths, n, kernel, slots.data(), order.data(), nullptr);
+  if (rc == S3H_OK && hipStreamSynchronize(nullptr) != hipSuccess)  // pageable sources
+    rc = fail(S3H_EHIP, "plan upload failed");
+  if (rc) {
+    s3h_plan_destroy(P);
+    return rc;
   }
   *out = P;
   return S3H_OK;
@@ -235,7 +229,7 @@ s3h::LaunchArgs make_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests
   A.blk_end = b1;
   A.blk_origin = origin;
   A.n = uint32_t(P->n);
-  A.flags = flags | prio_flags();
+  A.flags = flags;
   A.clocks = P->d_clocks;
   return A;
 }
@@ -258,28 +252,14 @@ int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t
     hipLaunchKernelGGL((s3h::sha256_skew_kernel<1, true>), dim3(P->grid), dim3(128), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_SKEW && P->quad_waves == 1)
     hipLaunchKernelGGL(s3h::sha256_skew_kernel<1>, dim3(P->grid), dim3(128), 0, stream, A);
-  else if (P->kernel == S3H_KERNEL_SKEW && P->quad_waves == 2)
-    hipLaunchKernelGGL(s3h::sha256_skew_kernel<2>, dim3(P->grid), dim3(192), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_SKEW)
-    hipLaunchKernelGGL(s3h::sha256_skew_kernel<4>, dim3(P->grid), dim3(320), 0, stream, A);
+    hipLaunchKernelGGL(s3h::sha256_skew_kernel<2>, dim3(P->grid), dim3(192), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_PC)
     hipLaunchKernelGGL(s3h::sha256_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
-  else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 1 && quad_shadow())
-    hipLaunchKernelGGL((s3h::sha256_quad_kernel<1, 1>), dim3(P->grid), dim3(192), 0, stream, A);
-  else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 2 && quad_shadow())
-    hipLaunchKernelGGL((s3h::sha256_quad_kernel<2, 1>), dim3(P->grid), dim3(320), 0, stream, A);
-  else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 1 && quad_bps() == 2)
-    hipLaunchKernelGGL((s3h::sha256_quad_kernel<1, 0, 2>), dim3(P->grid), dim3(128), 0, stream, A);
-  else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 1 && quad_bps() == 4)
-    hipLaunchKernelGGL((s3h::sha256_quad_kernel<1, 0, 4>), dim3(P->grid), dim3(128), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 1)
     hipLaunchKernelGGL(s3h::sha256_quad_kernel<1>, dim3(P->grid), dim3(128), 0, stream, A);
-  else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 2)
-    hipLaunchKernelGGL(s3h::sha256_quad_kernel<2>, dim3(P->grid), dim3(192), 0, stream, A);
-  else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 3)
-    hipLaunchKernelGGL(s3h::sha256_quad_kernel<3>, dim3(P->grid), dim3(256), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_QUAD)
-    hipLaunchKernelGGL(s3h::sha256_quad_kernel<4>, dim3(P->grid), dim3(320), 0, stream, A);
+    hipLaunchKernelGGL(s3h::sha256_quad_kernel<2>, dim3(P->grid), dim3(192), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_PAIR)
     hipLaunchKernelGGL(s3h::sha256_pair_kernel, dim3(P->grid), dim3(s3h::kPairThreads), 0, stream, A);
   else
@@ -293,7 +273,7 @@ int plan_launch(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint64_t
   if (!P || !d_base || !d_digests) return fail(S3H_EINVAL, "launch: null plan/base/digests");
   if (b1 <= b0) return S3H_OK;
   DeviceGuard g(P->device);
-  if (ranged && !P->d_state) HIP_TRY(hipMalloc(&P->d_state, P->n * 8 * sizeof(uint32_t)));
+  if (ranged && !P->d_state) HIP_TRY(hipMalloc(&P->d_state, P->cap * 8 * sizeof(uint32_t)));
   return launch_args(P, d_base, d_digests, ranged ? P->d_state : nullptr, b0, b1, origin, 0,
                      nullptr, stream);
 }
@@ -303,9 +283,17 @@ int plan_launch(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint64_t
 // then launches the two plans on two streams).
 // The fused grid must fit one workgroup per CU: beyond that its MD5 workgroups (the grid's
 // tail) would only start as SHA-256 ones retire, i.e. run after them.
-int device_cus(int device) {
-  hipDeviceProp_t prop;
-  return hipGetDeviceProperties(&prop, device) == hipSuccess ? prop.multiProcessorCount : 0;
+int device_cus(int device) {  // cached: the host pipeline asks once per slice
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> cus[kMaxDev] = {};
+  if (device < 0 || device >= kMaxDev) return 0;
+  int c = cus[device].load(std::memory_order_relaxed);
+  if (c == 0) {
+    hipDeviceProp_t prop;
+    c = hipGetDeviceProperties(&prop, device) == hipSuccess ? prop.multiProcessorCount : -1;
+    cus[device].store(c, std::memory_order_relaxed);
+  }
+  return c > 0 ? c : 0;
 }
 
 bool dual_eligible(const s3h_plan_s* S, const s3h_plan_s* M, uint64_t b0, uint64_t b1) {
@@ -320,8 +308,8 @@ int dual_launch(s3h_plan_s* S, s3h_plan_s* M, const void* d_base, uint32_t* d_sh
   if (!dual_eligible(S, M, b0, b1)) return S3H_EINVAL;
   if (b1 <= b0) return S3H_OK;
   DeviceGuard g(S->device);
-  if (ranged && !S->d_state) HIP_TRY(hipMalloc(&S->d_state, S->n * 8 * sizeof(uint32_t)));
-  if (ranged && !M->d_state) HIP_TRY(hipMalloc(&M->d_state, M->n * 8 * sizeof(uint32_t)));
+  if (ranged && !S->d_state) HIP_TRY(hipMalloc(&S->d_state, S->cap * 8 * sizeof(uint32_t)));
+  if (ranged && !M->d_state) HIP_TRY(hipMalloc(&M->d_state, M->cap * 8 * sizeof(uint32_t)));
   const s3h::LaunchArgs A = make_args(S, d_base, d_sha, ranged ? S->d_state : nullptr, b0, b1,
                                       origin, 0, nullptr);
   const s3h::LaunchArgs B = make_args(M, d_base, d_md5, ranged ? M->d_state : nullptr, b0, b1,
@@ -399,74 +387,40 @@ class CopyPool {
   bool stop_ = false;
 };
 
-// Per-device cache of the host path's big buffers (the HBM ring and the pinned staging
-// ring): an uploader calls the batch once per file, and allocating ~100 MiB of pinned memory
-// costs tens of milliseconds per call.  One cached buffer per (device, kind), grown on demand;
-// s3h_trim() frees them.
-struct BufferCache {
-  struct Entry {
-    void* p = nullptr;
-    size_t bytes = 0;
-    bool busy = false;
-  };
-  std::mutex m;
-  std::vector<Entry> dev, host;  // indexed by device
-
-  // A buffer of >= bytes, or nullptr (and *err) on failure.  Never shared by two callers.
-  void* acquire(int device, bool pinned, size_t bytes, hipError_t* err) {
-    std::lock_guard<std::mutex> l(m);
-    auto& v = pinned ? host : dev;
-    if (v.size() <= size_t(device)) v.resize(device + 1);
-    Entry& e = v[device];
-    *err = hipSuccess;
-    if (e.busy) {  // a concurrent call on this device: give it a private buffer
-      void* p = nullptr;
-      *err = pinned ? hipHostMalloc(&p, bytes, hipHostMallocDefault) : hipMalloc(&p, bytes);
-      return *err == hipSuccess ? p : nullptr;
-    }
-    if (e.bytes < bytes) {
-      if (e.p) (void)(pinned ? hipHostFree(e.p) : hipFree(e.p));
-      e.p = nullptr;
-      e.bytes = 0;
-      *err = pinned ? hipHostMalloc(&e.p, bytes, hipHostMallocDefault) : hipMalloc(&e.p, bytes);
-      if (*err != hipSuccess) return nullptr;
-      e.bytes = bytes;
-    }
-    e.busy = true;
-    return e.p;
-  }
-  void release(int device, bool pinned, void* p) {
-    std::lock_guard<std::mutex> l(m);
-    auto& v = pinned ? host : dev;
-    if (size_t(device) < v.size() && v[device].p == p) {
-      v[device].busy = false;
-      return;
-    }
-    (void)(pinned ? hipHostFree(p) : hipFree(p));  // a private buffer
-  }
-  void trim() {
-    std::lock_guard<std::mutex> l(m);
-    for (int pinned = 0; pinned < 2; ++pinned)
-      for (Entry& e : pinned ? host : dev)
-        if (e.p && !e.busy) {
-          (void)(pinned ? hipHostFree(e.p) : hipFree(e.p));
-          e = Entry{};
-        }
-  }
-};
-
-BufferCache& buffer_cache() {
-  static BufferCache* c = new BufferCache();  // never destroyed: HIP may be gone at exit
-  return *c;
-}
-
-// Per-device cache of the host path's small resources: streams, ring events, the copy-thread
-// pool, and the last call's plans and digest buffers (reused when the next call has the same
-// part count and algorithms: the slots are re-sorted and re-uploaded in place).  An uploader
-// hashes file after file with one geometry; creating and freeing these per call cost about as
-// much as the pipeline itself (hipFree synchronises the device), profiles/r01_app_upload_hash.txt.
+// ------------------------------------------------------------------ host-path context
+// Everything one host-path call needs on a device -- streams, ring events, the copy-thread
+// pool, plans, digest buffers, the pinned geometry staging, the HBM ring and the pinned
+// staging ring -- is cached per device and reused by the next call (an uploader hashes file
+// after file; creating and freeing these per call cost ~8 ms of a 27 ms call on a 512 MiB
+// file, profiles/r01_app_upload_hash.txt).  Buffers only grow; an HBM ring above
+// kKeepRingBytes is freed when the call returns, so a cached context holds at most
+// kKeepRingBytes of HBM plus 3 x kStageSlot of pinned memory; s3h_trim() frees idle contexts.
+// A call that finds the device's context busy (a concurrent caller) builds a private one.
 constexpr int kHostRing = 3;
 constexpr int kHostMaxAlgo = 2;
+constexpr uint64_t kStageSlot = 32ull << 20;     // pinned staging bytes per ring slot
+constexpr uint64_t kKeepRingBytes = 1ull << 30;  // largest HBM ring kept between calls
+
+// Where a shard's part bytes come from: host memory (pinned or pageable) or byte ranges of an
+// open file (read with pread straight into the pinned staging ring).
+struct PartSource {
+  const uint8_t* const* parts = nullptr;  // memory parts, or null for a file
+  int fd = -1;                            // file parts: part i = [file_off[i], +lengths[i])
+  const uint64_t* file_off = nullptr;
+  bool fill(uint64_t i, uint64_t byte0, uint64_t cnt, uint8_t* dst) const {
+    if (parts) {
+      std::memcpy(dst, parts[i] + byte0, cnt);
+      return true;
+    }
+    for (uint64_t done = 0; done < cnt;) {
+      const ssize_t r = pread(fd, dst + done, cnt - done, off_t(file_off[i] + byte0 + done));
+      if (r < 0 && errno == EINTR) continue;
+      if (r <= 0) return false;  // error or a part past the end of the file
+      done += uint64_t(r);
+    }
+    return true;
+  }
+};
 
 struct HostCtx {
   int device = 0;
@@ -478,12 +432,18 @@ struct HostCtx {
   s3h_plan_s* plan[kHostMaxAlgo] = {};
   uint32_t* d_dig[kHostMaxAlgo] = {};
   uint64_t dig_bytes[kHostMaxAlgo] = {};
+  uint8_t* pin = nullptr;    // pinned slot/order staging of both plans' geometry
+  uint64_t pin_bytes = 0;
+  uint8_t* ring = nullptr;   // HBM ring: kHostRing slots of n * slice bytes
+  uint64_t ring_bytes = 0;
+  uint8_t* stage = nullptr;  // pinned staging ring (pageable and file sources)
+  uint64_t stage_bytes = 0;
 
   hipError_t ensure_streams() {
     hipError_t e = hipSuccess;
     if (!copy_s) e = hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking);
-    for (hipStream_t& s : hash_s)
-      if (e == hipSuccess && !s) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    for (hipStream_t& st : hash_s)
+      if (e == hipSuccess && !st) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
     for (int r = 0; r < kHostRing && e == hipSuccess; ++r) {
       if (!copied[r]) e = hipEventCreateWithFlags(&copied[r], hipEventDisableTiming);
       for (hipEvent_t& h : hashed[r])
@@ -491,14 +451,26 @@ struct HostCtx {
     }
     return e;
   }
-  hipError_t ensure_digests(int a, uint64_t bytes) {
-    if (dig_bytes[a] >= bytes) return hipSuccess;
-    if (d_dig[a]) (void)hipFree(d_dig[a]);
-    d_dig[a] = nullptr;
-    dig_bytes[a] = 0;
-    const hipError_t e = hipMalloc(&d_dig[a], bytes);
-    if (e == hipSuccess) dig_bytes[a] = bytes;
+  static hipError_t grow_dev(uint8_t** p, uint64_t* have, uint64_t want) {
+    if (*have >= want) return hipSuccess;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+    const hipError_t e = hipMalloc(p, want);
+    if (e == hipSuccess) *have = want;
     return e;
+  }
+  static hipError_t grow_pinned(uint8_t** p, uint64_t* have, uint64_t want) {
+    if (*have >= want) return hipSuccess;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *have = 0;
+    const hipError_t e = hipHostMalloc(p, want, hipHostMallocDefault);
+    if (e == hipSuccess) *have = want;
+    return e;
+  }
+  hipError_t ensure_digests(int a, uint64_t bytes) {
+    return grow_dev(reinterpret_cast<uint8_t**>(&d_dig[a]), &dig_bytes[a], bytes);
   }
   CopyPool* ensure_pool(unsigned workers) {
     if (!pool || pool_workers != workers) {
@@ -507,10 +479,36 @@ struct HostCtx {
     }
     return pool.get();
   }
+  // plan[a] for algorithm `algo` with room for n parts (reallocated only to grow)
+  int ensure_plan(int a, int algo, uint64_t n) {
+    if (plan[a] && plan[a]->algo == algo && plan[a]->cap >= n) return S3H_OK;
+    s3h_plan_destroy(plan[a]);
+    plan[a] = nullptr;
+    return plan_alloc(device, algo, std::max<uint64_t>(n, 1024), &plan[a]);
+  }
+  // pinned geometry staging for plan a: cap slots + cap order entries
+  s3h::Slot* h_slots(int a) {
+    return reinterpret_cast<s3h::Slot*>(pin) + uint64_t(a) * pin_cap();
+  }
+  uint32_t* h_order(int a) {
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<s3h::Slot*>(pin) + kHostMaxAlgo * pin_cap()) +
+           uint64_t(a) * pin_cap();
+  }
+  uint64_t pin_cap() const { return pin_bytes / (kHostMaxAlgo * (sizeof(s3h::Slot) + 4)); }
+  hipError_t ensure_pin(uint64_t n) {
+    return grow_pinned(&pin, &pin_bytes, kHostMaxAlgo * std::max<uint64_t>(n, 1024) * (sizeof(s3h::Slot) + 4));
+  }
   void sync() {
     if (copy_s) (void)hipStreamSynchronize(copy_s);
-    for (hipStream_t s : hash_s)
-      if (s) (void)hipStreamSynchronize(s);
+    for (hipStream_t st : hash_s)
+      if (st) (void)hipStreamSynchronize(st);
+  }
+  void release_large() {  // after a call: do not keep a large HBM ring
+    if (ring_bytes > kKeepRingBytes) {
+      (void)hipFree(ring);
+      ring = nullptr;
+      ring_bytes = 0;
+    }
   }
   ~HostCtx() {
     DeviceGuard g(device);
@@ -522,12 +520,15 @@ struct HostCtx {
       for (hipEvent_t e : row)
         if (e) (void)hipEventDestroy(e);
     if (copy_s) (void)hipStreamDestroy(copy_s);
-    for (hipStream_t s : hash_s)
-      if (s) (void)hipStreamDestroy(s);
+    for (hipStream_t st : hash_s)
+      if (st) (void)hipStreamDestroy(st);
     for (uint32_t* d : d_dig)
       if (d) (void)hipFree(d);
     for (s3h_plan_s* p : plan)
       if (p) s3h_plan_destroy(p);
+    if (ring) (void)hipFree(ring);
+    if (stage) (void)hipHostFree(stage);
+    if (pin) (void)hipHostFree(pin);
   }
 };
 
@@ -551,44 +552,41 @@ struct HostCtxCache {
     c->busy = true;
     return c;
   }
-  void release(HostCtx* c, bool keep) {
+  // ok: the call succeeded (keep the cached context); a failed call drops its context.
+  void release(HostCtx* c, bool ok) {
+    {
+      DeviceGuard g(c->device);
+      c->release_large();
+    }
     {
       std::lock_guard<std::mutex> l(m);
       if (size_t(c->device) < v.size() && v[c->device] == c) {
-        if (keep) {
+        if (ok) {
           c->busy = false;
           return;
         }
-        v[c->device] = nullptr;  // failed call: drop its resources
+        v[c->device] = nullptr;
       }
     }
     delete c;
   }
   void trim() {
-    std::lock_guard<std::mutex> l(m);
-    for (HostCtx*& c : v)
-      if (c && !c->busy) {
-        delete c;
-        c = nullptr;
-      }
+    std::vector<HostCtx*> idle;
+    {
+      std::lock_guard<std::mutex> l(m);
+      for (HostCtx*& c : v)
+        if (c && !c->busy) {
+          idle.push_back(c);
+          c = nullptr;
+        }
+    }
+    for (HostCtx* c : idle) delete c;
   }
 };
 
 HostCtxCache& host_ctx_cache() {
   static HostCtxCache* c = new HostCtxCache();  // never destroyed: HIP may be gone at exit
   return *c;
-}
-
-// Re-sort a cached plan's slots for a new geometry with the same part count (same kernel,
-// grid and state buffer) and upload them.
-int plan_reuse(s3h_plan_s* P, const uint64_t* offsets, const uint64_t* lengths) {
-  std::vector<uint32_t> order(P->n);
-  std::vector<s3h::Slot> slots(P->n);
-  P->total_blocks = sort_slots(offsets, lengths, P->n, false, slots.data(), order.data());
-  P->max_blocks = s3h::nblocks(slots[0].len);
-  HIP_TRY(hipMemcpy(P->d_slots, slots.data(), P->n * sizeof(s3h::Slot), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(P->d_out_idx, order.data(), P->n * sizeof(uint32_t), hipMemcpyHostToDevice));
-  return S3H_OK;
 }
 
 // S3H_TRACE_HOST=1: per-shard phase times of the host path on stderr (setup, pipeline, drain).
@@ -626,134 +624,112 @@ struct HostShard {
 // Streams one device's parts through a 3-slot HBM ring; every slice is copied ONCE and
 // hashed by each requested algorithm (SHA-256 and/or MD5) on its own stream, so a dual
 // digest costs one PCIe pass.  digests[a] receives algo[a]'s digests (global part order).
-int run_host_shard(const HostShard& sh, const int* algos, int nalgo, const uint8_t* const* parts,
-                   const uint64_t* lengths, uint32_t* const* digests, uint64_t slice) {
-  constexpr int kMaxAlgo = 2;
-  if (nalgo < 1 || nalgo > kMaxAlgo) return fail(S3H_EINVAL, "host shard: %d algorithms", nalgo);
+// Copy modes per slice: pinned parts at a constant stride -> one 2-D DMA; other pinned parts
+// -> one DMA per part; pageable parts and file ranges -> host threads fill a pinned staging
+// slot (memcpy / pread) and one DMA moves it; more than kStageSlot/64 pageable parts (or no
+// pinned memory) -> one pageable DMA per part.
+int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
+                   const PartSource& src, const uint64_t* lengths, uint32_t* const* digests,
+                   uint64_t slice) {
+  if (nalgo < 1 || nalgo > kHostMaxAlgo) return fail(S3H_EINVAL, "host shard: %d algorithms", nalgo);
   const uint64_t n = sh.parts.size();
   if (n == 0) return S3H_OK;
   DeviceGuard g(sh.device);
+  const double t_start = wall_s();
   std::vector<uint64_t> offs(n), lens(n);
   for (uint64_t j = 0; j < n; ++j) lens[j] = lengths[sh.parts[j]];
-  // Fast path: all parts of this shard have one length and sit at a constant positive host
-  // stride (a file's chunks); then each slice is ONE hipMemcpy2DAsync instead of n copies,
-  // and small slices (short pipeline fill) pay off.  Otherwise per-part copies cost ~10 us
-  // each, so slices are larger (profiles/r01_host_slices.jsonl).
-  bool uniform = n > 1;
-  const intptr_t stride = n > 1 ? parts[sh.parts[1]] - parts[sh.parts[0]] : 0;
-  for (uint64_t j = 1; j < n && uniform; ++j)
-    uniform = lens[j] == lens[0] && parts[sh.parts[j]] - parts[sh.parts[j - 1]] == stride;
-  uniform = uniform && stride >= intptr_t(lens[0]) && lens[0] > 0;
-  // Pageable parts are staged through a pinned host ring filled by host threads, one
-  // contiguous DMA per slice; its slots are capped at kStageSlot bytes, so slices shrink
-  // with n (a 3-slot ring of n*slice bytes each side).
-  const double t_start = wall_s();
-  const bool staged = !all_pinned(parts, lengths, sh.parts);
-  constexpr uint64_t kStageSlot = 32ull << 20;
+  const uint8_t* const* parts = src.parts;
+  bool staged = !parts || !all_pinned(parts, lengths, sh.parts);
+  bool uniform = false;
+  intptr_t stride = 0;
+  if (!staged && n > 1) {  // equal-length parts at a constant positive host stride (file chunks)
+    stride = parts[sh.parts[1]] - parts[sh.parts[0]];
+    uniform = stride >= intptr_t(lens[0]) && lens[0] > 0;
+    for (uint64_t j = 1; j < n && uniform; ++j)
+      uniform = lens[j] == lens[0] && parts[sh.parts[j]] - parts[sh.parts[j - 1]] == stride;
+  }
+  // Too many pageable parts for the staging cap even at 64 B per slice: pageable DMAs.
+  bool direct_pageable = staged && parts && n * 64 > kStageSlot;
+  if (direct_pageable) staged = false;
   if (slice == 0)
-    slice = staged ? std::max<uint64_t>(4096, kStageSlot / n / 64 * 64)
+    slice = staged ? std::max<uint64_t>(64, kStageSlot / n / 64 * 64)
             : uniform ? (256ull << 10) : (2ull << 20);
   const uint64_t longest = *std::max_element(lens.begin(), lens.end());
   slice = std::min(slice, std::max<uint64_t>(64, (longest + 63) / 64 * 64));  // no idle slot bytes
-  // The 3-slot ring holds 3*n*slice bytes: keep it within min(16 GiB, free/4) of HBM.
+  // The ring holds kHostRing*n*slice bytes of HBM: keep it within min(16 GiB, free/4).
   size_t free_b = 0, total_b = 0;
   HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-  const uint64_t budget = std::min<uint64_t>(16ull << 30, free_b / 4);
-  if (3 * n * slice > budget) slice = std::max<uint64_t>(64, budget / (3 * n) / 64 * 64);
+  const uint64_t budget = std::min<uint64_t>(16ull << 30, (free_b + C.ring_bytes) / 4);
+  if (kHostRing * n * slice > budget) slice = std::max<uint64_t>(64, budget / (kHostRing * n) / 64 * 64);
   for (uint64_t j = 0; j < n; ++j) offs[j] = j * slice;
+  const uint64_t slot_bytes = n * slice;
 
-  struct Res {  // owns every device resource of this call
-    s3h_plan_s* plan[kMaxAlgo] = {};
-    uint32_t* d_dig[kMaxAlgo] = {};
-    int device = 0;
-    uint8_t* ring = nullptr;   // HBM ring (buffer cache)
-    uint8_t* stage = nullptr;  // pinned host ring, staged mode (buffer cache)
-    hipStream_t copy_s = nullptr, hash_s[kMaxAlgo] = {};
-    std::vector<hipEvent_t> events;
-    ~Res() {
-      if (copy_s) (void)hipStreamSynchronize(copy_s);
-      for (hipStream_t s : hash_s)
-        if (s) (void)hipStreamSynchronize(s);
-      for (hipEvent_t e : events) (void)hipEventDestroy(e);
-      if (copy_s) (void)hipStreamDestroy(copy_s);
-      for (hipStream_t s : hash_s)
-        if (s) (void)hipStreamDestroy(s);
-      for (uint32_t* d : d_dig)
-        if (d) (void)hipFree(d);
-      if (ring) buffer_cache().release(device, false, ring);
-      if (stage) buffer_cache().release(device, true, stage);
-      for (s3h_plan_s* p : plan)
-        if (p) s3h_plan_destroy(p);
+  HIP_TRY(C.ensure_streams());
+  hipError_t ce = hipSuccess;
+  if (staged) {
+    ce = HostCtx::grow_pinned(&C.stage, &C.stage_bytes, kHostRing * slot_bytes);
+    if (ce != hipSuccess) {
+      (void)hipGetLastError();
+      if (!parts) return fail(S3H_ENOMEM, "pinned staging (%llu B): %s",
+                              (unsigned long long)(kHostRing * slot_bytes), hipGetErrorString(ce));
+      staged = false;  // memory parts: fall back to pageable DMAs
+      direct_pageable = true;
     }
-    hipEvent_t event() {
-      hipEvent_t e = nullptr;
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
-      events.push_back(e);
-      return e;
-    }
-  } R;
-  R.device = sh.device;
+  }
+  ce = HostCtx::grow_dev(&C.ring, &C.ring_bytes, kHostRing * slot_bytes);
+  if (ce != hipSuccess) return fail(S3H_ENOMEM, "host ring (%llu B): %s",
+                                    (unsigned long long)(kHostRing * slot_bytes), hipGetErrorString(ce));
+  HIP_TRY(C.ensure_pin(n));
   uint64_t max_blocks = 0;
   for (int a = 0; a < nalgo; ++a) {
-    if (int rc = plan_build(sh.device, algos[a], offs.data(), lens.data(), n, S3H_KERNEL_AUTO,
-                            &R.plan[a]))
+    if (int rc = C.ensure_plan(a, algos[a], n)) return rc;
+    HIP_TRY(C.ensure_digests(a, n * digest_words(algos[a]) * sizeof(uint32_t)));
+    // geometry upload on the copy stream: every launch waits for a later copy on it
+    if (int rc = plan_geometry(C.plan[a], offs.data(), lens.data(), n, S3H_KERNEL_AUTO,
+                               C.h_slots(a), C.h_order(a), C.copy_s))
       return rc;
-    max_blocks = std::max(max_blocks, R.plan[a]->max_blocks);
-    HIP_TRY(hipMalloc(&R.d_dig[a], n * digest_words(algos[a]) * sizeof(uint32_t)));
-    HIP_TRY(hipStreamCreateWithFlags(&R.hash_s[a], hipStreamNonBlocking));
+    max_blocks = std::max(max_blocks, C.plan[a]->max_blocks);
   }
-  constexpr int kRing = 3;
-  hipError_t ce = hipSuccess;
-  R.ring = static_cast<uint8_t*>(buffer_cache().acquire(sh.device, false, kRing * n * slice, &ce));
-  if (!R.ring) return fail(S3H_ENOMEM, "host ring (%llu B): %s",
-                           (unsigned long long)(kRing * n * slice), hipGetErrorString(ce));
-  std::unique_ptr<CopyPool> pool;
+  CopyPool* pool = nullptr;
   if (staged) {
-    R.stage = static_cast<uint8_t*>(buffer_cache().acquire(sh.device, true, kRing * n * slice, &ce));
-    if (!R.stage) return fail(S3H_ENOMEM, "pinned staging (%llu B): %s",
-                              (unsigned long long)(kRing * n * slice), hipGetErrorString(ce));
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    pool.reset(new CopyPool(std::min(15u, std::max(1u, hw / unsigned(sh.ndevices)) - 1)));
-  }
-  HIP_TRY(hipStreamCreateWithFlags(&R.copy_s, hipStreamNonBlocking));
-  hipEvent_t copied[kRing], hashed[kRing][kMaxAlgo];
-  for (int r = 0; r < kRing; ++r) {
-    if (!(copied[r] = R.event())) return fail(S3H_EHIP, "event create failed");
-    for (int a = 0; a < nalgo; ++a)
-      if (!(hashed[r][a] = R.event())) return fail(S3H_EHIP, "event create failed");
+    pool = C.ensure_pool(std::min(15u, std::max(2u, hw / unsigned(sh.ndevices)) - 1));
   }
   const uint64_t bps = slice / 64;  // blocks per slice
-  const bool fused = nalgo == 2 && R.plan[0]->max_blocks == R.plan[1]->max_blocks &&
-                     dual_eligible(R.plan[0], R.plan[1], 0, bps);
+  s3h_plan_s* P0 = C.plan[0];
+  s3h_plan_s* P1 = nalgo == 2 ? C.plan[1] : nullptr;
+  const bool fused = nalgo == 2 && P0->max_blocks == P1->max_blocks &&
+                     dual_eligible(P0, P1, 0, bps);
   int rc = S3H_OK;
   uint64_t k = 0;
   const double t_setup = wall_s();
   for (uint64_t b0 = 0; b0 < max_blocks && rc == S3H_OK; b0 += bps, ++k) {
-    const int r = int(k % kRing);
-    uint8_t* slot_base = R.ring + uint64_t(r) * n * slice;
+    const int r = int(k % kHostRing);
+    uint8_t* slot_base = C.ring + uint64_t(r) * slot_bytes;
     hipError_t e = hipSuccess;
-    for (int a = 0; a < nalgo && k >= kRing && e == hipSuccess; ++a)
-      e = hipStreamWaitEvent(R.copy_s, hashed[r][a], 0);  // slot reusable once all hashed it
+    for (int a = 0; a < nalgo && k >= kHostRing && e == hipSuccess; ++a)
+      e = hipStreamWaitEvent(C.copy_s, C.hashed[r][a], 0);  // slot reusable once all hashed it
     if (e != hipSuccess) { rc = fail(S3H_EHIP, "wait: %s", hipGetErrorString(e)); break; }
     const uint64_t byte0 = b0 * 64;
     if (staged) {
       // host slot r is free once the DMA that last read it (copied[r]) has finished
-      uint8_t* hslot = R.stage + uint64_t(r) * n * slice;
-      if (k >= kRing) e = hipEventSynchronize(copied[r]);
+      uint8_t* hslot = C.stage + uint64_t(r) * slot_bytes;
+      if (k >= kHostRing) e = hipEventSynchronize(C.copied[r]);
       if (e != hipSuccess) { rc = fail(S3H_EHIP, "stage wait: %s", hipGetErrorString(e)); break; }
+      std::atomic<bool> bad{false};
       pool->run(n, [&](uint64_t j) {
         const uint64_t len = lens[j];
-        if (byte0 < len)
-          std::memcpy(hslot + j * slice, parts[sh.parts[j]] + byte0, std::min(slice, len - byte0));
+        if (byte0 < len && !src.fill(sh.parts[j], byte0, std::min(slice, len - byte0), hslot + j * slice))
+          bad.store(true, std::memory_order_relaxed);
       });
-      e = hipMemcpyAsync(slot_base, hslot, n * slice, hipMemcpyHostToDevice, R.copy_s);
+      if (bad.load()) { rc = fail(S3H_EINVAL, "reading a part failed (file shorter than a part?)"); break; }
+      e = hipMemcpyAsync(slot_base, hslot, slot_bytes, hipMemcpyHostToDevice, C.copy_s);
       if (e != hipSuccess) rc = fail(S3H_EHIP, "H2D staged: %s", hipGetErrorString(e));
     } else if (uniform) {
-      // equal-length parts at a constant host stride (file chunks): one 2-D copy per slice
       if (byte0 < lens[0]) {
         const uint64_t cnt = std::min(slice, lens[0] - byte0);
         e = hipMemcpy2DAsync(slot_base, slice, parts[sh.parts[0]] + byte0, stride, cnt, n,
-                             hipMemcpyHostToDevice, R.copy_s);
+                             hipMemcpyHostToDevice, C.copy_s);
         if (e != hipSuccess) rc = fail(S3H_EHIP, "H2D 2D: %s", hipGetErrorString(e));
       }
     } else {
@@ -762,26 +738,26 @@ int run_host_shard(const HostShard& sh, const int* algos, int nalgo, const uint8
         if (byte0 >= len) continue;
         const uint64_t cnt = std::min(slice, len - byte0);
         e = hipMemcpyAsync(slot_base + j * slice, parts[sh.parts[j]] + byte0, cnt,
-                           hipMemcpyHostToDevice, R.copy_s);
+                           hipMemcpyHostToDevice, C.copy_s);
         if (e != hipSuccess) rc = fail(S3H_EHIP, "H2D: %s", hipGetErrorString(e));
       }
     }
     if (rc) break;
-    e = hipEventRecord(copied[r], R.copy_s);
+    e = hipEventRecord(C.copied[r], C.copy_s);
     if (fused) {  // both digests from one grid on one stream
-      if (e == hipSuccess) e = hipStreamWaitEvent(R.hash_s[0], copied[r], 0);
+      if (e == hipSuccess) e = hipStreamWaitEvent(C.hash_s[0], C.copied[r], 0);
       if (e != hipSuccess) { rc = fail(S3H_EHIP, "event: %s", hipGetErrorString(e)); break; }
-      rc = dual_launch(R.plan[0], R.plan[1], slot_base, R.d_dig[0], R.d_dig[1], b0, b0 + bps, b0,
-                       true, R.hash_s[0]);
-      if (rc == S3H_OK) e = hipEventRecord(hashed[r][0], R.hash_s[0]);
-      if (e == hipSuccess) e = hipEventRecord(hashed[r][1], R.hash_s[0]);
+      rc = dual_launch(P0, P1, slot_base, C.d_dig[0], C.d_dig[1], b0, b0 + bps, b0, true,
+                       C.hash_s[0]);
+      if (rc == S3H_OK) e = hipEventRecord(C.hashed[r][0], C.hash_s[0]);
+      if (e == hipSuccess) e = hipEventRecord(C.hashed[r][1], C.hash_s[0]);
     }
     for (int a = 0; a < nalgo && rc == S3H_OK && !fused; ++a) {
-      if (e == hipSuccess) e = hipStreamWaitEvent(R.hash_s[a], copied[r], 0);
+      if (e == hipSuccess) e = hipStreamWaitEvent(C.hash_s[a], C.copied[r], 0);
       if (e != hipSuccess) { rc = fail(S3H_EHIP, "event: %s", hipGetErrorString(e)); break; }
-      if (b0 < R.plan[a]->max_blocks)  // both pad 9 B, so equal block counts; guard anyway
-        rc = plan_launch(R.plan[a], slot_base, R.d_dig[a], b0, b0 + bps, b0, R.hash_s[a], true);
-      if (rc == S3H_OK) e = hipEventRecord(hashed[r][a], R.hash_s[a]);
+      if (b0 < C.plan[a]->max_blocks)  // both pad 9 B, so equal block counts; guard anyway
+        rc = plan_launch(C.plan[a], slot_base, C.d_dig[a], b0, b0 + bps, b0, C.hash_s[a], true);
+      if (rc == S3H_OK) e = hipEventRecord(C.hashed[r][a], C.hash_s[a]);
     }
     if (rc == S3H_OK && e != hipSuccess) rc = fail(S3H_EHIP, "event: %s", hipGetErrorString(e));
   }
@@ -789,19 +765,21 @@ int run_host_shard(const HostShard& sh, const int* algos, int nalgo, const uint8
   for (int a = 0; a < nalgo && rc == S3H_OK; ++a) {
     const uint32_t dw = digest_words(algos[a]);
     std::vector<uint32_t> local(n * dw);
-    hipStream_t hs = R.hash_s[fused ? 0 : a];
-    hipError_t e = hipMemcpyAsync(local.data(), R.d_dig[a], n * dw * 4, hipMemcpyDeviceToHost, hs);
+    hipStream_t hs = C.hash_s[fused ? 0 : a];
+    hipError_t e = hipMemcpyAsync(local.data(), C.d_dig[a], n * dw * 4, hipMemcpyDeviceToHost, hs);
     if (e == hipSuccess) e = hipStreamSynchronize(hs);
     if (e != hipSuccess) { rc = fail(S3H_EHIP, "D2H digests: %s", hipGetErrorString(e)); break; }
     for (uint64_t j = 0; j < n; ++j)
       std::memcpy(digests[a] + dw * sh.parts[j], &local[dw * j], dw * 4);
   }
+  C.sync();  // nothing of this call may still run when the context is handed on
   if (trace_host())
     std::fprintf(stderr,
                  "[s3h host] dev %d: %llu parts, slice %llu B, %s, %llu slices: setup %.2f ms, "
                  "issue %.2f ms, drain %.2f ms\n",
                  sh.device, (unsigned long long)n, (unsigned long long)slice,
-                 staged ? "staged (pageable)" : uniform ? "pinned 2-D" : "pinned per-part",
+                 !parts ? "staged (file pread)" : staged ? "staged (pageable)"
+                 : direct_pageable ? "pageable per-part" : uniform ? "pinned 2-D" : "pinned per-part",
                  (unsigned long long)k, 1e3 * (t_setup - t_start), 1e3 * (t_issue - t_setup),
                  1e3 * (wall_s() - t_issue));
   return rc;
@@ -952,7 +930,7 @@ const char* s3h_last_error(void) { return g_err.c_str(); }
 int s3h_api_version(void) { return S3H_API_VERSION; }
 
 int s3h_trim(void) {
-  buffer_cache().trim();
+  host_ctx_cache().trim();
   return S3H_OK;
 }
 
@@ -1049,30 +1027,38 @@ int s3h_md5_batch_device(int device, const void* d_base, const uint64_t* offsets
   return batch_device(device, S3H_ALGO_MD5, d_base, offsets, lengths, n, d_digests, stream);
 }
 
-static int batch_host(const int* algos, int nalgo, const uint8_t* const* parts,
+static int batch_host(const int* algos, int nalgo, const PartSource& src,
                       const uint64_t* lengths, uint64_t n, uint32_t* const* digests, int ndevices,
                       uint64_t slice_bytes) {
-  if (!parts || !lengths || n == 0) return fail(S3H_EINVAL, "batch_host: bad arguments");
+  if (!lengths || n == 0) return fail(S3H_EINVAL, "batch_host: bad arguments");
   for (int a = 0; a < nalgo; ++a)
     if (!digests[a]) return fail(S3H_EINVAL, "batch_host: null digest array");
   int count = 0;
   if (int rc = s3h_device_count(&count)) return rc;
   if (ndevices <= 0 || ndevices > count) ndevices = count;
+  if (ndevices > int(n)) ndevices = int(n);
   if (slice_bytes % 64) return fail(S3H_EINVAL, "slice_bytes must be a multiple of 64");
-  for (uint64_t i = 0; i < n; ++i)
-    if (!parts[i] && lengths[i]) return fail(S3H_EINVAL, "batch_host: part %llu is null", (unsigned long long)i);
+  if (src.parts)
+    for (uint64_t i = 0; i < n; ++i)
+      if (!src.parts[i] && lengths[i]) return fail(S3H_EINVAL, "batch_host: part %llu is null", (unsigned long long)i);
   std::vector<HostShard> shards(ndevices);
   for (int d = 0; d < ndevices; ++d) shards[d] = {d, ndevices, {}};
   for (uint64_t i = 0; i < n; ++i) shards[i % ndevices].parts.push_back(i);
   std::vector<int> rcs(ndevices, S3H_OK);
   std::vector<std::string> errs(ndevices);
-  std::vector<std::thread> pool;
-  for (int d = 0; d < ndevices; ++d)
-    pool.emplace_back([&, d] {
-      rcs[d] = run_host_shard(shards[d], algos, nalgo, parts, lengths, digests, slice_bytes);
-      if (rcs[d]) errs[d] = g_err;
-    });
-  for (auto& t : pool) t.join();
+  auto run = [&](int d) {
+    HostCtx* C = host_ctx_cache().acquire(d);
+    rcs[d] = run_host_shard(*C, shards[d], algos, nalgo, src, lengths, digests, slice_bytes);
+    if (rcs[d]) errs[d] = g_err;
+    host_ctx_cache().release(C, rcs[d] == S3H_OK);
+  };
+  if (ndevices == 1) {
+    run(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (int d = 0; d < ndevices; ++d) pool.emplace_back(run, d);
+    for (auto& t : pool) t.join();
+  }
   for (int d = 0; d < ndevices; ++d)
     if (rcs[d]) return fail(rcs[d], "device %d: %s", d, errs[d].c_str());
   return S3H_OK;
@@ -1080,8 +1066,11 @@ static int batch_host(const int* algos, int nalgo, const uint8_t* const* parts,
 
 static int batch_host(int algo, const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
                       uint32_t* digests, int ndevices, uint64_t slice_bytes) {
+  if (!parts) return fail(S3H_EINVAL, "batch_host: null parts");
   uint32_t* const out[1] = {digests};
-  return batch_host(&algo, 1, parts, lengths, n, out, ndevices, slice_bytes);
+  PartSource src;
+  src.parts = parts;
+  return batch_host(&algo, 1, src, lengths, n, out, ndevices, slice_bytes);
 }
 
 int s3h_sha256_batch_host(const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
@@ -1099,7 +1088,26 @@ int s3h_sha256_md5_batch_host(const uint8_t* const* parts, const uint64_t* lengt
                               uint64_t slice_bytes) {
   static const int algos[2] = {S3H_ALGO_SHA256, S3H_ALGO_MD5};
   uint32_t* const out[2] = {sha256_digests, md5_digests};
-  return batch_host(algos, 2, parts, lengths, n, out, ndevices, slice_bytes);
+  if (!parts) return fail(S3H_EINVAL, "batch_host: null parts");
+  PartSource src;
+  src.parts = parts;
+  return batch_host(algos, 2, src, lengths, n, out, ndevices, slice_bytes);
+}
+
+int s3h_sha256_file_parts(const char* path, const uint64_t* offsets, const uint64_t* lengths,
+                          uint64_t n, uint32_t* digests, int ndevices, uint64_t slice_bytes) {
+  if (!path || !offsets || !lengths || !digests || n == 0)
+    return fail(S3H_EINVAL, "file_parts: bad arguments");
+  const int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return fail(S3H_EINVAL, "file_parts: cannot open %s: %s", path, std::strerror(errno));
+  PartSource src;
+  src.fd = fd;
+  src.file_off = offsets;
+  static const int algo = S3H_ALGO_SHA256;
+  uint32_t* const out[1] = {digests};
+  const int rc = batch_host(&algo, 1, src, lengths, n, out, ndevices, slice_bytes);
+  close(fd);
+  return rc;
 }
 
 int s3h_sha256_md5_batch_device(int device, const void* d_base, const uint64_t* offsets,

@@ -35,8 +35,6 @@ namespace s3h {
 // LaunchArgs::flags
 constexpr uint32_t kNoPad = 1;   // hash only the slot's whole 64-B blocks; never pad or emit
 constexpr uint32_t kResume = 2;  // load the chaining state even at blk_begin == 0
-constexpr uint32_t kPrioNone = 4;  // experiment (S3H_PRIO=1): consumers keep priority 0
-constexpr uint32_t kPrioAll = 8;   // experiment (S3H_PRIO=2): producer raises priority too
 
 struct LaunchArgs {
   const uint8_t* base;       // part p's block b is at base + slots[p].off + 64*(b - blk_origin)
@@ -471,16 +469,14 @@ constexpr int kQuadChainsPerWave = 8;
 #define S3H_Q16(S, NX) S3H_QG(S, 0, S##0, 1) S3H_QG(S, 1, S##0, 2) S3H_QG(S, 2, S##0, 3) S3H_QG(S, 3, NX, 0)
 #define S3H_Q16_FIRST S3H_QG_FIRST S3H_QG(a, 1, a0, 2) S3H_QG(a, 2, a0, 3) S3H_QG(a, 3, b0, 0)
 
-template <int NC, int SH = 0, int BPS = 0>
-__global__ __launch_bounds__(64 * (NC * (1 + SH) + 1)) void sha256_quad_kernel(LaunchArgs A) {
-  // SH = 1: every consumer wave has a SHADOW wave (wave + NC) running the identical
-  // instruction stream on the same chains, output discarded (issue-rate experiment).
+template <int NC>
+__global__ __launch_bounds__(64 * (NC + 1)) void sha256_quad_kernel(LaunchArgs A) {
   constexpr uint32_t kParts = kQuadChainsPerWave * NC;
-  constexpr uint32_t kProducer = NC * (1 + SH);
+  constexpr uint32_t kProducer = NC;
   // Blocks per step: the producer's 64 lanes each make one (part, block) per step, so a step
   // covers 64 / kParts blocks (8 at NC = 1) for the same producer issue time, and the
   // consumers pass one barrier per step instead of one per 2 blocks.
-  constexpr uint32_t kBps = BPS ? BPS : 64 / kParts >= 2 ? 64 / kParts : 2;
+  constexpr uint32_t kBps = 64 / kParts >= 2 ? 64 / kParts : 2;
   constexpr uint32_t kLanes = kParts * kBps;  // producer lanes with distinct work (<= 64)
   __shared__ uint4 lds_wk[2][kBps][16][kParts];  // [buffer][block in step][row][part]
 
@@ -496,7 +492,6 @@ __global__ __launch_bounds__(64 * (NC * (1 + SH) + 1)) void sha256_quad_kernel(L
 
   if (wave == kProducer) {
     // ---------------------------------------------------------------- producer
-    if (A.flags & kPrioAll) __builtin_amdgcn_s_setprio(3);
     // Lane = (part, block h of the step): consecutive lanes take consecutive blocks of one
     // part (coalesced 64*kBps-byte runs).  Lanes >= kLanes repeat lanes 0.. (same loads, same
     // LDS writes), which keeps every lane on one branch-free path at no extra issue cost.
@@ -531,9 +526,8 @@ __global__ __launch_bounds__(64 * (NC * (1 + SH) + 1)) void sha256_quad_kernel(L
     }
   } else {
     // ---------------------------------------------------------------- consumer
-    if (!(A.flags & kPrioNone)) __builtin_amdgcn_s_setprio(3);
-    const uint32_t cw = wave % NC;  // chain group (a shadow wave repeats wave cw's chains)
-    const uint32_t part = kQuadChainsPerWave * cw + (lane >> 4) * 2u + ((lane >> 3) & 1u);
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t part = kQuadChainsPerWave * wave + (lane >> 4) * 2u + ((lane >> 3) & 1u);
     const bool ahalf = (lane >> 2) & 1u;
     const uint32_t k4 = lane & 3u;
     const uint32_t slot = slot0 + part;
@@ -609,7 +603,7 @@ __global__ __launch_bounds__(64 * (NC * (1 + SH) + 1)) void sha256_quad_kernel(L
       }
       __syncthreads();
     }
-    if (valid && nb > b0 && k4 == 0 && wave < NC) {
+    if (valid && nb > b0 && k4 == 0) {
       if (emits(A, nb)) {
         uint4* o = reinterpret_cast<uint4*>(A.digests + 8ull * A.out_idx[slot] + w0);
         o[0] = make_uint4(bswap(s0), bswap(s1), bswap(s2), bswap(s3));
@@ -740,7 +734,7 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t bl
     return;
   }
   // ------------------------------------------------------------------ consumer
-  if (!(A.flags & kPrioNone)) __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(3);
   const bool ahalf = (lane >> 2) & 1u;
   const uint32_t k4 = lane & 3u;
   // quad: lanes 8c..8c+7 = chain c; pair: half-row h holds chains 4h..4h+3 (e-lane k, a-lane 7-k)

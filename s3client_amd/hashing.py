@@ -17,6 +17,7 @@ the HIP kernels in s3client_amd/csrc.  Nothing here falls back to the CPU for a 
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Iterable, Sequence
 
 import numpy as np
@@ -330,6 +331,26 @@ class Stream:
 def sha256_batch_host(parts: Sequence, ndevices: int = 0, slice_bytes: int = 0) -> np.ndarray:
     """Digest host-resident parts (bytes / numpy uint8 arrays) on the GPUs: (n, 8) uint32."""
     return _host_batch(lib().s3h_sha256_batch_host, DIGEST_WORDS, parts, ndevices, slice_bytes)
+
+
+def sha256_file_parts(path: str, offsets, lengths, ndevices: int = 0,
+                      slice_bytes: int = 0) -> np.ndarray:
+    """Digests of byte ranges [offsets[i], offsets[i]+lengths[i]) of a file, read by host
+    threads straight into the pinned staging ring (s3h_sha256_file_parts): the (file, offset,
+    size) parts of S3Api::UploadFilePart.  (n, 8) uint32."""
+    offs, lens = _u64(offsets), _u64(lengths)
+    if offs.shape != lens.shape or offs.ndim != 1 or offs.size == 0:
+        raise ValueError("offsets and lengths must be 1-D, equal length and non-empty")
+    out = np.zeros((offs.size, DIGEST_WORDS), dtype=np.uint32)
+    check(lib().s3h_sha256_file_parts(os.fsencode(path), _p64(offs), _p64(lens), offs.size,
+                                      out.ctypes.data, ndevices, slice_bytes))
+    return out
+
+
+def trim() -> None:
+    """Free the host path's cached per-device buffers (HBM ring, pinned staging, plans):
+    s3h_trim.  A process that shares the GPU with other work calls this when it is done."""
+    check(lib().s3h_trim())
 
 
 def generate_parts(data, offsets, lengths, part_ids, seed: int, stream=None) -> None:

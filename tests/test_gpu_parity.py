@@ -280,8 +280,7 @@ def test_quad_two_consumer_waves_ragged(torch_cuda, oracle, kernel):
     rng = np.random.default_rng(31)
     n = 3000
     plan = s3.Plan([0] * n, [1] * n, kernel=kernel)
-    if "S3H_QUAD_WAVES" not in os.environ:  # sweeps force the consumer-wave count
-        assert plan.info()["grid"] == (n + 15) // 16
+    assert plan.info()["grid"] == (n + 15) // 16
     lens = rng.integers(0, 9000, n)
     lens[:4] = [0, 55, 56, 64]
     offs = np.concatenate([[0], np.cumsum(lens + rng.integers(0, 5, n))[:-1]])
