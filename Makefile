@@ -15,9 +15,16 @@ LIB := $(LIBDIR)/libs3hash.so
 
 all: $(LIB) oracle cpptests
 
-$(LIBDIR)/capi.o: $(CSRC)/capi.hip $(CSRC)/sha256_kernels.hip $(CSRC)/sha256_device.hpp $(CSRC)/sha256_skew_rounds.inc include/s3hash.h
-	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+# The device code object is kept (build/isa, -save-temps) and the chain-loop instruction counts
+# bench.py reports are derived from its disassembly (tools/isa_counts.py ->
+# s3client_amd/kernel_isa_counts.json).
+OBJDUMP ?= /opt/rocm/lib/llvm/bin/llvm-objdump
+ISA_DIS := build/isa/capi_gfx950.dis
+$(LIBDIR)/capi.o: $(CSRC)/capi.hip $(CSRC)/sha256_kernels.hip $(CSRC)/sha256_device.hpp $(CSRC)/sha256_skew_rounds.inc include/s3hash.h tools/isa_counts.py
+	@mkdir -p $(LIBDIR) build/isa
+	cd build/isa && $(HIPCC) $(HIPFLAGS) -save-temps -c -o ../../$@ ../../$<
+	$(OBJDUMP) -d --symbolize-operands build/isa/capi-hip-amdgcn-amd-amdhsa-gfx950.o > $(ISA_DIS)
+	python3 tools/isa_counts.py $(ISA_DIS) s3client_amd/kernel_isa_counts.json
 
 $(LIBDIR)/lib_hash.o: $(CSRC)/cpu/lib_hash.cpp include/sha256.h include/utility.h include/s3hash.h
 	@mkdir -p $(LIBDIR)
@@ -50,9 +57,7 @@ tests/cpp/build/sign_test: tests/cpp/sign_test.cpp s3client_amd/host/aws_sign.cp
 	$(CXX) -O2 -std=c++17 -Iinclude -Is3client_amd/host -o $@ $< s3client_amd/host/aws_sign.cpp \
 	    -L$(LIBDIR) -ls3hash -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)'
 
-isa: $(CSRC)/capi.hip
-	@mkdir -p build/isa
-	cd build/isa && $(HIPCC) $(HIPFLAGS) -c -save-temps -o capi.o ../../$(CSRC)/capi.hip
+isa: $(LIBDIR)/capi.o
 
 clean:
 	rm -rf $(LIBDIR) tests/cpp/build apps/build build

@@ -31,11 +31,23 @@ MIB = 1 << 20
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 CLOCK_GHZ = 2.4                 # MI355X peak engine clock (used when no clock probe ran)
 ISSUE_FLOOR_CPI = 4.0           # one wave: <= 1 instruction per 4 cycles (MI355X_MICROARCH.md)
-# Instructions one chain's wave issues per 64-B block (ISA audit of the consumer loop:
-# `make isa` + llvm-objdump; skew = 523 VALU + 16 ds_read_b128 + 2 s_waitcnt + ~2 alignment
-# s_nop + loop control; pair = 640 round VALU + bookkeeping + 16 ds_read_b128).  A wave issues
-# at most one instruction per ~4 cycles: this, not HBM, bounds each part's chain.
-CHAIN_INSTR_PER_BLOCK = {"skew": 544, "skewp": 608, "quad": 592, "pair": 672, "pc": 923, "lane": 1425, "md5-pc": 280}
+# Instructions one chain's wave issues per 64-B block.  A wave issues at most one instruction
+# per ~4 cycles: this, not HBM, bounds each part's chain.  The AUTO kernels' counts come from
+# the shipped code object (make -> tools/isa_counts.py -> s3client_amd/kernel_isa_counts.json:
+# the consumer's unrolled fast loop in the llvm-objdump disassembly / blocks per step); the
+# rest are round-1 hand counts of their multi-block loops.
+HAND_INSTR_PER_BLOCK = {"quad": 592, "pair": 672, "pc": 923, "lane": 1425, "md5-pc": 280}
+
+
+def chain_instr_per_block(kname: str, quad_waves: int):
+    """(instructions per block, source) for the kernel a plan runs."""
+    key = "skew_nc2" if kname == "skew" and quad_waves == 2 else kname
+    try:
+        with open(os.path.join(ROOT, "s3client_amd", "kernel_isa_counts.json")) as f:
+            k = json.load(f)["kernels"][key]
+        return k["instr_per_block"], f"code object ({k['symbol']} loop {k['loop_label']})"
+    except (OSError, KeyError):
+        return HAND_INSTR_PER_BLOCK[kname], "round-1 hand count"
 
 
 def parse():
@@ -49,7 +61,7 @@ def parse():
     ap.add_argument("--kernel", default="auto", choices=["auto", "skew", "skewp", "quad", "pair", "pc", "lane"])
     ap.add_argument("--algo", default="sha256", choices=["sha256", "md5"],
                     help="md5: the SURVEY 8(f) Content-MD5/ETag kernel (not the metric)")
-    ap.add_argument("--cpu-sample-parts", type=int, default=384)
+    ap.add_argument("--cpu-sample-parts", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--slice-bytes", type=int, default=0, help="host mode: bytes per part per slice")
     ap.add_argument("--mode", default="device",
@@ -58,6 +70,10 @@ def parse():
                          "appended chunk by chunk through s3h_stream_*; dual / host-dual: "
                          "SHA-256 + MD5 of every part in one pass (none of these is the metric)")
     ap.add_argument("--chunk-bytes", type=int, default=MIB, help="stream mode: bytes per append")
+    ap.add_argument("--no-host-resident", action="store_true",
+                    help="skip the H2D-inclusive sub-measurement of the default C2 line")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="skip the BASELINE config-4 sub-measurement of multi-GPU runs")
     return ap.parse_args()
 
 
@@ -101,20 +117,55 @@ def pmc_traffic(cfg: str, kernel: str, algo_bytes: float):
     return int(round(ratio * algo_bytes)), os.path.relpath(files[-1], ROOT)
 
 
+def _cgroup_cpu_quota():
+    """CPUs this container may use per the cgroup v2/v1 quota (None: unlimited/unknown)."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else round(q / per, 2)
+    except Exception:
+        return None
+
+
+def _cpu_baseline_lib():
+    """oracle/cpu_baseline.c (lib/hash's cost structure) built HERE with the reference's release
+    flags -Ofast -march=native -flto (lib/CMakeLists.txt:45); the prebuilt portable
+    oracle/libcpubase.so (-march=x86-64-v3) if no compiler is usable."""
+    import tempfile
+    src = os.path.join(ROOT, "oracle", "cpu_baseline.c")
+    out = os.path.join(tempfile.mkdtemp(prefix="s3h_cpubase_"), "libcpubase_native.so")
+    flags = "-Ofast -march=native -flto -DNDEBUG"
+    try:
+        import subprocess
+        subprocess.run(["gcc", "-std=gnu11", *flags.split(), "-fPIC", "-shared", "-pthread",
+                        "-o", out, src], check=True, capture_output=True, timeout=120)
+        return out, flags
+    except Exception:
+        return os.path.join(ROOT, "oracle", "libcpubase.so"), "-Ofast -march=x86-64-v3 -flto (prebuilt)"
+
+
 def cpu_baseline(host: np.ndarray, offs, lens, gpu_digests: np.ndarray, nsample: int,
                  algo: str = "sha256"):
-    """lib/hash timed on this host's cores over a bounded sample of the same parts.  MD5: the
-    reference has no padded in-memory md5 (md5.cpp:119-122), so the oracle port is timed."""
-    from tests.oracle_lib import REF_SO, ORACLE_SO, u64p
-    kind = "reference" if os.path.exists(REF_SO) and algo == "sha256" else "port"
-    L = ctypes.CDLL(REF_SO if kind == "reference" else ORACLE_SO)
+    """lib/hash's sha256::sha256 cost structure (oracle/cpu_baseline.c, calibrated against the
+    real lib/hash: profiles/r02_cpu_baseline_calibration.json) timed on this host's cores over
+    the same parts as the GPU: one thread per available CPU (sched_getaffinity), parts
+    round-robin, plus a 1-thread figure.  MD5: the oracle port (the reference has no padded
+    in-memory md5, md5.cpp:119-122)."""
+    from tests.oracle_lib import ORACLE_SO, u64p
     if algo == "md5":
-        fn = L.oracle_md5_batch
+        path, flags = ORACLE_SO, "-O2 (oracle)"
+        fn = ctypes.CDLL(path).oracle_md5_batch
     else:
-        fn = L.ref_sha256_batch if kind == "reference" else L.oracle_sha256_batch
+        path, flags = _cpu_baseline_lib()
+        fn = ctypes.CDLL(path).base_sha256_batch
     words = 4 if algo == "md5" else 8
     fn.argtypes = [ctypes.c_void_p, u64p, u64p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
-    threads = int(os.environ.get("S3H_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    threads = int(os.environ.get("S3H_CPU_THREADS", len(os.sched_getaffinity(0))))
     n = min(nsample, len(lens))
     o = np.ascontiguousarray(offs[:n], dtype=np.uint64)
     ln = np.ascontiguousarray(lens[:n], dtype=np.uint64)
@@ -122,7 +173,7 @@ def cpu_baseline(host: np.ndarray, offs, lens, gpu_digests: np.ndarray, nsample:
     t0 = time.perf_counter()
     fn(host.ctypes.data, o.ctypes.data_as(u64p), ln.ctypes.data_as(u64p), n, out.ctypes.data, threads)
     dt = time.perf_counter() - t0
-    n1 = min(8, n)
+    n1 = min(16, n)
     out1 = np.zeros((n1, words), dtype=np.uint32)
     t1 = time.perf_counter()
     fn(host.ctypes.data, o.ctypes.data_as(u64p), ln.ctypes.data_as(u64p), n1, out1.ctypes.data, 1)
@@ -135,11 +186,15 @@ def cpu_baseline(host: np.ndarray, offs, lens, gpu_digests: np.ndarray, nsample:
     except Exception:
         pass
     gib = float(ln.sum()) / 2**30
-    return {"value": round(gib / dt, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "sample": f"{n} of the bench's parts ({gib:.2f} GiB) with "
-                      f"{'lib/hash sha256::sha256' if kind == 'reference' else 'the oracle port (' + algo + ')'}"
-                      f" on {threads} threads, round-robin; same bytes as the GPU",
+    return {"value": round(gib / dt, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{n} of the bench's parts ({gib:.2f} GiB, the same bytes as the GPU) with "
+                      f"{'oracle/cpu_baseline.c (lib/hash sha256::sha256 cost structure)' if algo == 'sha256' else 'the oracle MD5 port'}"
+                      f" on {threads} threads (one per CPU in sched_getaffinity), parts round-robin",
+            "build_flags": flags, "cgroup_cpu_quota": _cgroup_cpu_quota(),
             "single_thread_GiBps": round(float(ln[:n1].sum()) / 2**30 / dt1, 3),
+            "single_thread_sample": f"{n1} parts",
+            "calibration": "restatement / real lib/hash = 0.93-1.01 (1 thread, -march=native, "
+                           "profiles/r02_cpu_baseline_calibration.json)",
             "cpu_model": cpu_model, "digests_match_gpu": parity}
 
 
@@ -264,9 +319,10 @@ def main():
     else:
         cyc_per_block = kern_ms / 1e3 * CLOCK_GHZ * 1e9 / info["max_blocks"]
         clock_src = f"kernel time x assumed {CLOCK_GHZ} GHz"
-    cpi = cyc_per_block / CHAIN_INSTR_PER_BLOCK[kname]
+    ipb, ipb_src = chain_instr_per_block(kname, 2 if (kname == "skew" and len(lens) > 2048) else 1)
+    cpi = cyc_per_block / ipb
     issue = {"bound": "per-wave instruction issue of each part's sequential chain",
-             "chain_instr_per_block": CHAIN_INSTR_PER_BLOCK[kname],
+             "chain_instr_per_block": ipb, "chain_instr_source": ipb_src,
              "cycles_per_block": round(cyc_per_block, 1), "cycles_source": clock_src,
              "cycles_per_instr": round(cpi, 3),
              # floor: one wave issues at most one instruction per 4 cycles (MI355X_MICROARCH.md
@@ -277,7 +333,7 @@ def main():
              "clock_GHz": probe["clock_GHz"] if probe else CLOCK_GHZ,
              # chip-wide INT32-VALU roof (256 CU x 64 lanes x clock / VALU per
              # block of the one-lane-per-part kernel x 64 B) and the parallelism ceiling
-             "valu_roof_GBps": round(256 * 64 * CLOCK_GHZ * 1e9 / CHAIN_INSTR_PER_BLOCK["lane"]
+             "valu_roof_GBps": round(256 * 64 * CLOCK_GHZ * 1e9 / HAND_INSTR_PER_BLOCK["lane"]
                                      * 64 / 1e9, 1),
              "parallelism_ceiling": round(min(len(lens), 65536) / 65536, 5)}
 
@@ -307,15 +363,105 @@ def main():
                          "lanes_occupied_frac": round(min(len(lens), 65536) / 65536, 5)},
             "issue": issue,
         }
+        if (world == 1 and args.config == "c2" and args.algo == "sha256" and not args.parts_per_gpu
+                and not args.part_bytes and not args.no_host_resident):
+            line["host_resident"] = host_resident(s3, torch, data, ids, lens, offs, gd)
         if world == 1 and not args.no_cpu_baseline:
             n = min(args.cpu_sample_parts, len(lens))
             end = int(offs[n - 1] + lens[n - 1])
             host = data[:end].cpu().numpy()
             line["cpu_baseline"] = cpu_baseline(host, offs, lens, gd, n, args.algo)
+    c4 = None
+    if world > 1 and args.config == "c2" and args.algo == "sha256" and not args.no_c4:
+        del data, digests
+        plan.close()
+        torch.cuda.empty_cache()
+        c4 = c4_shard(args, s3, torch, dist, dev, rank, world, local, backend)
+    if rank == 0:
+        if c4 is not None:
+            line["c4"] = c4
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def host_resident(s3, torch, data, ids, lens, offs, gd, reps: int = 3):
+    """The same C2 batch starting and ending in HOST memory (H2D included): the parts are
+    copied once into pinned memory (outside the timed region), then s3h_sha256_batch_host
+    streams them through the HBM ring and returns the digests to the host."""
+    end = int(offs[-1] + lens[-1])
+    host = torch.empty(end, dtype=torch.uint8, pin_memory=True)
+    host.copy_(data[:end])
+    h = host.numpy()
+    views = [h[int(o):int(o) + int(L)] for o, L in zip(offs, lens)]
+    out = s3.sha256_batch_host(views, ndevices=1)  # warm: the per-device context is cached
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = s3.sha256_batch_host(views, ndevices=1)
+        times.append(time.perf_counter() - t0)
+    gib = float(lens.sum()) / 2**30
+    res = {"metric": "host-resident (H2D-inclusive) SHA-256 GiB/s, same C2 parts",
+           "value": round(gib / float(np.mean(times)), 3), "best": round(gib / min(times), 3),
+           "unit": "GiB/s", "ms_per_batch": round(1e3 * float(np.mean(times)), 2), "reps": reps,
+           "path": "pinned host parts -> 3-slot HBM ring (one 2-D H2D copy per 256 KiB slice) -> "
+                   "skew kernel per slice -> digests D2H (s3h_sha256_batch_host)",
+           "fixture_mismatches": _fixture_mismatches(s3, ids, out),
+           "digests_match_device_run": bool(np.array_equal(out, gd))}
+    del host, h, views
+    return res
+
+
+def c4_shard(args, s3, torch, dist, dev, rank, world, local, backend, steps: int = 3):
+    """BASELINE config 4 beside the C2 headline of a multi-GPU run: 8,192 x 8 MiB per GPU,
+    global part p on rank p % N (65,536 parts = 512 GiB at N = 8), no collective on the data
+    path; per-GPU and aggregate GiB/s with the max-over-ranks time."""
+    from s3client_amd.shard import shard_ids
+    per, L = 8192, 8 * MIB
+    ids = shard_ids(per * world, rank, world)
+    lens = np.full(per, L, dtype=np.uint64)
+    offs = np.arange(per, dtype=np.uint64) * np.uint64(L)
+    data = torch.empty(per * L, dtype=torch.uint8, device=dev)
+    s3.generate_parts(data, offs, lens, ids, SEED)
+    stream = torch.cuda.current_stream(dev)
+    plan = s3.Plan(offs, lens, device=local)
+    out = torch.zeros((per, 8), dtype=torch.int32, device=dev)
+    plan.launch(data, out, stream)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        plan.launch(data, out, stream)
+    torch.cuda.synchronize(dev)
+    mine = time.perf_counter() - t0
+    dist.barrier()
+    wall = time.perf_counter() - t0
+    tt = torch.tensor([mine], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    allt = [torch.zeros_like(tt) for _ in range(world)]
+    dist.all_gather(allt, tt)
+    per_rank = [float(x[0]) for x in allt]
+    gd = out.cpu().numpy().view(np.uint32)
+    with open(os.path.join(ROOT, "tests", "golden", "sha256_golden.json")) as f:
+        gold = json.load(f)
+    fx = {e["p"]: e["digest"] for e in gold["c2_parts"] + gold["c4_parts"]}
+    bad = sum(s3.hash_to_text(gd[k]) != fx[int(p)] for k, p in enumerate(ids) if int(p) in fx)
+    badt = torch.tensor([bad, sum(int(p) in fx for p in ids)], dtype=torch.int64,
+                        device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(badt)
+    kernel = plan.info()["kernel"]
+    plan.close()
+    del data, out
+    torch.cuda.empty_cache()
+    gib_gpu = per * L * steps / 2**30
+    return {"workload": f"C4: {per} x 8 MiB per GPU, {per * world} parts over {world} GPUs "
+                        "(part p on rank p % N)",
+            "kernel": kernel, "steps": steps,
+            "per_gpu_GiBps": [round(gib_gpu / t, 3) for t in per_rank],
+            "aggregate_GiBps": round(gib_gpu * world / max(max(per_rank), wall), 3),
+            "ms_per_step_max_rank": round(1e3 * max(per_rank) / steps, 3),
+            "parity": {"fixtures_checked": int(badt[1]), "mismatches": int(badt[0])}}
 
 
 def host_mode(args, s3, torch, dist, data, ids, lens, offs, world, rank, name):

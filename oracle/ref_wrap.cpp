@@ -3,8 +3,9 @@
 // extern "C" shims over the REAL reference lib/hash (compiled from /root/reference by
 // oracle/Makefile into oracle/_ref/libref_hash.so).  No reference source is copied: this
 // file only calls the reference's own symbols.  Used (a) by tests/golden/gen_golden.py to
-// produce the committed fixtures and (b) by bench.py's cpu_baseline leg as the
-// "reference" CPU baseline (lib/hash's sha256::sha256 timed on the host cores).
+// produce the committed fixtures, (b) by tests/test_ref_differential.py and (c) by
+// tools/calibrate_cpu_baseline.py to calibrate oracle/cpu_baseline.c against the real lib/hash
+// (all in the build container: oracle/_ref never travels to the GPU box).
 #include <cstdint>
 #include <cstddef>
 #include <thread>

@@ -6,7 +6,8 @@ from .hashing import (Plan, device_count, digests_to_text, generate_parts, hash_
                       hmac256, nblocks, sha256, sha256_batch_device, sha256_batch_host,
                       cpu_backend, md5, md5_batch_device, md5_batch_host, multipart_etag,
                       verify_batch_device, verify_batch_host, Stream,
-                      sha256_md5_batch_device, sha256_md5_batch_host)
+                      sha256_md5_batch_device, sha256_md5_batch_host, sha256_file_parts,
+                      trim)
 from .upload import upload_parts_geometry, UploadPart
 from ._native import S3HashError, LIB_PATH
 
@@ -14,5 +15,5 @@ __all__ = ["Plan", "device_count", "digests_to_text", "generate_parts", "hash_to
            "hmac256", "nblocks", "sha256", "sha256_batch_device", "sha256_batch_host",
            "cpu_backend", "md5", "md5_batch_device", "md5_batch_host", "multipart_etag",
            "verify_batch_device", "verify_batch_host", "Stream",
-           "sha256_md5_batch_device", "sha256_md5_batch_host",
+           "sha256_md5_batch_device", "sha256_md5_batch_host", "sha256_file_parts", "trim",
            "upload_parts_geometry", "UploadPart", "S3HashError", "LIB_PATH"]

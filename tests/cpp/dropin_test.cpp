@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <algorithm>
 #include <cstring>
+#include <future>
 #include <string>
 #include <vector>
 
@@ -165,6 +166,61 @@ int main(int argc, char** argv) {
     bool sok = true;
     for (size_t i = 0; i < msgs.size(); ++i) sok &= sh[i] == digest(msgs[i]);
     report("gpu stream_batch", sok);
+
+    // Concurrent callers in the shape of lib/src/upload.cpp:89-110 + 136-140: the transfer
+    // test's object (test/parallel-file-transfer-test.cpp:50-59, bytes i % 128) sliced into
+    // 3 jobs x 2 parts; each job is a std::async thread that hashes ITS parts with its own
+    // batch call while the others do (the device's cached host context goes to one of them,
+    // the rest build private ones), plus a fourth job hashing the same parts from a file.
+    {
+      const uint64_t size = 38000007;
+      std::vector<uint8_t> obj(size);
+      for (uint64_t i = 0; i < size; ++i) obj[i] = uint8_t(i % 128);
+      const char* want[6] = {
+          "6dcb77e2b805f5cf4962377e29401180e87ee214d469a71d2c9b14f7a99cc52c",
+          "f9b1736fa43ac57591e39848316506aa821605e047ba754955d58cd322a3ea35",
+          "61da16a2a47588d0ce1395076a3d238235bd76001af269e378b2b74fb9777776",
+          "f8ebaab206806551bcb184b6626cbabb017ab968c5c34db7231fa548fbbb94a3",
+          "272da9db8caf86bf7e463fca5f7b002dd158eaa49b6f992b41e3593f37ff95fb",
+          "0aa12676f0770a0be4618bb2992d5e48ebef5c4858965bb8f3f2ee417ffbc1cb"};
+      std::vector<uint64_t> offs, lens;  // upload.cpp:98-107 + :133
+      const uint64_t per_job = (size + 2) / 3;
+      for (int j = 0; j < 3; ++j) {
+        uint64_t off = j * per_job;
+        const uint64_t chunk = std::min(per_job, size - off), psz = (chunk + 1) / 2;
+        for (int k = 0; k < 2; ++k) {
+          const uint64_t sz = std::min(psz, chunk - k * psz);
+          offs.push_back(off);
+          lens.push_back(sz);
+          off += sz;
+        }
+      }
+      const std::string path = "/tmp/s3h_dropin_xfer.bin";
+      FILE* f = std::fopen(path.c_str(), "wb");
+      std::fwrite(obj.data(), 1, size, f);
+      std::fclose(f);
+      bool cok = true;
+      for (int rep = 0; rep < 3 && cok; ++rep) {
+        std::vector<std::future<std::vector<std::string>>> jobs;
+        for (int j = 0; j < 3; ++j)
+          jobs.push_back(std::async(std::launch::async, [&, j] {
+            return sha256::payload_hashes({obj.data() + offs[2 * j], obj.data() + offs[2 * j + 1]},
+                                          {lens[2 * j], lens[2 * j + 1]});
+          }));
+        auto file_job = std::async(std::launch::async, [&] {
+          return sha256::file_part_hashes(path, offs, lens);
+        });
+        for (int j = 0; j < 3; ++j) {
+          const auto h = jobs[j].get();
+          cok &= h.size() == 2 && h[0] == want[2 * j] && h[1] == want[2 * j + 1];
+        }
+        const auto fh = file_job.get();
+        for (int i = 0; i < 6; ++i) cok &= fh[i] == want[i];
+      }
+      std::remove(path.c_str());
+      report("gpu concurrent jobs", cok);
+    }
+    sha256::trim();
   }
   return fails ? 1 : 0;
 }

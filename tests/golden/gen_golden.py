@@ -114,11 +114,18 @@ def main():
     ps = list(range(16)) + [511, 1022, 1023]
     out["c2_parts"] = [{"p": p, "L": L8, "digest": ref_digest(ref, gen(orc, p, L8))} for p in ps]
 
-    # 4. C3 ragged lengths (first 64) + digests of a few whole C3 parts
-    c3 = [int(orc.oracle_c3_length(SEED, p)) for p in range(64)]
-    out["c3_lengths"] = c3
-    out["c3_parts"] = [{"p": p, "L": c3[p], "digest": ref_digest(ref, gen(orc, p, c3[p]))}
-                       for p in (0, 1)]
+    # 4. C3 ragged lengths (first 64) + digests of whole C3 parts: p 0, 1, the longest and the
+    #    shortest of the 4096, and four more spread over the batch (BASELINE configs[2])
+    c3all = [int(orc.oracle_c3_length(SEED, p)) for p in range(4096)]
+    out["c3_lengths"] = c3all[:64]
+    c3ids = [0, 1, int(np.argmax(c3all)), int(np.argmin(c3all)), 777, 2048, 3000, 4095]
+    out["c3_parts"] = [{"p": p, "L": c3all[p], "digest": ref_digest(ref, gen(orc, p, c3all[p]))}
+                       for p in c3ids]
+
+    # 4b. C4 (BASELINE configs[3]): 65536 x 8 MiB, part p on device p % 8.  Digests of parts of
+    #     rank 0's shard (p = 8k) beyond the C2 fixtures, incl. its first, middle and last parts.
+    out["c4_parts"] = [{"p": p, "L": 8 << 20, "digest": ref_digest(ref, gen(orc, p, 8 << 20))}
+                       for p in (8, 16, 4096, 32768, 65520, 65528)]
 
     # 5. test/parallel-file-transfer-test.cpp:50-59 data (i % 128, 38000007 B), parts sliced
     #    with lib/src/upload.cpp:98-107 geometry (3 jobs x 2 parts)

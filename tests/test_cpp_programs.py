@@ -39,6 +39,7 @@ def test_dropin_gpu_batch(programs):
     assert rc == 0, rows
     got = {r[1]: r[2] for r in rows}
     assert got["gpu batch payload_hashes"] == "1" and got["gpu stream_batch"] == "1", rows
+    assert got["gpu sha256_md5_batch"] == "1" and got["gpu concurrent jobs"] == "1", rows
 
 
 def _xfer_file(tmp_path, golden):
@@ -70,11 +71,38 @@ def test_upload_counterpart_cpu(programs, tmp_path, golden):
 
 
 @pytest.mark.gpu
-def test_upload_counterpart_gpu(programs, tmp_path, golden):
+@pytest.mark.parametrize("source", ["file", "mmap", "memory"])
+@pytest.mark.parametrize("per_job", [False, True])
+def test_upload_counterpart_gpu(programs, tmp_path, golden, source, per_job):
+    """UploadFile (file ranges / mmap) and UploadData (memory buffer) counterparts, one batch
+    call or one concurrent call per job: the transfer test's 3 jobs x 2 parts vs lib/hash."""
     path, t = _xfer_file(tmp_path, golden)
     app = os.path.join(ROOT, "apps", "build", "s3-upload-hash")
-    r = subprocess.run([app, "-f", path, "-j", "3", "-n", "2", "--verify"],
-                       capture_output=True, text=True, timeout=300)
+    cmd = [app, "-f", path, "-j", "3", "-n", "2", "--verify", "--source", source, "--print-headers"]
+    r = subprocess.run(cmd + (["--per-job"] if per_job else []), capture_output=True, text=True,
+                       timeout=300)
     assert r.returncode == 0, r.stderr
     rows = _parse_parts(r.stdout)
     assert [x[4] for x in rows] == [p["digest"] for p in t["parts"]]
+    heads = [l for l in r.stdout.splitlines() if " x-amz-content-sha256: " in l]
+    assert [h.split(": ")[-1] for h in heads] == [p["digest"] for p in t["parts"]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jobs,ppj", [(1, 3), (2, 1)])
+def test_upload_counterpart_memory_multipart(programs, tmp_path, golden, jobs, ppj):
+    """UploadData geometry of test/api/multipart-upload-test.cpp:47-54 (19,000,000 iota bytes in
+    3 or 2 chunks): the memory path forwards each part's digest into its signature (the
+    reference's DoUploadPart drops it, multipart_upload.cpp:131-136)."""
+    import numpy as np
+    mp = golden["multipart"]
+    path = tmp_path / "mp.bin"
+    (np.arange(mp["size"], dtype=np.uint64) % 256).astype(np.uint8).tofile(path)
+    app = os.path.join(ROOT, "apps", "build", "s3-upload-hash")
+    r = subprocess.run([app, "-f", str(path), "-j", str(jobs), "-n", str(ppj), "--source", "memory",
+                        "--per-job", "--print-headers"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    rows = _parse_parts(r.stdout)
+    want = [p for p in mp["parts"] if p["chunks"] == jobs * ppj]
+    assert [(int(x[2]), int(x[3]), x[4]) for x in rows] == [(p["offset"], p["size"], p["digest"]) for p in want]
+    assert "UNSIGNED-PAYLOAD" not in r.stdout

@@ -1,0 +1,91 @@
+"""BASELINE configs 3 and 4 at full size on one MI355X (pytest -m gpu).
+
+C3 (configs[2]): 4096 parts of U[5,64] MiB (~138 GiB resident in HBM), AUTO -> skew with two
+consumer waves per workgroup (grid 256).  C4 (configs[3]): rank 0's shard of 65,536 x 8 MiB over
+8 GPUs -- global parts p = 8k, 8,192 x 8 MiB = 64 GiB -- AUTO -> skewp.  Each batch is checked
+against (i) the lib/hash golden digests of the parts that have fixtures (tests/golden: C3 ids
+incl. the longest and shortest part, C4 ids of rank 0) and (ii) the oracle on 64 randomly
+chosen parts copied back from HBM.  Bar: bit-exact."""
+import numpy as np
+import pytest
+
+import s3client_amd as s3
+
+pytestmark = pytest.mark.gpu
+SEED = 20241008
+MIB = 1 << 20
+
+
+def _oracle_sample(torch, oracle, data, offs, lens, slots, threads=16):
+    """Oracle digests of the parts in `slots`, copied out of the device buffer."""
+    chunks = [data[int(offs[i]):int(offs[i]) + int(lens[i])].cpu().numpy() for i in slots]
+    host = np.concatenate(chunks)
+    so = np.concatenate([[0], np.cumsum([c.size for c in chunks])[:-1]]).astype(np.uint64)
+    return oracle.batch(host, so, [c.size for c in chunks], threads=threads)
+
+
+def _release(torch):
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def test_c3_full_ragged_batch(torch_cuda, oracle, golden):
+    torch = torch_cuda
+    n = 4096
+    lens = np.array([oracle.c3_length(p) for p in range(n)], dtype=np.uint64)
+    padded = (lens + np.uint64(255)) // np.uint64(256) * np.uint64(256)
+    offs = np.concatenate([[0], np.cumsum(padded)[:-1]]).astype(np.uint64)
+    total = int(offs[-1] + lens[-1]) + 256
+    assert 130 << 30 < total < 150 << 30  # ~138 GiB, BASELINE configs[2]
+    data = torch.empty(total, dtype=torch.uint8, device="cuda")
+    try:
+        s3.generate_parts(data, offs, lens, np.arange(n), SEED)
+        with s3.Plan(offs, lens) as plan:
+            info = plan.info()
+            assert info["kernel"] == "skew" and info["grid"] == 256, info
+            out = torch.empty((n, 8), dtype=torch.int32, device="cuda")
+            plan.launch(data, out)
+            torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint32)
+        txt = s3.digests_to_text(got)
+        fx = golden["c3_parts"]
+        assert {e["p"] for e in fx} >= {int(np.argmax(lens)), int(np.argmin(lens))}
+        for e in fx:
+            assert int(lens[e["p"]]) == e["L"] and txt[e["p"]] == e["digest"], e["p"]
+        rng = np.random.default_rng(303)
+        slots = np.sort(rng.choice(n, 64, replace=False))
+        assert np.array_equal(got[slots], _oracle_sample(torch, oracle, data, offs, lens, slots))
+    finally:
+        del data
+        _release(torch)
+
+
+def test_c4_rank0_shard(torch_cuda, oracle, golden):
+    torch = torch_cuda
+    world, rank, per = 8, 0, 8192
+    ids = np.arange(rank, per * world, world, dtype=np.uint64)       # global parts p % 8 == 0
+    from s3client_amd.shard import shard_ids
+    assert np.array_equal(ids, shard_ids(per * world, rank, world))
+    L = 8 * MIB
+    lens = np.full(per, L, dtype=np.uint64)
+    offs = np.arange(per, dtype=np.uint64) * np.uint64(L)
+    data = torch.empty(per * L, dtype=torch.uint8, device="cuda")     # 64 GiB
+    try:
+        s3.generate_parts(data, offs, lens, ids, SEED)
+        with s3.Plan(offs, lens) as plan:
+            assert plan.info()["kernel"] == "skewp"
+            out = torch.empty((per, 8), dtype=torch.int32, device="cuda")
+            plan.launch(data, out)
+            torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint32)
+        txt = s3.digests_to_text(got)
+        fx = [e for e in golden["c2_parts"] + golden["c4_parts"] if e["p"] % world == rank]
+        assert len(fx) >= 7
+        for e in fx:
+            assert txt[e["p"] // world] == e["digest"], e["p"]
+        rng = np.random.default_rng(404)
+        slots = np.sort(rng.choice(per, 64, replace=False))
+        assert np.array_equal(got[slots], _oracle_sample(torch, oracle, data, offs, lens, slots))
+    finally:
+        del data
+        _release(torch)

@@ -1,0 +1,144 @@
+"""Host-resident path (H2D included) under the conditions a real uploader creates: cached
+per-device contexts that grow and are trimmed, many pageable parts, concurrent callers, parts
+read from a file, and plans launched on two streams at once.  Every digest vs the oracle or
+the lib/hash goldens (bit-exact)."""
+import threading
+
+import numpy as np
+import pytest
+
+import s3client_amd as s3
+
+pytestmark = pytest.mark.gpu
+MIB = 1 << 20
+
+
+def _free(torch):
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return torch.cuda.mem_get_info()[0]
+
+
+def test_context_grows_keeps_small_ring_and_trims(torch_cuda, oracle):
+    """Small call, then a larger one (the cached ring and plans grow), then one whose HBM ring
+    exceeds the 1 GiB keep limit (freed when the call returns), then s3h_trim (all freed)."""
+    torch = torch_cuda
+    s3.trim()
+    free0 = _free(torch)
+    rng = np.random.default_rng(51)
+    small = [rng.integers(0, 256, int(L), dtype=np.uint8) for L in rng.integers(0, 5000, 64)]
+    assert np.array_equal(s3.sha256_batch_host(small),
+                          np.stack([oracle.sha256(p.tobytes()) for p in small]))
+    larger = [rng.integers(0, 256, int(L), dtype=np.uint8) for L in rng.integers(0, 300000, 1500)]
+    assert np.array_equal(s3.sha256_batch_host(larger),
+                          np.stack([oracle.sha256(p.tobytes()) for p in larger]))
+    kept = free0 - _free(torch)
+    assert 0 <= kept < 256 * MIB, kept           # small ring + plans stay cached
+    # pinned, non-uniform parts -> 2 MiB slices: ring = 3 x 200 x 2 MiB = 1.2 GiB > 1 GiB
+    pinned = torch.empty(200 * (2 * MIB + 64), dtype=torch.uint8, pin_memory=True)
+    h = pinned.numpy()
+    h[:] = rng.integers(0, 256, h.size, dtype=np.uint8)
+    views = [h[i * (2 * MIB + 64): i * (2 * MIB + 64) + 2 * MIB + (i % 7)] for i in range(200)]
+    want = oracle.batch(h, [i * (2 * MIB + 64) for i in range(200)], [v.size for v in views])
+    assert np.array_equal(s3.sha256_batch_host(views), want)
+    after_big = free0 - _free(torch)
+    assert after_big < 512 * MIB, after_big       # the 1.2 GiB ring was not kept
+    s3.trim()
+    trimmed = free0 - _free(torch)
+    assert trimmed < 64 * MIB, trimmed
+
+
+def test_pageable_parts_beyond_staging_slot_cap(torch_cuda, oracle):
+    """> 8,192 pageable parts: slices shrink below 4 KiB so the pinned staging slot stays at
+    32 MiB; > 524,288 parts: per-part pageable DMAs.  Both vs the oracle."""
+    rng = np.random.default_rng(52)
+    n = 10000
+    lens = rng.integers(0, 9000, n)
+    lens[:3] = [0, 55, 4097]
+    buf = rng.integers(0, 256, int(lens.sum()) + 64, dtype=np.uint8)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    views = [buf[o:o + L] for o, L in zip(offs, lens)]
+    assert np.array_equal(s3.sha256_batch_host(views), oracle.batch(buf, offs, lens))
+    n = 530000
+    lens = rng.integers(0, 40, n)
+    buf = rng.integers(0, 256, int(lens.sum()) + 64, dtype=np.uint8)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    views = [buf[o:o + L] for o, L in zip(offs, lens)]
+    got = s3.sha256_batch_host(views)
+    idx = rng.choice(n, 3000, replace=False)
+    assert np.array_equal(got[idx], oracle.batch(buf, offs[idx], lens[idx]))
+
+
+def test_concurrent_host_callers(torch_cuda, oracle, golden):
+    """Four threads hash at the same time (ctypes drops the GIL): one uses the device's cached
+    context, the others build private ones -- as upload.cpp:136-140 runs one std::async job per
+    part group.  Each thread's digests vs the transfer-test goldens / the oracle."""
+    t = golden["transfer"]
+    data = (np.arange(t["size"], dtype=np.uint64) % 128).astype(np.uint8)
+    views = [data[p["offset"]:p["offset"] + p["size"]] for p in t["parts"]]
+    want_x = [p["digest"] for p in t["parts"]]
+    rng = np.random.default_rng(53)
+    sets = [[rng.integers(0, 256, int(L), dtype=np.uint8) for L in rng.integers(0, 200000, 300)]
+            for _ in range(3)]
+    want_r = [np.stack([oracle.sha256(p.tobytes()) for p in s]) for s in sets]
+    errors, results = [], {}
+
+    def job(k):
+        try:
+            for _ in range(3):
+                if k == 0:
+                    results[k] = s3.digests_to_text(s3.sha256_batch_host(views))
+                else:
+                    results[k] = s3.sha256_batch_host(sets[k - 1])
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=job, args=(k,)) for k in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    assert results[0] == want_x
+    for k in range(1, 4):
+        assert np.array_equal(results[k], want_r[k - 1]), k
+
+
+def test_file_parts_transfer_geometry(torch_cuda, golden, tmp_path):
+    """s3h_sha256_file_parts: the transfer test's file, parts as (offset, size) ranges sliced by
+    lib/src/upload.cpp geometry (3 jobs x 2 parts), preads straight into pinned staging."""
+    t = golden["transfer"]
+    path = tmp_path / "xfer.bin"
+    (np.arange(t["size"], dtype=np.uint64) % 128).astype(np.uint8).tofile(path)
+    offs = [p["offset"] for p in t["parts"]]
+    sizes = [p["size"] for p in t["parts"]]
+    for sl in (0, 64 << 10):
+        got = s3.digests_to_text(s3.sha256_file_parts(str(path), offs, sizes, slice_bytes=sl))
+        assert got == [p["digest"] for p in t["parts"]], sl
+    with pytest.raises(s3.S3HashError):  # a part past the end of the file
+        s3.sha256_file_parts(str(path), [t["size"] - 10], [100])
+    with pytest.raises(s3.S3HashError):
+        s3.sha256_file_parts(str(tmp_path / "missing.bin"), [0], [1])
+
+
+def test_two_plans_on_two_streams(torch_cuda, oracle):
+    """Two device-resident plans launched concurrently on two torch streams."""
+    torch = torch_cuda
+    rng = np.random.default_rng(54)
+    bufs, plans, outs, wants = [], [], [], []
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for k, n in enumerate((1000, 6000)):
+        lens = rng.integers(0, 70000, n)
+        offs = np.concatenate([[0], np.cumsum(lens + 5)[:-1]])
+        host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+        bufs.append(torch.from_numpy(host).cuda())
+        plans.append(s3.Plan(offs, lens))
+        outs.append(torch.zeros((n, 8), dtype=torch.int32, device="cuda"))
+        wants.append(oracle.batch(host, offs, lens))
+    torch.cuda.synchronize()
+    for k in range(2):
+        plans[k].launch(bufs[k], outs[k], streams[k])
+    torch.cuda.synchronize()
+    for k in range(2):
+        assert np.array_equal(outs[k].cpu().numpy().view(np.uint32), wants[k]), k
+        plans[k].close()

@@ -105,19 +105,26 @@ def _c2(torch, nparts):
     return data, offs, lens
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
-def test_c2_full_batch_bit_exact(torch_cuda, oracle, golden, kernel):
-    """BASELINE config 2: 1024 x 8 MiB in HBM; fixtures p in {0..15, 511, 1022, 1023} and all
-    1024 digests against the oracle on the same bytes."""
+@pytest.fixture(scope="module")
+def c2_batch(torch_cuda, oracle):
+    """BASELINE config 2 in HBM (1024 x 8 MiB) and the oracle's 1024 digests of the same bytes."""
     data, offs, lens = _c2(torch_cuda, 1024)
+    want = oracle.batch(data.cpu().numpy(), offs, lens, threads=16)
+    yield data, offs, lens, want
+    del data
+    torch_cuda.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_c2_full_batch_bit_exact(torch_cuda, golden, c2_batch, kernel):
+    """BASELINE config 2: 1024 x 8 MiB in HBM; fixtures p in {0..15, 511, 1022, 1023} and all
+    1024 digests against the oracle on the same bytes, for every kernel."""
+    data, offs, lens, want = c2_batch
     out = s3.sha256_batch_device(data, offs, lens, kernel=kernel).cpu().numpy().view(np.uint32)
     txt = s3.digests_to_text(out)
     for e in golden["c2_parts"]:
         assert txt[e["p"]] == e["digest"], e["p"]
-    if kernel in ("skew", "skewp", "quad", "pair"):
-        host = data.cpu().numpy()
-        want = oracle.batch(host, offs, lens, threads=16)
-        assert np.array_equal(out, want)
+    assert np.array_equal(out, want)
 
 
 def test_resumable_ranges_match_single_launch(torch_cuda, oracle):
@@ -163,11 +170,12 @@ def test_host_path_multipart_and_small_slices(torch_cuda, golden):
 
 
 def test_c3_parts_ragged(torch_cuda, oracle, golden):
-    """Two whole BASELINE config-3 parts (50.5 MiB and 8.7 MiB, not multiples of 64) plus a
-    ragged batch of 64 C3-distributed lengths scaled down 64x, packed at 256-B offsets."""
+    """The whole BASELINE config-3 parts that have lib/hash fixtures (5.0-64 MiB, not
+    multiples of 64) as one small batch, plus a ragged batch of 64 C3-distributed lengths
+    scaled down 64x, packed at 256-B offsets, on every kernel."""
     lens = [e["L"] for e in golden["c3_parts"]]
-    offs = [0, (lens[0] + 255) // 256 * 256]
-    data = torch_cuda.empty(offs[1] + lens[1] + 256, dtype=torch_cuda.uint8, device="cuda")
+    offs = np.concatenate([[0], np.cumsum([(L + 255) // 256 * 256 for L in lens])[:-1]])
+    data = torch_cuda.empty(int(offs[-1]) + lens[-1] + 256, dtype=torch_cuda.uint8, device="cuda")
     s3.generate_parts(data, offs, lens, [e["p"] for e in golden["c3_parts"]], SEED)
     got = s3.digests_to_text(s3.sha256_batch_device(data, offs, lens).cpu().numpy())
     assert got == [e["digest"] for e in golden["c3_parts"]]
@@ -230,8 +238,8 @@ def test_md5_edges_all_alignments(torch_cuda, oracle, golden):
     assert got == want
 
 
-def test_md5_c2_and_ragged_vs_oracle(torch_cuda, oracle, golden):
-    data, offs, lens = _c2(torch_cuda, 1024)
+def test_md5_c2_and_ragged_vs_oracle(torch_cuda, oracle, golden, c2_batch):
+    data, offs, lens, _ = c2_batch
     out = s3.md5_batch_device(data, offs, lens).cpu().numpy().view(np.uint32)
     txt = s3.digests_to_text(out, 4)
     for e in golden["md5"]["c2_parts"]:

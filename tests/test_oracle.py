@@ -3,6 +3,7 @@
 tests/golden/sha256_golden.json was produced by tests/golden/gen_golden.py from the REAL
 lib/hash compiled from /root/reference (and cross-checked there with hashlib)."""
 import hashlib
+import os
 import hmac as pyhmac
 
 import numpy as np
@@ -83,3 +84,39 @@ def test_md5_oracle_golden(oracle, golden):
         assert list(oracle.md5_stream(iv, big[:s["L"]])) == s["state"], s["L"]
     for e in md["c2_parts"][:1]:
         assert oracle.md5(oracle.generate(e["p"], e["L"])).tobytes().hex() == e["digest"]
+
+
+def test_cpu_baseline_restatement_matches_goldens(oracle, golden):
+    """oracle/cpu_baseline.c (the lib/hash-cost-structure baseline bench.py times) is bit-exact
+    on the reference KATs, every golden edge length (4 KiB scratch vs calloc'd copy) and a
+    threaded batch of C2 parts."""
+    import ctypes
+    import subprocess
+    import numpy as np
+    from tests.oracle_lib import ROOT, u64p
+    so = os.path.join(ROOT, "oracle", "libcpubase.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+    L = ctypes.CDLL(so)
+    L.base_sha256.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    L.base_sha256_batch.argtypes = [ctypes.c_void_p, u64p, u64p, ctypes.c_uint64, ctypes.c_void_p,
+                                    ctypes.c_int]
+
+    def h(b: bytes) -> str:
+        out = np.zeros(8, np.uint32)
+        L.base_sha256(b, len(b), out.ctypes.data)
+        return out.tobytes().hex()
+
+    for k in golden["kat"]:
+        assert h(k["ascii"].encode()) == k["digest"], k["name"]
+    big = oracle.generate(7, max(e["L"] for e in golden["edge"]))
+    for e in golden["edge"]:
+        assert h(big[:e["L"]]) == e["digest"], e["L"]
+    ps = [e for e in golden["c2_parts"]][:6]
+    buf = np.concatenate([np.frombuffer(oracle.generate(e["p"], e["L"]), np.uint8) for e in ps])
+    offs = np.arange(len(ps), dtype=np.uint64) * np.uint64(8 << 20)
+    lens = np.full(len(ps), 8 << 20, dtype=np.uint64)
+    out = np.zeros((len(ps), 8), np.uint32)
+    assert L.base_sha256_batch(buf.ctypes.data, offs.ctypes.data_as(u64p), lens.ctypes.data_as(u64p),
+                               len(ps), out.ctypes.data, 4) == 0
+    assert [r.tobytes().hex() for r in out] == [e["digest"] for e in ps]
