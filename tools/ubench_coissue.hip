@@ -46,7 +46,7 @@ constexpr int kQ64Instr = 64 * 9;
 #define VP_8 "v_perm_b32 %0, %1, %3, %6\n\tv_lshrrev_b32 %2, 25, %3\n\tv_xor_b32 %4, %0, %2\n\tv_add_u32 %5, %5, %4\n\t" \
              "v_or_b32 %1, %1, %5\n\tv_lshrrev_b32 %3, 3, %3\n\tv_xor_b32 %2, %3, %4\n\tv_add_u32 %0, %0, %1\n\t"
 
-template <int P>
+template <int P, int CPRIO, int PPRIO>
 __global__ __launch_bounds__(512) void coissue(uint32_t* out, uint64_t* rec, int iters) {
   __shared__ volatile uint32_t done[5];  // [simd] = that SIMD's consumer finished; [4] = count
   __shared__ uint4 scratch[8][64];
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(512) void coissue(uint32_t* out, uint64_t* rec, int
   uint64_t t0, t1, count = 0;
   uint32_t sink = 0;
   if (wave < 4) {
-    __builtin_amdgcn_s_setprio(3);
+    if (CPRIO) __builtin_amdgcn_s_setprio(3);
     uint32_t s0 = lane * 3 + 1, s1 = lane * 5 + 2, s2 = lane * 7 + 3, s3 = lane * 11 + 4;
     uint32_t xa = 0, xb = 0, q1, q2, q3, q4;
     const uint32_t w = lane ^ 0x1234, sh = 6 + (lane & 3), msk = (lane & 4) ? ~0u : 0u;
@@ -75,6 +75,7 @@ __global__ __launch_bounds__(512) void coissue(uint32_t* out, uint64_t* rec, int
     if (lane == 0) atomicAdd(const_cast<uint32_t*>(&done[4]), 1u);
     sink = s0 ^ s1 ^ s2 ^ s3;
   } else {
+    if (PPRIO) __builtin_amdgcn_s_setprio(3);
     if (P == 0) {
       t0 = t1 = 0;
     } else {
@@ -128,7 +129,7 @@ __global__ __launch_bounds__(512) void coissue(uint32_t* out, uint64_t* rec, int
   }
 }
 
-template <int P>
+template <int P, int CPRIO = 1, int PPRIO = 0>
 int run(int grid, const char* label) {
   const int iters = 300;
   uint32_t* out;
@@ -136,7 +137,7 @@ int run(int grid, const char* label) {
   CHECK(hipMalloc(&out, size_t(grid) * 512 * 4));
   CHECK(hipMalloc(&rec, size_t(grid) * 8 * 4 * 8));
   for (int rep = 0; rep < 2; ++rep) {
-    hipLaunchKernelGGL(coissue<P>, dim3(grid), dim3(512), 0, 0, out, rec, iters);
+    hipLaunchKernelGGL((coissue<P, CPRIO, PPRIO>), dim3(grid), dim3(512), 0, 0, out, rec, iters);
     CHECK(hipDeviceSynchronize());
   }
   std::vector<uint64_t> h(size_t(grid) * 8 * 4);
@@ -161,9 +162,9 @@ int run(int grid, const char* label) {
     for (int w = 4; w < 8; ++w)
       for (int c = 0; c < 4; ++c) paired += simd_of[w] == simd_of[c];
   }
-  printf("%-40s grid=%3d consumer cyc/instr mean %.3f max %.3f | partner instr/cycle %.3f "
+  printf("%-40s prio c%d/p%d grid=%3d consumer cyc/instr mean %.3f max %.3f | partner instr/cycle %.3f "
          "(= %.2f cyc/instr) | partners sharing a consumer's SIMD %d/%d\n",
-         label, grid, ccpi / nc, cmax, np ? pipc / np : 0.0, np && pipc > 0 ? np / pipc : 0.0,
+         label, CPRIO * 3, PPRIO * 3, grid, ccpi / nc, cmax, np ? pipc / np : 0.0, np && pipc > 0 ? np / pipc : 0.0,
          paired, 4 * grid);
   CHECK(hipFree(out));
   CHECK(hipFree(rec));
@@ -178,6 +179,15 @@ int main() {
     if (run<3>(grid, "partner: VOP2 + ds_write_b128 / 16")) return 1;
     if (run<4>(grid, "partner: VOP2 + v_perm / 8")) return 1;
     if (run<5>(grid, "partner: consumer stream")) return 1;
+  }
+  // equal priorities (both 0, both 3): does a partner get slots, and at what cost?
+  for (int grid : {256}) {
+    if (run<1, 0, 0>(grid, "partner: VOP2 (lshl/lshr/xor/add/or)")) return 1;
+    if (run<3, 0, 0>(grid, "partner: VOP2 + ds_write_b128 / 16")) return 1;
+    if (run<2, 0, 0>(grid, "partner: VOP3 (alignbit/bitop3/add3)")) return 1;
+    if (run<5, 0, 0>(grid, "partner: consumer stream")) return 1;
+    if (run<1, 1, 1>(grid, "partner: VOP2 (lshl/lshr/xor/add/or)")) return 1;
+    if (run<5, 1, 1>(grid, "partner: consumer stream")) return 1;
   }
   return 0;
 }
