@@ -59,8 +59,15 @@ tests/cpp/build/sign_test: tests/cpp/sign_test.cpp s3client_amd/host/aws_sign.cp
 
 isa: $(LIBDIR)/capi.o
 
+# Kernel experiment builds (never the product): make exp TAG=name EXPFLAGS="-DS3H_EXP_..."
+# -> tools/exp/libs3hash_<TAG>.so, loaded with S3H_LIBRARY=... python bench.py ...
+exp: $(LIBDIR)/lib_hash.o $(LIBDIR)/lib_md5.o
+	@mkdir -p tools/exp
+	$(HIPCC) $(HIPFLAGS) $(EXPFLAGS) -c -o tools/exp/capi_$(TAG).o $(CSRC)/capi.hip
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o tools/exp/libs3hash_$(TAG).so tools/exp/capi_$(TAG).o $^ -lpthread
+
 clean:
 	rm -rf $(LIBDIR) tests/cpp/build apps/build build
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle cpptests isa clean
+.PHONY: all oracle cpptests isa exp clean

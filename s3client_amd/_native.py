@@ -12,6 +12,9 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libs3hash.so")
+# Kernel experiments only (`make exp` builds variants under tools/exp/): S3H_LIBRARY points the
+# Python layer at one of them.  Unset in every test, smoke and default bench run.
+LIB_PATH = os.environ.get("S3H_LIBRARY", LIB_PATH)
 
 S3H_OK, S3H_EINVAL, S3H_ENODEV, S3H_EHIP, S3H_ENOMEM = 0, -1, -2, -3, -4
 KERNEL_AUTO, KERNEL_LANE, KERNEL_PC, KERNEL_PAIR, KERNEL_QUAD, KERNEL_SKEW, KERNEL_SKEWP = 0, 1, 2, 3, 4, 5, 6

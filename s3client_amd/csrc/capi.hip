@@ -109,7 +109,12 @@ uint32_t digest_words(int algo) { return algo == S3H_ALGO_MD5 ? 4u : 8u; }
 
 // Skew / quad kernels: consumer waves per workgroup -- the fewest that keep the grid within
 // one workgroup per CU (256): one up to 2,048 parts, two up to 4,096 (kQuadMaxParts).
-int quad_waves(uint64_t n) { return n <= 256ull * s3h::kQuadChainsPerWave ? 1 : 2; }
+int quad_waves(uint64_t n) {
+#ifdef S3H_EXP_FORCE_NC  // tools/ experiment builds only
+  return S3H_EXP_FORCE_NC;
+#endif
+  return n <= 256ull * s3h::kQuadChainsPerWave ? 1 : 2;
+}
 
 // Slots in descending length order (so block counts descend too, padded or not: the kernels
 // bound a workgroup's loop by its first slot); returns the total compressions.
@@ -252,8 +257,8 @@ int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t
     hipLaunchKernelGGL((s3h::sha256_skew_kernel<1, true>), dim3(P->grid), dim3(128), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_SKEW && P->quad_waves == 1)
     hipLaunchKernelGGL(s3h::sha256_skew_kernel<1>, dim3(P->grid), dim3(128), 0, stream, A);
-  else if (P->kernel == S3H_KERNEL_SKEW)
-    hipLaunchKernelGGL(s3h::sha256_skew_kernel<2>, dim3(P->grid), dim3(192), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_SKEW)  // two flag-synchronised groups per workgroup
+    hipLaunchKernelGGL(s3h::sha256_skew_pairs_kernel, dim3(P->grid), dim3(256), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_PC)
     hipLaunchKernelGGL(s3h::sha256_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 1)
@@ -296,16 +301,29 @@ int device_cus(int device) {  // cached: the host pipeline asks once per slice
   return c > 0 ? c : 0;
 }
 
-bool dual_eligible(const s3h_plan_s* S, const s3h_plan_s* M, uint64_t b0, uint64_t b1) {
-  return M->algo == S3H_ALGO_MD5 && S->algo == S3H_ALGO_SHA256 && b1 - b0 < (1ull << 31) &&
-         ((S->kernel == S3H_KERNEL_SKEW && S->quad_waves == 1) || S->kernel == S3H_KERNEL_SKEWP) &&
-         S->grid + M->grid <= uint64_t(device_cus(S->device));
+// How one grid can produce both digests of plan S (SHA-256) and plan M (MD5, same parts in
+// the same order): kDualSplit = sha256_md5_dual_kernel (skew with one consumer per workgroup:
+// S's workgroups then M's, all within one workgroup per CU); kDualGroup =
+// sha256_md5_group_kernel (skewp: each workgroup runs a SHA-256 group and an MD5 group of the
+// same 32 parts, S->grid <= one per CU); kDualNone = two launches on two streams.
+enum DualMode { kDualNone = 0, kDualSplit = 1, kDualGroup = 2 };
+
+DualMode dual_mode(const s3h_plan_s* S, const s3h_plan_s* M, uint64_t b0, uint64_t b1) {
+  if (M->algo != S3H_ALGO_MD5 || S->algo != S3H_ALGO_SHA256 || b1 - b0 >= (1ull << 31) ||
+      S->n != M->n)
+    return kDualNone;
+  const uint64_t cus = uint64_t(device_cus(S->device));
+  if (S->kernel == S3H_KERNEL_SKEW && S->quad_waves == 1 && S->grid + M->grid <= cus)
+    return kDualSplit;
+  if (S->kernel == S3H_KERNEL_SKEWP && S->grid <= cus) return kDualGroup;
+  return kDualNone;
 }
 
 int dual_launch(s3h_plan_s* S, s3h_plan_s* M, const void* d_base, uint32_t* d_sha,
                 uint32_t* d_md5, uint64_t b0, uint64_t b1, uint64_t origin, bool ranged,
                 hipStream_t stream) {
-  if (!dual_eligible(S, M, b0, b1)) return S3H_EINVAL;
+  const DualMode mode = dual_mode(S, M, b0, b1);
+  if (mode == kDualNone) return S3H_EINVAL;
   if (b1 <= b0) return S3H_OK;
   DeviceGuard g(S->device);
   if (ranged && !S->d_state) HIP_TRY(hipMalloc(&S->d_state, S->cap * 8 * sizeof(uint32_t)));
@@ -314,13 +332,12 @@ int dual_launch(s3h_plan_s* S, s3h_plan_s* M, const void* d_base, uint32_t* d_sh
                                       origin, 0, nullptr);
   const s3h::LaunchArgs B = make_args(M, d_base, d_md5, ranged ? M->d_state : nullptr, b0, b1,
                                       origin, 0, nullptr);
-  const dim3 grid(S->grid + M->grid);
-  if (S->kernel == S3H_KERNEL_SKEWP)
-    hipLaunchKernelGGL(s3h::sha256_md5_dual_kernel<true>, grid, dim3(128), 0, stream, A, B,
-                       uint32_t(S->grid));
+  if (mode == kDualGroup)
+    hipLaunchKernelGGL(s3h::sha256_md5_group_kernel<true>, dim3(S->grid), dim3(256), 0, stream,
+                       A, B);
   else
-    hipLaunchKernelGGL(s3h::sha256_md5_dual_kernel<false>, grid, dim3(128), 0, stream, A, B,
-                       uint32_t(S->grid));
+    hipLaunchKernelGGL(s3h::sha256_md5_dual_kernel<false>, dim3(S->grid + M->grid), dim3(128), 0,
+                       stream, A, B, uint32_t(S->grid));
   HIP_TRY(hipGetLastError());
   return S3H_OK;
 }
@@ -699,7 +716,7 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
   s3h_plan_s* P0 = C.plan[0];
   s3h_plan_s* P1 = nalgo == 2 ? C.plan[1] : nullptr;
   const bool fused = nalgo == 2 && P0->max_blocks == P1->max_blocks &&
-                     dual_eligible(P0, P1, 0, bps);
+                     dual_mode(P0, P1, 0, bps) != kDualNone;
   int rc = S3H_OK;
   uint64_t k = 0;
   const double t_setup = wall_s();
@@ -1132,7 +1149,7 @@ int s3h_sha256_md5_batch_device(int device, const void* d_base, const uint64_t* 
   if (int rc = plan_build(device, S3H_ALGO_MD5, offsets, lengths, n, S3H_KERNEL_AUTO, &P[1])) return rc;
   DeviceGuard g(device);
   hipStream_t main_s = static_cast<hipStream_t>(stream);
-  if (dual_eligible(P[0], P[1], 0, P[0]->max_blocks)) {  // one grid: both digests
+  if (dual_mode(P[0], P[1], 0, P[0]->max_blocks) != kDualNone) {  // one grid: both digests
     if (int rc = dual_launch(P[0], P[1], d_base, d_sha256, d_md5, 0, P[0]->max_blocks, 0, false,
                              main_s))
       return rc;

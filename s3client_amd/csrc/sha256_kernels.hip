@@ -30,6 +30,20 @@
 // (kNoPad | kResume) and a final padded launch with each message's total bit length.
 #include "sha256_device.hpp"
 
+// Compile-time experiment parameters (tools/ builds only: `make exp`; the product build uses
+// these defaults).
+#ifndef S3H_EXP_SKEW_BPS_NC2
+#define S3H_EXP_SKEW_BPS_NC2 8  // skew NC=2: blocks per producer step
+#endif
+#ifndef S3H_EXP_PRODUCER_ROLLED
+#define S3H_EXP_PRODUCER_ROLLED 0  // 1: skew producer loops over its items without unrolling
+#endif
+#if S3H_EXP_PRODUCER_ROLLED
+#define S3H_PROD_UNROLL _Pragma("unroll 1")
+#else
+#define S3H_PROD_UNROLL _Pragma("unroll")
+#endif
+
 namespace s3h {
 
 // LaunchArgs::flags
@@ -650,24 +664,72 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_quad_kernel(LaunchArgs A
 
 // PAIR: the lane-pair layout of the same schedule (S3H_SKEWP_*, 9 VALU per round): a chain on
 // e-lane k and a-lane 7-k of a half-row, 32 chains per consumer wave.
-// The kernel body takes its workgroup index as `blk` so sha256_md5_dual_kernel can run it
-// beside MD5 workgroups in one grid.
+//
+// A GROUP is NC consumer waves (kCpw chains each) fed by one producer wave through a W+K
+// double buffer in LDS.  Two ways to synchronise a group:
+//   FLAGS = false: s_barrier, one per producer step (the group is the whole workgroup);
+//   FLAGS = true : two LDS step counters per group (produced / consumed, release-acquire at
+//                  workgroup scope), so several independent groups -- or a SHA-256 group and
+//                  an MD5 group -- share one workgroup without stalling on each other's
+//                  barriers (NC = 1 in this mode).  Every wait is bounded (kFlagSpinLimit), so
+//                  a wave can never hang on a counter.
+// `group` numbers the group's parts (slots group*kParts...), `role` is the wave's job in it:
+// consumer index 0..NC-1, or NC for the producer.
 template <int NC, bool PAIR>
-__device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t blk) {
-  constexpr uint32_t kCpw = PAIR ? 32 : kQuadChainsPerWave;  // chains per consumer wave
-  constexpr uint32_t kParts = kCpw * NC;
+struct SkewGeom {
+  static constexpr uint32_t kCpw = PAIR ? 32 : kQuadChainsPerWave;  // chains per consumer wave
+  static constexpr uint32_t kParts = kCpw * NC;
   // Blocks per producer step: 8 when the producer's lanes make at most two (part, block)
-  // items per step (one step of prefetch = ~8 blocks of chain time, one barrier per 8
-  // blocks); fewer for wider workgroups, whose producer would spill.
-  constexpr uint32_t kBps = PAIR ? 4 : NC >= 4 ? 2 : 8;
+  // items per step (one step of prefetch = ~8 blocks of chain time, one sync per 8 blocks);
+  // fewer for wider groups, whose producer would spill.
+  static constexpr uint32_t kBps = PAIR ? 4 : NC >= 4 ? 2 : NC == 2 ? S3H_EXP_SKEW_BPS_NC2 : 8;
+  static constexpr uint32_t kCols = kParts + 1;  // column kParts holds ones (read by the a-quads)
+};
+template <int NC, bool PAIR>
+struct SkewLds {
+  uint4 wk[2][SkewGeom<NC, PAIR>::kBps][16][SkewGeom<NC, PAIR>::kCols];
+};
+
+constexpr uint32_t kFlagSpinLimit = 1u << 24;  // x s_sleep 1 (64 clocks): ~0.45 s
+__device__ __forceinline__ void flag_publish(uint32_t* f, uint32_t v) {
+  __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Wait for *f >= v.  `alive` (wave-uniform) turns false after one timed-out wait and every
+// later wait of the wave returns at once: a synchronisation fault costs one timeout per wave
+// (wrong digests, caught by every parity test) instead of a hung GPU.
+__device__ __forceinline__ void flag_wait_ge(uint32_t* f, uint32_t v, bool& alive) {
+  if (!alive) return;
+  uint32_t spin = 0;
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) {
+    if (++spin >= kFlagSpinLimit) {
+      alive = false;
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+template <int NC, bool PAIR, bool FLAGS>
+__device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t group,
+                                          const uint32_t role, SkewLds<NC, PAIR>& L,
+                                          uint32_t* flags) {
+  static_assert(!FLAGS || NC == 1, "flag-synchronised groups have one consumer wave");
+  using G = SkewGeom<NC, PAIR>;
+  constexpr uint32_t kCpw = G::kCpw, kParts = G::kParts, kBps = G::kBps, kCols = G::kCols;
   constexpr uint32_t kLanes = kParts * kBps;
   constexpr uint32_t kItems = kLanes / 64;  // == NC
-  constexpr uint32_t kCols = kParts + 1;    // column kParts holds ones (read by the a-quads)
-  __shared__ uint4 lds_wk[2][kBps][16][kCols];
+  auto& lds_wk = L.wk;
+  bool alive = true;  // FLAGS: false after a timed-out wait (flag_wait_ge)
+  // FLAGS: flags[0] = producer steps published, flags[1] = consumer steps released
+#define S3H_SYNC_PRODUCED(m)                 \
+  do {                                       \
+    if constexpr (FLAGS) flag_publish(&flags[0], (m)); \
+    else __syncthreads();                    \
+  } while (0)
 
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t slot0 = blk * kParts;
+  const uint32_t slot0 = group * kParts;
+  if (slot0 >= A.n) return;
   const uint64_t b0 = A.blk_begin;
   const uint64_t wg_nb = slot_blocks(A, A.slots[slot0].len);
   const uint64_t wg_end = wg_nb < A.blk_end ? wg_nb : A.blk_end;
@@ -675,7 +737,7 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t bl
   const uint64_t iters = wg_end - b0;
   const uint64_t steps = (iters + kBps - 1) / kBps;
 
-  if (wave == NC) {
+  if (role == NC) {
     // ---------------------------------------------------------------- producer
     for (uint32_t i = lane; i < 2 * kBps * 16; i += 64)
       lds_wk[i / (kBps * 16)][(i / 16) % kBps][i % 16][kParts] = make_uint4(1u, 1u, 1u, 1u);
@@ -709,36 +771,46 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t bl
 #pragma unroll
     for (uint32_t r = 0; r < kItems; ++r)
       produce_block(ra[r], sel[r], p[r], len[r], bits[r], bh[r], A.blk_end, lds_wk[0][h[r]], part[r]);
-    __syncthreads();
+    S3H_SYNC_PRODUCED(1u);
+    // Step k goes into buffer k & 1, which held step k - 2: FLAGS waits until the consumer
+    // has released that step (the barrier of the other mode orders the same thing).
     for (uint64_t k = 1; k <= steps; k += 2) {
       if (k < steps) {
-#pragma unroll
+        if constexpr (FLAGS) {
+          if (k >= 2) flag_wait_ge(&flags[1], uint32_t(k - 1), alive);
+        }
+        S3H_PROD_UNROLL
         for (uint32_t r = 0; r < kItems; ++r) {
           fetch_full(p[r] + kStride * (k + 1), bh[r] + kBps * (k + 1) < fend[r], A.zero, ra[r]);
           produce_block(rb[r], sel[r], p[r] + kStride * k, len[r], bits[r], bh[r] + kBps * k,
                         A.blk_end, lds_wk[1][h[r]], part[r]);
         }
       }
-      __syncthreads();
+      S3H_SYNC_PRODUCED(uint32_t(k + 1));
       if (k + 1 > steps) break;
       if (k + 1 < steps) {
-#pragma unroll
+        if constexpr (FLAGS) flag_wait_ge(&flags[1], uint32_t(k), alive);
+        S3H_PROD_UNROLL
         for (uint32_t r = 0; r < kItems; ++r) {
           fetch_full(p[r] + kStride * (k + 2), bh[r] + kBps * (k + 2) < fend[r], A.zero, rb[r]);
           produce_block(ra[r], sel[r], p[r] + kStride * (k + 1), len[r], bits[r],
                         bh[r] + kBps * (k + 1), A.blk_end, lds_wk[0][h[r]], part[r]);
         }
       }
-      __syncthreads();
+      S3H_SYNC_PRODUCED(uint32_t(k + 2));
     }
     return;
   }
+#undef S3H_SYNC_PRODUCED
   // ------------------------------------------------------------------ consumer
+#ifdef S3H_EXP_LONE_CONSUMER  // experiment: only consumer wave 0 works (wrong digests)
+  if (role != 0) return;
+#endif
   __builtin_amdgcn_s_setprio(3);
   const bool ahalf = (lane >> 2) & 1u;
   const uint32_t k4 = lane & 3u;
   // quad: lanes 8c..8c+7 = chain c; pair: half-row h holds chains 4h..4h+3 (e-lane k, a-lane 7-k)
-  const uint32_t part = kCpw * wave + (PAIR ? 4 * (lane >> 3) + (ahalf ? 3 - k4 : k4) : lane >> 3);
+  const uint32_t part = kCpw * role + (PAIR ? 4 * (lane >> 3) + (ahalf ? 3 - k4 : k4) : lane >> 3);
   const uint32_t slot = slot0 + part;
   const bool valid = slot < A.n;
   const uint64_t nb = valid ? slot_blocks(A, A.slots[slot].len) : 0;
@@ -799,7 +871,18 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t bl
   const uint32_t nb_rel = nb > b0 ? uint32_t(nb - b0) : 0u;
 
   uint32_t wa[64], wb[64];
-  __syncthreads();
+  // consumer side of a step boundary: FLAGS releases the steps read so far and waits for the
+  // next one (the barrier of the other mode)
+#define S3H_SYNC_STEP(released, needed)                        \
+  do {                                                         \
+    if constexpr (FLAGS) {                                     \
+      flag_publish(&flags[1], (released));                     \
+      if ((needed) != 0u) flag_wait_ge(&flags[0], (needed), alive);   \
+    } else {                                                   \
+      __syncthreads();                                         \
+    }                                                          \
+  } while (0)
+  S3H_SYNC_STEP(0u, 1u);
   uint64_t clk0 = 0, rt0 = 0;
   if (A.clocks) {
     clk0 = __builtin_amdgcn_s_memtime();
@@ -818,7 +901,7 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t bl
 #define S3H_SKEW_FAST(L, P, CUR, NXT)                                                           \
   asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_A_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));           \
   if (i == kBps - 1) {                                                                          \
-    __syncthreads();                                                                            \
+    S3H_SYNC_STEP(j + 1, j + 2);                                                                \
     load(NXT, nbuf);                                                                            \
   } else {                                                                                      \
     load(NXT, buf + (i + 1) * kBlkStride);                                                      \
@@ -830,7 +913,7 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t bl
   {                                                                                             \
     asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_A_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));         \
     const uint32_t nx = bb + 1;                                                                 \
-    if (nx % kBps == 0 || nx >= it32) __syncthreads();                                          \
+    if (nx % kBps == 0 || nx >= it32) S3H_SYNC_STEP(nx / kBps, nx < it32 ? nx / kBps + 1 : 0u); \
     load(NXT, lbase + ((nx / kBps) & 1) * kBufStride + (nx % kBps) * kBlkStride);               \
     asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_B_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));         \
     if (bb >= cap_from) {                                                                       \
@@ -898,10 +981,11 @@ drain:
 #undef S3H_SKEW_SLOW
 #undef S3H_SKEW_LOOPS
 #undef S3H_SKEW_CAPTURE
+#undef S3H_SYNC_STEP
   if (A.clocks) {
     const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
-      uint64_t* c = A.clocks + 4ull * (blk * NC + wave);
+      uint64_t* c = A.clocks + 4ull * (group * NC + role);
       c[0] = clk0; c[1] = clk1; c[2] = rt0; c[3] = rt1;
     }
   }
@@ -918,7 +1002,23 @@ drain:
 
 template <int NC, bool PAIR = false>
 __global__ __launch_bounds__(64 * (NC + 1)) void sha256_skew_kernel(LaunchArgs A) {
-  skew_body<NC, PAIR>(A, blockIdx.x);
+  __shared__ SkewLds<NC, PAIR> L;
+  skew_body<NC, PAIR, false>(A, blockIdx.x, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L,
+                             nullptr);
+}
+
+// Two independent (consumer, producer) groups per workgroup, flag-synchronised: waves 0 and 1
+// consume groups 2b and 2b+1, waves 2 and 3 produce for them.  Four waves = one per SIMD, and
+// neither consumer ever waits for the other (with one s_barrier for both, as in
+// sha256_skew_kernel<2>, every step boundary waits for the slower of the two).
+__global__ __launch_bounds__(256) void sha256_skew_pairs_kernel(LaunchArgs A) {
+  __shared__ SkewLds<1, false> L[2];
+  __shared__ uint32_t flags[2][2];
+  if (threadIdx.x < 4) flags[threadIdx.x >> 1][threadIdx.x & 1] = 0;
+  __syncthreads();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t g = wave & 1u;
+  skew_body<1, false, true>(A, 2 * blockIdx.x + g, wave >> 1, L[g], flags[g]);
 }
 
 // ------------------------------------------------------------- MD5 (producer/consumer)
@@ -1032,13 +1132,23 @@ __device__ __forceinline__ void md5_produce(const RawBlock& r, uint32_t sel, con
     buf[q][lane] = make_uint4(km[4 * q], km[4 * q + 1], km[4 * q + 2], km[4 * q + 3]);
 }
 
-__device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t blk) {
-  __shared__ uint4 lds_km[2][16][64];
+// MD5 group: one consumer wave (role 0) and one producer wave (role 1) over kChains <= 64
+// chains (one lane each; slots group*kChains...).  FLAGS as in skew_body: s_barrier per block
+// (the group is the workgroup) or two LDS step counters (the group shares its workgroup).
+struct Md5Lds {
+  uint4 km[2][16][64];
+};
+
+template <bool FLAGS, uint32_t kChains = 64>
+__device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t group,
+                                            const uint32_t role, Md5Lds& L, uint32_t* flags) {
+  auto& lds_km = L.km;
+  bool alive = true;  // FLAGS: false after a timed-out wait (flag_wait_ge)
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t slot0 = blk * 64u;
+  const uint32_t slot0 = group * kChains;
+  if (slot0 >= A.n) return;
   const uint32_t slot = slot0 + lane;
-  const bool valid = slot < A.n;
+  const bool valid = lane < kChains && slot < A.n;
   Slot s = {0, 0};
   if (valid) s = A.slots[slot];
   const uint64_t nb = valid ? slot_blocks(A, s.len) : 0;
@@ -1047,10 +1157,11 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
   if (wg_end <= A.blk_begin) return;
   const uint64_t iters = wg_end - A.blk_begin;
 
-  if (wave == 1) {
+  if (role == 1) {
     // An MD5 block takes the consumer only ~0.9 us, less than an HBM round trip under load,
     // so the producer keeps TWO blocks in flight: three register sets rotate, and the load
-    // for block j+2 is issued while block j is produced.
+    // for block j+2 is issued while block j is produced.  Block j goes into buffer j & 1,
+    // which held block j - 2 (FLAGS: wait until the consumer released it).
     const uint64_t b0 = A.blk_begin;
     const uint8_t* p = A.base + s.off + 64ull * (b0 - A.blk_origin);
     const uint32_t sel = le_selector(uint32_t(reinterpret_cast<uintptr_t>(p) & 3));
@@ -1061,13 +1172,18 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
     fetch_full(p + 64, b0 + 1 < fend, A.zero, rb);
     fetch_full(p + 128, b0 + 2 < fend, A.zero, rc);
     md5_produce(ra, sel, p, s.len, bits, b0, A.blk_end, lds_km[0], lane);
-    __syncthreads();
+    if constexpr (FLAGS) flag_publish(&flags[0], 1u);
+    else __syncthreads();
 #define S3H_MD5_PSTEP(J, NEXT, CUR)                                                        \
     if ((J) < iters) {                                                                     \
       fetch_full(p + 64 * ((J) + 2), b0 + (J) + 2 < fend, A.zero, NEXT);                    \
+      if constexpr (FLAGS) {                                                               \
+        if ((J) >= 2) flag_wait_ge(&flags[1], uint32_t((J) - 1), alive);                           \
+      }                                                                                    \
       md5_produce(CUR, sel, p + 64 * (J), s.len, bits, b0 + (J), A.blk_end, lds_km[(J) & 1], lane); \
     }                                                                                      \
-    __syncthreads();                                                                       \
+    if constexpr (FLAGS) flag_publish(&flags[0], uint32_t((J) + 1));                       \
+    else __syncthreads();                                                                  \
     if ((J) + 1 > iters) break;
     for (uint64_t j = 1;; j += 3) {
       S3H_MD5_PSTEP(j, ra, rb)
@@ -1082,7 +1198,8 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
       const uint4 v = reinterpret_cast<const uint4*>(A.state + 8ull * A.out_idx[slot])[0];
       st[0] = v.x; st[1] = v.y; st[2] = v.z; st[3] = v.w;
     }
-    __syncthreads();
+    if constexpr (FLAGS) flag_wait_ge(&flags[0], 1u, alive);
+    else __syncthreads();
     for (uint64_t i = 0; i < iters; ++i) {
       uint32_t km[64];
 #pragma unroll
@@ -1097,7 +1214,12 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
       st[1] = live ? st[1] + b : st[1];
       st[2] = live ? st[2] + c : st[2];
       st[3] = live ? st[3] + d : st[3];
-      __syncthreads();
+      if constexpr (FLAGS) {
+        flag_publish(&flags[1], uint32_t(i + 1));
+        if (i + 1 < iters) flag_wait_ge(&flags[0], uint32_t(i + 2), alive);
+      } else {
+        __syncthreads();
+      }
     }
     if (valid && nb > A.blk_begin) {
       if (emits(A, nb))
@@ -1110,24 +1232,51 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
   }
 }
 
-__global__ __launch_bounds__(kPcThreads) void md5_pc_kernel(LaunchArgs A) { md5_pc_body(A, blockIdx.x); }
+__global__ __launch_bounds__(kPcThreads) void md5_pc_kernel(LaunchArgs A) {
+  __shared__ Md5Lds L;
+  md5_pc_body<false>(A, blockIdx.x, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L, nullptr);
+}
 
 // ------------------------------------------------------------- dual digest (SHA-256 + MD5)
-// One grid for x-amz-content-sha256 AND Content-MD5 of the same parts: workgroups
-// [0, sha_grid) run the skew SHA-256 body (PAIR: skewp), the rest the MD5 body.  Two
-// separate concurrent launches let the dispatcher stack MD5 workgroups onto CUs already
-// running SHA-256 ones, where the two consumers share a SIMD's issue and both chains slow
-// ~1.4-2.2x (kernel trace, profiles/r01_dual_kernel_trace.txt); one grid of <= 256
-// workgroups is placed one per CU (profiles/r01_placement.txt).  Both bodies are 128-thread
-// (1 consumer + 1 producer wave).
+// x-amz-content-sha256 AND Content-MD5 of the same parts in one grid.
+//
+// sha256_md5_dual_kernel: workgroups [0, sha_grid) run the skew SHA-256 body (PAIR: skewp),
+// the rest the MD5 body (128-thread workgroups each).  Two separate concurrent launches let
+// the dispatcher stack MD5 workgroups onto CUs already running SHA-256 ones, where the two
+// consumers share a SIMD's issue and both chains slow ~1.4-2.2x (kernel trace,
+// profiles/r01_dual_kernel_trace.txt); one grid of <= 256 workgroups is placed one per CU
+// (profiles/r01_placement.txt).  Used while sha_grid + md5_grid <= #CUs (skew, <= 2,048 parts).
 static_assert(kPcThreads == 128, "dual kernel assumes 128-thread MD5 workgroups");
 template <bool PAIR>
 __global__ __launch_bounds__(128) void sha256_md5_dual_kernel(LaunchArgs S, LaunchArgs M,
                                                               uint32_t sha_grid) {
+  __shared__ SkewLds<1, PAIR> LS;
+  __shared__ Md5Lds LM;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (blockIdx.x < sha_grid)
-    skew_body<1, PAIR>(S, blockIdx.x);
+    skew_body<1, PAIR, false>(S, blockIdx.x, wave, LS, nullptr);
   else
-    md5_pc_body(M, blockIdx.x - sha_grid);
+    md5_pc_body<false>(M, blockIdx.x - sha_grid, wave, LM, nullptr);
+}
+
+// sha256_md5_group_kernel: every workgroup holds BOTH digests of the same kCpw parts -- a
+// SHA-256 group (wave 0 consumes, wave 2 produces) and an MD5 group (wave 1 consumes, wave 3
+// produces), flag-synchronised so neither waits for the other's steps.  Four waves, one per
+// SIMD: the MD5 chain (4 VALU per step) runs on its own SIMD beside the SHA-256 chain, so a
+// grid of <= 256 workgroups (skewp: <= 8,192 parts, BASELINE C4's per-GPU shard) gets both
+// digests in the SHA-256 time.  The MD5 plan must hold the same parts in the same order.
+template <bool PAIR>
+__global__ __launch_bounds__(256) void sha256_md5_group_kernel(LaunchArgs S, LaunchArgs M) {
+  __shared__ SkewLds<1, PAIR> LS;
+  __shared__ Md5Lds LM;
+  __shared__ uint32_t flags[2][2];
+  if (threadIdx.x < 4) flags[threadIdx.x >> 1][threadIdx.x & 1] = 0;
+  __syncthreads();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if ((wave & 1u) == 0)
+    skew_body<1, PAIR, true>(S, blockIdx.x, wave >> 1, LS, flags[0]);
+  else
+    md5_pc_body<true, SkewGeom<1, PAIR>::kParts>(M, blockIdx.x, wave >> 1, LM, flags[1]);
 }
 
 // ------------------------------------------------------------- verification

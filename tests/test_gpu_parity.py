@@ -366,3 +366,47 @@ def test_host_path_pinned_and_pageable_agree(torch_cuda, oracle):
     assert np.array_equal(s3.sha256_batch_host(copies), want)
     sha, _ = s3.sha256_md5_batch_host(copies)
     assert np.array_equal(sha, want)
+
+
+def test_dual_digest_group_kernel_device_and_host(torch_cuda, oracle):
+    """sha256_md5_group_kernel (skewp SHA-256 group + MD5 group of the same 32 parts in one
+    flag-synchronised workgroup): 8,192 ragged parts on the device (grid 256), and 5,000
+    pageable host parts streamed in 4 KiB slices (ranged launches of the same kernel)."""
+    rng = np.random.default_rng(61)
+    n = 8192
+    rl = rng.integers(0, 6000, n)
+    rl[:4] = [0, 55, 56, 64]
+    ro = np.cumsum(rng.integers(0, 40, n) + np.concatenate([[0], rl[:-1]]))
+    host = rng.integers(0, 256, int(ro[-1] + rl[-1]) + 8, dtype=np.uint8)
+    assert s3.Plan(ro, rl).info()["kernel"] == "skewp"
+    sha, m5 = s3.sha256_md5_batch_device(_dev_buffer(torch_cuda, host), ro, rl)
+    assert np.array_equal(sha.cpu().numpy().view(np.uint32), oracle.batch(host, ro, rl))
+    assert np.array_equal(m5.cpu().numpy().view(np.uint32), oracle.md5_batch(host, ro, rl))
+    parts = [rng.integers(0, 256, int(L), dtype=np.uint8) for L in rng.integers(0, 20000, 5000)]
+    sha, m5 = s3.sha256_md5_batch_host(parts, slice_bytes=4096)
+    assert np.array_equal(sha, np.stack([oracle.sha256(p.tobytes()) for p in parts]))
+    assert np.array_equal(m5, np.stack([oracle.md5(p.tobytes()) for p in parts]))
+
+
+@pytest.mark.parametrize("n,kernel", [(3000, "skew"), (5000, "skewp")])
+def test_flag_synchronised_kernels_resumable(torch_cuda, oracle, n, kernel):
+    """The two-group skew kernel (2,049-4,096 parts) and skewp: resumable ranged launches of
+    odd block counts == one launch == the oracle (the step counters restart per launch)."""
+    rng = np.random.default_rng(62)
+    lens = rng.integers(0, 40000, n)
+    lens[:3] = [0, 63, 64]
+    offs = np.concatenate([[0], np.cumsum(lens + 3)[:-1]])
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 8, dtype=np.uint8)
+    data = _dev_buffer(torch_cuda, host)
+    plan = s3.Plan(offs, lens, kernel=kernel)
+    if kernel == "skew":
+        assert plan.info()["grid"] == (n + 15) // 16
+    one = torch_cuda.zeros((n, 8), dtype=torch_cuda.int32, device="cuda")
+    plan.launch(data, one)
+    many = torch_cuda.zeros((n, 8), dtype=torch_cuda.int32, device="cuda")
+    for b0 in range(0, plan.info()["max_blocks"], 101):
+        plan.launch_range(data.data_ptr(), many, b0, b0 + 101, 0)
+    torch_cuda.cuda.synchronize()
+    assert torch_cuda.equal(one, many)
+    assert np.array_equal(one.cpu().numpy().view(np.uint32), oracle.batch(host, offs, lens))
+    plan.close()

@@ -4,9 +4,8 @@ llvm-objdump, so the alignment s_nop the assembler inserts are counted too), wri
 field -- so cycles/instruction is always computed against the shipped code, never a
 hand-typed table.
 
-For each kernel the consumer's steady-state loop is the largest loop that is ONE basic block
-(a label followed by straight-line code and a branch back to it): the unrolled fast step of
-the skew/skewp/quad kernels.  Its instructions (VALU, LDS, SALU, waitcnt, alignment s_nop,
+For each kernel the consumer's steady-state loop is the largest loop (a label and a branch
+back to it, nested spin loops left out): the unrolled fast step of the skew / skewp kernels.  Its instructions (VALU, LDS, SALU, waitcnt, alignment s_nop,
 barrier, branch -- everything the wave issues) divided by the blocks one step covers give the
 chain instructions per 64-B block.
 
@@ -22,7 +21,7 @@ import sys
 # others' consumer loops span several basic blocks and keep hand counts.
 KERNELS = {
     "skew": ("_ZN3s3h18sha256_skew_kernelILi1ELb0EEEvNS_10LaunchArgsE", 8),
-    "skew_nc2": ("_ZN3s3h18sha256_skew_kernelILi2ELb0EEEvNS_10LaunchArgsE", 8),
+    "skew_nc2": ("_ZN3s3h24sha256_skew_pairs_kernelENS_10LaunchArgsE", 8),
     "skewp": ("_ZN3s3h18sha256_skew_kernelILi1ELb1EEEvNS_10LaunchArgsE", 4),
 }
 INSTR = re.compile(r"^\t([a-z_][a-z0-9_]*)")
@@ -38,24 +37,30 @@ def function_body(lines, sym):
     return lines[start + 1:end]
 
 
-def single_block_loops(body):
-    """(label, [instruction mnemonics]) for each loop that is one basic block."""
-    loops, cur_label, cur = [], None, []
+def loops(body):
+    """(label, [mnemonics]) per loop (a label and a later branch back to it).  Instructions of
+    loops nested inside are left out: in the consumer's fast loop those are the flag spin
+    loops of the flag-synchronised kernels, which a wave whose producer is ahead never runs
+    (their entry check, outside the nested span, is counted)."""
+    ops, label_at, back = [], {}, []
     for l in body:
         m = LABEL.match(l)
         if m:
-            cur_label, cur = m.group(1), []
+            label_at[m.group(1)] = len(ops)
             continue
         mi = INSTR.match(l)
         if not mi:
             continue
-        cur.append(mi.group(1))
         mb = BRANCH.match(l)
-        if mb:  # a branch ends the basic block
-            if cur_label and mb.group(1) == cur_label:
-                loops.append((cur_label, list(cur)))
-            cur_label, cur = None, []
-    return loops
+        if mb and mb.group(1) in label_at:  # backward branch: a loop
+            back.append((label_at[mb.group(1)], len(ops), mb.group(1)))
+        ops.append(mi.group(1))
+    out = []
+    for t, i, name in back:
+        inner = [(t2, i2) for t2, i2, _ in back if t <= t2 and i2 < i and (t2, i2) != (t, i)]
+        keep = [ops[k] for k in range(t, i + 1) if not any(t2 <= k <= i2 for t2, i2 in inner)]
+        out.append((name, keep))
+    return out
 
 
 def classify(ops):
@@ -81,8 +86,10 @@ def main(src, dst):
     out = {"source": "gfx950 code object of capi.hip, llvm-objdump (tools/isa_counts.py)",
            "kernels": {}}
     for name, (sym, bps) in KERNELS.items():
-        loops = single_block_loops(function_body(lines, sym))
-        label, ops = max(loops, key=lambda x: len(x[1]))
+        # the consumer's loop: reads W+K from LDS, never writes it (ds_write_b128) or touches global memory
+        cand = [(n, o) for n, o in loops(function_body(lines, sym))
+                if not any(x.startswith(("ds_write_b128", "global_", "buffer_", "flat_")) for x in o)]
+        label, ops = max(cand, key=lambda x: len(x[1]))
         c = classify(ops)
         out["kernels"][name] = {
             "symbol": sym, "loop_label": label, "blocks_per_step": bps,
