@@ -304,8 +304,8 @@ int device_cus(int device) {  // cached: the host pipeline asks once per slice
 // How one grid can produce both digests of plan S (SHA-256) and plan M (MD5, same parts in
 // the same order): kDualSplit = sha256_md5_dual_kernel (skew with one consumer per workgroup:
 // S's workgroups then M's, all within one workgroup per CU); kDualGroup =
-// sha256_md5_group_kernel (skewp: each workgroup runs a SHA-256 group and an MD5 group of the
-// same 32 parts, S->grid <= one per CU); kDualNone = two launches on two streams.
+// sha256_md5_group_kernel (skewp: each workgroup runs a SHA-256 group and a self-fed MD5 wave
+// over the same 32 parts, S->grid <= one per CU); kDualNone = two launches on two streams.
 enum DualMode { kDualNone = 0, kDualSplit = 1, kDualGroup = 2 };
 
 DualMode dual_mode(const s3h_plan_s* S, const s3h_plan_s* M, uint64_t b0, uint64_t b1) {
@@ -333,7 +333,7 @@ int dual_launch(s3h_plan_s* S, s3h_plan_s* M, const void* d_base, uint32_t* d_sh
   const s3h::LaunchArgs B = make_args(M, d_base, d_md5, ranged ? M->d_state : nullptr, b0, b1,
                                       origin, 0, nullptr);
   if (mode == kDualGroup)
-    hipLaunchKernelGGL(s3h::sha256_md5_group_kernel<true>, dim3(S->grid), dim3(256), 0, stream,
+    hipLaunchKernelGGL(s3h::sha256_md5_group_kernel<true>, dim3(S->grid), dim3(192), 0, stream,
                        A, B);
   else
     hipLaunchKernelGGL(s3h::sha256_md5_dual_kernel<false>, dim3(S->grid + M->grid), dim3(128), 0,

@@ -38,6 +38,9 @@
 #ifndef S3H_EXP_PRODUCER_ROLLED
 #define S3H_EXP_PRODUCER_ROLLED 0  // 1: skew producer loops over its items without unrolling
 #endif
+#ifndef S3H_EXP_MD5_SELF_DEPTH
+#define S3H_EXP_MD5_SELF_DEPTH 4  // self-fed MD5: blocks fetched ahead
+#endif
 #if S3H_EXP_PRODUCER_ROLLED
 #define S3H_PROD_UNROLL _Pragma("unroll 1")
 #else
@@ -1102,6 +1105,17 @@ __device__ __forceinline__ void md5_step(uint32_t& a, uint32_t b, uint32_t c, ui
   a = b + __builtin_amdgcn_alignbit(t, t, 32 - md5_s(I));
 }
 
+// The 64 steps straight from the message words (M[g(i)] + K[i] formed at each step, so no
+// 64-word array is live at once: the self-fed MD5 wave keeps its register budget).
+template <int I>
+__device__ __forceinline__ void md5_steps_w(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d,
+                                            const uint32_t w[16]) {
+  if constexpr (I < 64) {
+    md5_step<I>(a, b, c, d, w[md5_g(I)] + S3H_MD5_K(I));
+    md5_steps_w<I + 1>(d, a, b, c, w);
+  }
+}
+
 template <int I>
 __device__ __forceinline__ void md5_steps(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d,
                                           const uint32_t km[64]) {
@@ -1111,10 +1125,10 @@ __device__ __forceinline__ void md5_steps(uint32_t& a, uint32_t& b, uint32_t& c,
   }
 }
 
-__device__ __forceinline__ void md5_produce(const RawBlock& r, uint32_t sel, const uint8_t* bp,
-                                            uint64_t len, uint64_t bits, uint64_t blk,
-                                            uint64_t limit, uint4 (*buf)[64], uint32_t lane) {
-  uint32_t w[16];
+// Decoded message words of MD5 block `blk` (zeros past the launch's range, padding at the end).
+__device__ __forceinline__ void md5_decode(const RawBlock& r, uint32_t sel, const uint8_t* bp,
+                                           uint64_t len, uint64_t bits, uint64_t blk,
+                                           uint64_t limit, uint32_t w[16]) {
   if (blk >= limit) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) w[j] = 0;
@@ -1124,6 +1138,13 @@ __device__ __forceinline__ void md5_produce(const RawBlock& r, uint32_t sel, con
   } else {
     md5_tail(bp, len, bits, blk, w);
   }
+}
+
+__device__ __forceinline__ void md5_produce(const RawBlock& r, uint32_t sel, const uint8_t* bp,
+                                            uint64_t len, uint64_t bits, uint64_t blk,
+                                            uint64_t limit, uint4 (*buf)[64], uint32_t lane) {
+  uint32_t w[16];
+  md5_decode(r, sel, bp, len, bits, blk, limit, w);
   uint32_t km[64];
 #pragma unroll
   for (int i = 0; i < 64; ++i) km[i] = w[md5_g(i)] + S3H_MD5_K(i);
@@ -1132,23 +1153,105 @@ __device__ __forceinline__ void md5_produce(const RawBlock& r, uint32_t sel, con
     buf[q][lane] = make_uint4(km[4 * q], km[4 * q + 1], km[4 * q + 2], km[4 * q + 3]);
 }
 
-// MD5 group: one consumer wave (role 0) and one producer wave (role 1) over kChains <= 64
-// chains (one lane each; slots group*kChains...).  FLAGS as in skew_body: s_barrier per block
-// (the group is the workgroup) or two LDS step counters (the group shares its workgroup).
-struct Md5Lds {
-  uint4 km[2][16][64];
-};
-
-template <bool FLAGS, uint32_t kChains = 64>
-__device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t group,
-                                            const uint32_t role, Md5Lds& L, uint32_t* flags) {
-  auto& lds_km = L.km;
-  bool alive = true;  // FLAGS: false after a timed-out wait (flag_wait_ge)
+// Self-fed MD5: one wave, one lane per chain (kChains <= 64, slots group*kChains...), each lane
+// loads, decodes and hashes its own blocks -- no producer wave, no LDS, no synchronisation.
+// ~350 instructions per block (64 M+K adds + 16 byte-order perms on top of the 4-VALU steps),
+// i.e. well under a SHA-256 skew/skewp chain's 544-609, so it keeps pace with the SHA-256
+// group it shares a workgroup with (sha256_md5_group_kernel).  Loads run kDepth blocks ahead
+// (an MD5 block is ~0.6 us of chain time; HBM latency under a full-chip load is several).
+template <uint32_t kChains>
+__device__ __forceinline__ void md5_self_body(const LaunchArgs& A, const uint32_t group) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t slot0 = group * kChains;
   if (slot0 >= A.n) return;
   const uint32_t slot = slot0 + lane;
   const bool valid = lane < kChains && slot < A.n;
+  Slot s = {0, 0};
+  if (valid) s = A.slots[slot];
+  const uint64_t nb = valid ? slot_blocks(A, s.len) : 0;
+  const uint64_t wg_nb = slot_blocks(A, A.slots[slot0].len);
+  const uint64_t wg_end = wg_nb < A.blk_end ? wg_nb : A.blk_end;
+  const uint64_t b0 = A.blk_begin;
+  if (wg_end <= b0) return;
+  const uint64_t iters = wg_end - b0;
+  const uint8_t* p = A.base + s.off + 64ull * (b0 - A.blk_origin);
+  const uint32_t sel = le_selector(uint32_t(reinterpret_cast<uintptr_t>(p) & 3));
+  const uint64_t fend = fetch_end(s.len, A.blk_end);
+  const uint64_t bits = valid ? msg_bits(A, slot, s.len) : 0;
+  __builtin_amdgcn_s_setprio(3);
+  uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+  if (valid && resumes(A)) {
+    const uint4 v = reinterpret_cast<const uint4*>(A.state + 8ull * A.out_idx[slot])[0];
+    st[0] = v.x; st[1] = v.y; st[2] = v.z; st[3] = v.w;
+  }
+  // ring[k % kRing] holds block k's raw bytes; block k + kDepth is fetched while block k is
+  // hashed (the loops are unrolled by kRing so every ring index is a compile-time constant).
+  // Blocks below every lane's first partial block (slots are sorted by length: the group's
+  // last slot is the shortest) take the branch-free fast loop -- decode is one v_perm per
+  // word -- so the compiler keeps counted vmcnt waits; the padding blocks at the end run the
+  // general decode (its byte loads would otherwise force a full vmcnt drain every block).
+  constexpr uint32_t kDepth = S3H_EXP_MD5_SELF_DEPTH, kRing = kDepth + 1;
+  const uint32_t last = (slot0 + kChains <= A.n ? slot0 + kChains : A.n) - 1;
+  const uint64_t full_end = (A.slots[last].len >> 6) < A.blk_end ? (A.slots[last].len >> 6) : A.blk_end;
+  const uint64_t nfast = full_end > b0 ? (full_end - b0) / kRing * kRing : 0;  // whole rings
+  RawBlock ring[kRing];
+#pragma unroll
+  for (uint32_t k = 0; k < kDepth; ++k) fetch_full(p + 64 * k, b0 + k < fend, A.zero, ring[k]);
+  auto hash_words = [&](const uint32_t w[16], uint64_t J) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+    md5_steps_w<0>(a, b, c, d, w);
+    const bool live = b0 + J < nb;
+    st[0] = live ? st[0] + a : st[0];
+    st[1] = live ? st[1] + b : st[1];
+    st[2] = live ? st[2] + c : st[2];
+    st[3] = live ? st[3] + d : st[3];
+  };
+  for (uint64_t j = 0; j < nfast; j += kRing) {
+#pragma unroll
+    for (uint32_t u = 0; u < kRing; ++u) {
+      const uint64_t J = j + u;
+      fetch_full(p + 64 * (J + kDepth), b0 + J + kDepth < fend, A.zero, ring[(u + kDepth) % kRing]);
+      uint32_t w[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_perm(ring[u].d[k + 1], ring[u].d[k], sel);
+      hash_words(w, J);
+    }
+  }
+  for (uint64_t j = nfast;; j += kRing) {
+#pragma unroll
+    for (uint32_t u = 0; u < kRing; ++u) {
+      const uint64_t J = j + u;
+      if (J >= iters) goto md5_done;
+      fetch_full(p + 64 * (J + kDepth), b0 + J + kDepth < fend, A.zero, ring[(u + kDepth) % kRing]);
+      uint32_t w[16];
+      md5_decode(ring[u], sel, p + 64 * J, s.len, bits, b0 + J, A.blk_end, w);
+      hash_words(w, J);
+    }
+  }
+md5_done:
+  if (valid && nb > b0) {
+    if (emits(A, nb))
+      reinterpret_cast<uint4*>(A.digests + 4ull * A.out_idx[slot])[0] =
+          make_uint4(st[0], st[1], st[2], st[3]);
+    else if (A.state)
+      reinterpret_cast<uint4*>(A.state + 8ull * A.out_idx[slot])[0] =
+          make_uint4(st[0], st[1], st[2], st[3]);
+  }
+}
+
+// MD5 group: one consumer wave (role 0) and one producer wave (role 1) over 64 chains (one
+// lane each; slots group*64...), an s_barrier per block.
+struct Md5Lds {
+  uint4 km[2][16][64];
+};
+
+__device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t group,
+                                            const uint32_t role, Md5Lds& L) {
+  auto& lds_km = L.km;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t slot0 = group * 64u;
+  const uint32_t slot = slot0 + lane;
+  const bool valid = slot < A.n;
   Slot s = {0, 0};
   if (valid) s = A.slots[slot];
   const uint64_t nb = valid ? slot_blocks(A, s.len) : 0;
@@ -1160,8 +1263,7 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
   if (role == 1) {
     // An MD5 block takes the consumer only ~0.9 us, less than an HBM round trip under load,
     // so the producer keeps TWO blocks in flight: three register sets rotate, and the load
-    // for block j+2 is issued while block j is produced.  Block j goes into buffer j & 1,
-    // which held block j - 2 (FLAGS: wait until the consumer released it).
+    // for block j+2 is issued while block j is produced.
     const uint64_t b0 = A.blk_begin;
     const uint8_t* p = A.base + s.off + 64ull * (b0 - A.blk_origin);
     const uint32_t sel = le_selector(uint32_t(reinterpret_cast<uintptr_t>(p) & 3));
@@ -1172,18 +1274,13 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
     fetch_full(p + 64, b0 + 1 < fend, A.zero, rb);
     fetch_full(p + 128, b0 + 2 < fend, A.zero, rc);
     md5_produce(ra, sel, p, s.len, bits, b0, A.blk_end, lds_km[0], lane);
-    if constexpr (FLAGS) flag_publish(&flags[0], 1u);
-    else __syncthreads();
+    __syncthreads();
 #define S3H_MD5_PSTEP(J, NEXT, CUR)                                                        \
     if ((J) < iters) {                                                                     \
       fetch_full(p + 64 * ((J) + 2), b0 + (J) + 2 < fend, A.zero, NEXT);                    \
-      if constexpr (FLAGS) {                                                               \
-        if ((J) >= 2) flag_wait_ge(&flags[1], uint32_t((J) - 1), alive);                           \
-      }                                                                                    \
       md5_produce(CUR, sel, p + 64 * (J), s.len, bits, b0 + (J), A.blk_end, lds_km[(J) & 1], lane); \
     }                                                                                      \
-    if constexpr (FLAGS) flag_publish(&flags[0], uint32_t((J) + 1));                       \
-    else __syncthreads();                                                                  \
+    __syncthreads();                                                                       \
     if ((J) + 1 > iters) break;
     for (uint64_t j = 1;; j += 3) {
       S3H_MD5_PSTEP(j, ra, rb)
@@ -1198,8 +1295,7 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
       const uint4 v = reinterpret_cast<const uint4*>(A.state + 8ull * A.out_idx[slot])[0];
       st[0] = v.x; st[1] = v.y; st[2] = v.z; st[3] = v.w;
     }
-    if constexpr (FLAGS) flag_wait_ge(&flags[0], 1u, alive);
-    else __syncthreads();
+    __syncthreads();
     for (uint64_t i = 0; i < iters; ++i) {
       uint32_t km[64];
 #pragma unroll
@@ -1214,12 +1310,7 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
       st[1] = live ? st[1] + b : st[1];
       st[2] = live ? st[2] + c : st[2];
       st[3] = live ? st[3] + d : st[3];
-      if constexpr (FLAGS) {
-        flag_publish(&flags[1], uint32_t(i + 1));
-        if (i + 1 < iters) flag_wait_ge(&flags[0], uint32_t(i + 2), alive);
-      } else {
-        __syncthreads();
-      }
+      __syncthreads();
     }
     if (valid && nb > A.blk_begin) {
       if (emits(A, nb))
@@ -1234,7 +1325,7 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
 
 __global__ __launch_bounds__(kPcThreads) void md5_pc_kernel(LaunchArgs A) {
   __shared__ Md5Lds L;
-  md5_pc_body<false>(A, blockIdx.x, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L, nullptr);
+  md5_pc_body(A, blockIdx.x, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L);
 }
 
 // ------------------------------------------------------------- dual digest (SHA-256 + MD5)
@@ -1256,27 +1347,29 @@ __global__ __launch_bounds__(128) void sha256_md5_dual_kernel(LaunchArgs S, Laun
   if (blockIdx.x < sha_grid)
     skew_body<1, PAIR, false>(S, blockIdx.x, wave, LS, nullptr);
   else
-    md5_pc_body<false>(M, blockIdx.x - sha_grid, wave, LM, nullptr);
+    md5_pc_body(M, blockIdx.x - sha_grid, wave, LM);
 }
 
-// sha256_md5_group_kernel: every workgroup holds BOTH digests of the same kCpw parts -- a
-// SHA-256 group (wave 0 consumes, wave 2 produces) and an MD5 group (wave 1 consumes, wave 3
-// produces), flag-synchronised so neither waits for the other's steps.  Four waves, one per
-// SIMD: the MD5 chain (4 VALU per step) runs on its own SIMD beside the SHA-256 chain, so a
-// grid of <= 256 workgroups (skewp: <= 8,192 parts, BASELINE C4's per-GPU shard) gets both
-// digests in the SHA-256 time.  The MD5 plan must hold the same parts in the same order.
+// sha256_md5_group_kernel: every workgroup holds BOTH digests of the same kParts parts -- a
+// SHA-256 group (wave 0 consumes, wave 2 produces, flag-synchronised) and a self-fed MD5 wave
+// (wave 1, md5_self_body).  Three waves, one per SIMD: the MD5 chain runs on its own SIMD
+// beside the SHA-256 chain, so a grid of <= 256 workgroups (skewp: <= 8,192 parts, BASELINE
+// C4's per-GPU shard) gets both digests in about the SHA-256 time.  The MD5 plan must hold
+// the same parts in the same order (plans of the same geometry do: stable sort).
 template <bool PAIR>
-__global__ __launch_bounds__(256) void sha256_md5_group_kernel(LaunchArgs S, LaunchArgs M) {
+__global__ __launch_bounds__(192) void sha256_md5_group_kernel(LaunchArgs S, LaunchArgs M) {
   __shared__ SkewLds<1, PAIR> LS;
-  __shared__ Md5Lds LM;
-  __shared__ uint32_t flags[2][2];
-  if (threadIdx.x < 4) flags[threadIdx.x >> 1][threadIdx.x & 1] = 0;
+  __shared__ uint32_t flags[2];
+  if (threadIdx.x < 2) flags[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if ((wave & 1u) == 0)
-    skew_body<1, PAIR, true>(S, blockIdx.x, wave >> 1, LS, flags[0]);
+#ifdef S3H_EXP_GROUP_ONLY  // experiment: 1 = SHA-256 group only, 2 = MD5 wave only
+  if ((S3H_EXP_GROUP_ONLY == 1 && wave == 1) || (S3H_EXP_GROUP_ONLY == 2 && wave != 1)) return;
+#endif
+  if (wave == 1)
+    md5_self_body<SkewGeom<1, PAIR>::kParts>(M, blockIdx.x);
   else
-    md5_pc_body<true, SkewGeom<1, PAIR>::kParts>(M, blockIdx.x, wave >> 1, LM, flags[1]);
+    skew_body<1, PAIR, true>(S, blockIdx.x, wave >> 1, LS, flags);
 }
 
 // ------------------------------------------------------------- verification
