@@ -2,6 +2,8 @@
 lib/hash C++ drop-in symbols, and its single-message sha256/hmac256 match the golden
 vectors (no GPU needed; no compute call reaches HIP here)."""
 import ctypes
+import os
+import sys
 import hashlib
 import subprocess
 
@@ -9,6 +11,8 @@ import numpy as np
 import pytest
 
 import s3client_amd as s3
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 from s3client_amd import _native
 
 
@@ -94,3 +98,24 @@ def test_cpu_md5_golden(golden, oracle):
 def test_multipart_etag_golden(golden):
     words = [np.frombuffer(bytes.fromhex(p["digest"]), dtype=np.uint32) for p in golden["md5"]["transfer"]]
     assert s3.multipart_etag(np.stack(words)) == golden["md5"]["transfer_etag"]
+
+
+def test_kernel_isa_counts_match_the_built_code_object(tmp_path):
+    """bench.py's `issue` field divides cycles by s3client_amd/kernel_isa_counts.json; that file
+    must be what tools/isa_counts.py derives from the code object `make` just built."""
+    import json
+    import subprocess
+    dis = os.path.join(ROOT, "build", "isa", "capi_gfx950.dis")
+    if not os.path.exists(dis):
+        pytest.skip("build/isa not present (run make)")
+    out = tmp_path / "counts.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_counts.py"), dis, str(out)],
+                   check=True, capture_output=True)
+    with open(out) as f:
+        fresh = json.load(f)
+    with open(os.path.join(ROOT, "s3client_amd", "kernel_isa_counts.json")) as f:
+        shipped = json.load(f)
+    assert fresh == shipped
+    k = shipped["kernels"]
+    assert 540 < k["skew"]["instr_per_block"] < 550 and 600 < k["skewp"]["instr_per_block"] < 615
+    assert k["skew"]["per_block"]["lds"] == 16.0
