@@ -128,6 +128,13 @@ int s3h_sha256_batch_host(const uint8_t *const *parts, const uint64_t *lengths, 
 int s3h_md5_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                        uint32_t *digests, int ndevices, uint64_t slice_bytes);
 
+/* The same over an explicit device list: shard k = parts i with i % ndevices == k, hashed on
+ * devices[k].  A device may be listed more than once (its shards run concurrently, e.g. one
+ * per NUMA node's copy threads, or to exercise sharding on a one-GPU host). */
+int s3h_sha256_batch_host_on(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
+                             uint32_t *digests, const int *devices, int ndevices,
+                             uint64_t slice_bytes);
+
 /* Parts given as byte ranges of a file: part i = [offsets[i], offsets[i] + lengths[i]) of
  * `path` -- the (file, offset, size) parts that S3Api::UploadFilePart sends
  * (lib/src/api/multipart_upload.cpp:216-223 -> WebClient::UploadFile, webclient.cpp:331-355),

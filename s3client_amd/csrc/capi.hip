@@ -1044,41 +1044,57 @@ int s3h_md5_batch_device(int device, const void* d_base, const uint64_t* offsets
   return batch_device(device, S3H_ALGO_MD5, d_base, offsets, lengths, n, d_digests, stream);
 }
 
-static int batch_host(const int* algos, int nalgo, const PartSource& src,
-                      const uint64_t* lengths, uint64_t n, uint32_t* const* digests, int ndevices,
-                      uint64_t slice_bytes) {
+// Shard s (of nshards) gets parts i with i % nshards == s and runs on device devs[s]; a device
+// may appear more than once (its shards run concurrently, each on its own context).
+static int batch_host_on(const int* algos, int nalgo, const PartSource& src,
+                         const uint64_t* lengths, uint64_t n, uint32_t* const* digests,
+                         const std::vector<int>& devs, uint64_t slice_bytes) {
   if (!lengths || n == 0) return fail(S3H_EINVAL, "batch_host: bad arguments");
   for (int a = 0; a < nalgo; ++a)
     if (!digests[a]) return fail(S3H_EINVAL, "batch_host: null digest array");
   int count = 0;
   if (int rc = s3h_device_count(&count)) return rc;
-  if (ndevices <= 0 || ndevices > count) ndevices = count;
-  if (ndevices > int(n)) ndevices = int(n);
+  if (devs.empty()) return fail(S3H_EINVAL, "batch_host: no devices");
+  for (int d : devs)
+    if (d < 0 || d >= count) return fail(S3H_EINVAL, "batch_host: device %d out of range [0,%d)", d, count);
   if (slice_bytes % 64) return fail(S3H_EINVAL, "slice_bytes must be a multiple of 64");
   if (src.parts)
     for (uint64_t i = 0; i < n; ++i)
       if (!src.parts[i] && lengths[i]) return fail(S3H_EINVAL, "batch_host: part %llu is null", (unsigned long long)i);
-  std::vector<HostShard> shards(ndevices);
-  for (int d = 0; d < ndevices; ++d) shards[d] = {d, ndevices, {}};
-  for (uint64_t i = 0; i < n; ++i) shards[i % ndevices].parts.push_back(i);
-  std::vector<int> rcs(ndevices, S3H_OK);
-  std::vector<std::string> errs(ndevices);
-  auto run = [&](int d) {
-    HostCtx* C = host_ctx_cache().acquire(d);
-    rcs[d] = run_host_shard(*C, shards[d], algos, nalgo, src, lengths, digests, slice_bytes);
-    if (rcs[d]) errs[d] = g_err;
-    host_ctx_cache().release(C, rcs[d] == S3H_OK);
+  const int nshards = int(std::min<uint64_t>(devs.size(), n));
+  std::vector<HostShard> shards(nshards);
+  for (int k = 0; k < nshards; ++k) shards[k] = {devs[k], nshards, {}};
+  for (uint64_t i = 0; i < n; ++i) shards[i % nshards].parts.push_back(i);
+  std::vector<int> rcs(nshards, S3H_OK);
+  std::vector<std::string> errs(nshards);
+  auto run = [&](int k) {
+    HostCtx* C = host_ctx_cache().acquire(shards[k].device);
+    rcs[k] = run_host_shard(*C, shards[k], algos, nalgo, src, lengths, digests, slice_bytes);
+    if (rcs[k]) errs[k] = g_err;
+    host_ctx_cache().release(C, rcs[k] == S3H_OK);
   };
-  if (ndevices == 1) {
+  if (nshards == 1) {
     run(0);
   } else {
     std::vector<std::thread> pool;
-    for (int d = 0; d < ndevices; ++d) pool.emplace_back(run, d);
+    for (int k = 0; k < nshards; ++k) pool.emplace_back(run, k);
     for (auto& t : pool) t.join();
   }
-  for (int d = 0; d < ndevices; ++d)
-    if (rcs[d]) return fail(rcs[d], "device %d: %s", d, errs[d].c_str());
+  for (int k = 0; k < nshards; ++k)
+    if (rcs[k]) return fail(rcs[k], "device %d: %s", shards[k].device, errs[k].c_str());
   return S3H_OK;
+}
+
+// ndevices GPUs 0..ndevices-1 (0 or more than visible = all visible).
+static int batch_host(const int* algos, int nalgo, const PartSource& src,
+                      const uint64_t* lengths, uint64_t n, uint32_t* const* digests, int ndevices,
+                      uint64_t slice_bytes) {
+  int count = 0;
+  if (int rc = s3h_device_count(&count)) return rc;
+  if (ndevices <= 0 || ndevices > count) ndevices = count;
+  std::vector<int> devs(ndevices);
+  std::iota(devs.begin(), devs.end(), 0);
+  return batch_host_on(algos, nalgo, src, lengths, n, digests, devs, slice_bytes);
 }
 
 static int batch_host(int algo, const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
@@ -1109,6 +1125,18 @@ int s3h_sha256_md5_batch_host(const uint8_t* const* parts, const uint64_t* lengt
   PartSource src;
   src.parts = parts;
   return batch_host(algos, 2, src, lengths, n, out, ndevices, slice_bytes);
+}
+
+int s3h_sha256_batch_host_on(const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
+                             uint32_t* digests, const int* devices, int ndevices,
+                             uint64_t slice_bytes) {
+  if (!parts || !devices || ndevices <= 0) return fail(S3H_EINVAL, "batch_host_on: bad arguments");
+  static const int algo = S3H_ALGO_SHA256;
+  uint32_t* const out[1] = {digests};
+  PartSource src;
+  src.parts = parts;
+  return batch_host_on(&algo, 1, src, lengths, n, out, std::vector<int>(devices, devices + ndevices),
+                       slice_bytes);
 }
 
 int s3h_sha256_file_parts(const char* path, const uint64_t* offsets, const uint64_t* lengths,

@@ -333,6 +333,18 @@ def sha256_batch_host(parts: Sequence, ndevices: int = 0, slice_bytes: int = 0) 
     return _host_batch(lib().s3h_sha256_batch_host, DIGEST_WORDS, parts, ndevices, slice_bytes)
 
 
+def sha256_batch_host_on(parts: Sequence, devices: Sequence[int], slice_bytes: int = 0) -> np.ndarray:
+    """sha256_batch_host over an explicit device list (shard k = parts i % len(devices) == k on
+    devices[k]; repeats allowed): s3h_sha256_batch_host_on."""
+    arrs, ptrs, lens = _host_parts(parts)
+    n = len(arrs)
+    out = np.zeros((n, DIGEST_WORDS), dtype=np.uint32)
+    devs = (ctypes.c_int * len(devices))(*devices)
+    check(lib().s3h_sha256_batch_host_on(ptrs, _p64(lens), n, out.ctypes.data, devs, len(devices),
+                                         slice_bytes))
+    return out
+
+
 def sha256_file_parts(path: str, offsets, lengths, ndevices: int = 0,
                       slice_bytes: int = 0) -> np.ndarray:
     """Digests of byte ranges [offsets[i], offsets[i]+lengths[i]) of a file, read by host

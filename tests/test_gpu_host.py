@@ -142,3 +142,16 @@ def test_two_plans_on_two_streams(torch_cuda, oracle):
     for k in range(2):
         assert np.array_equal(outs[k].cpu().numpy().view(np.uint32), wants[k]), k
         plans[k].close()
+
+
+def test_sharded_host_batch_on_repeated_device(torch_cuda, oracle):
+    """The multi-device host path (one host thread and one context per shard, part i on shard
+    i % N, digests reassembled in part order) exercised on one GPU by listing it 3 times:
+    shards 1 and 2 run on private contexts concurrently with shard 0."""
+    rng = np.random.default_rng(55)
+    parts = [rng.integers(0, 256, int(L), dtype=np.uint8) for L in rng.integers(0, 300000, 301)]
+    want = np.stack([oracle.sha256(p.tobytes()) for p in parts])
+    assert np.array_equal(s3.sha256_batch_host_on(parts, [0, 0, 0]), want)
+    assert np.array_equal(s3.sha256_batch_host_on(parts[:2], [0, 0, 0, 0]), want[:2])
+    with pytest.raises(s3.S3HashError):
+        s3.sha256_batch_host_on(parts, [0, 99])
