@@ -153,8 +153,9 @@ def cpu_baseline(host: np.ndarray, offs, lens, gpu_digests: np.ndarray, nsample:
                  algo: str = "sha256"):
     """lib/hash's sha256::sha256 cost structure (oracle/cpu_baseline.c, calibrated against the
     real lib/hash: profiles/r02_cpu_baseline_calibration.json) timed on this host's cores over
-    the same parts as the GPU: one thread per available CPU (sched_getaffinity), parts
-    round-robin, plus a 1-thread figure.  MD5: the oracle port (the reference has no padded
+    the same parts as the GPU: one thread per available CPU (sched_getaffinity) and one per
+    CPU of the cgroup quota, the faster of the two reported, parts round-robin, plus a
+    1-thread figure.  MD5: the oracle port (the reference has no padded
     in-memory md5, md5.cpp:119-122)."""
     from tests.oracle_lib import ORACLE_SO, u64p
     if algo == "md5":
@@ -165,14 +166,24 @@ def cpu_baseline(host: np.ndarray, offs, lens, gpu_digests: np.ndarray, nsample:
         fn = ctypes.CDLL(path).base_sha256_batch
     words = 4 if algo == "md5" else 8
     fn.argtypes = [ctypes.c_void_p, u64p, u64p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
-    threads = int(os.environ.get("S3H_CPU_THREADS", len(os.sched_getaffinity(0))))
+    affinity = len(os.sched_getaffinity(0))
+    quota = _cgroup_cpu_quota()
     n = min(nsample, len(lens))
     o = np.ascontiguousarray(offs[:n], dtype=np.uint64)
     ln = np.ascontiguousarray(lens[:n], dtype=np.uint64)
-    out = np.zeros((n, words), dtype=np.uint32)
-    t0 = time.perf_counter()
-    fn(host.ctypes.data, o.ctypes.data_as(u64p), ln.ctypes.data_as(u64p), n, out.ctypes.data, threads)
-    dt = time.perf_counter() - t0
+    # One thread per available CPU (sched_getaffinity); when a cgroup quota is smaller than
+    # that (the GPU box: 16 CPUs of a 128-core host) the over-subscribed run is throttled and
+    # noisy, so the quota's thread count is timed too and the faster run is the baseline.
+    counts = [int(os.environ["S3H_CPU_THREADS"])] if "S3H_CPU_THREADS" in os.environ else \
+        sorted({affinity, max(1, min(affinity, int(np.ceil(quota))))} if quota else {affinity})
+    runs = {}
+    for threads in counts:
+        out = np.zeros((n, words), dtype=np.uint32)
+        t0 = time.perf_counter()
+        fn(host.ctypes.data, o.ctypes.data_as(u64p), ln.ctypes.data_as(u64p), n, out.ctypes.data, threads)
+        runs[threads] = (time.perf_counter() - t0, out)
+    threads = min(runs, key=lambda k: runs[k][0])
+    dt, out = runs[threads]
     n1 = min(16, n)
     out1 = np.zeros((n1, words), dtype=np.uint32)
     t1 = time.perf_counter()
@@ -186,11 +197,15 @@ def cpu_baseline(host: np.ndarray, offs, lens, gpu_digests: np.ndarray, nsample:
     except Exception:
         pass
     gib = float(ln.sum()) / 2**30
+    parity = parity and all(np.array_equal(r[1], gpu_digests[:n]) for r in runs.values())
     return {"value": round(gib / dt, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"{n} of the bench's parts ({gib:.2f} GiB, the same bytes as the GPU) with "
                       f"{'oracle/cpu_baseline.c (lib/hash sha256::sha256 cost structure)' if algo == 'sha256' else 'the oracle MD5 port'}"
-                      f" on {threads} threads (one per CPU in sched_getaffinity), parts round-robin",
-            "build_flags": flags, "cgroup_cpu_quota": _cgroup_cpu_quota(),
+                      f" on {threads} threads, parts round-robin (faster of {sorted(runs)} threads: "
+                      f"sched_getaffinity count and cgroup quota)",
+            "GiBps_by_threads": {str(k): round(gib / v[0], 3) for k, v in sorted(runs.items())},
+            "affinity_cpus": affinity,
+            "build_flags": flags, "cgroup_cpu_quota": quota,
             "single_thread_GiBps": round(float(ln[:n1].sum()) / 2**30 / dt1, 3),
             "single_thread_sample": f"{n1} parts",
             "calibration": "restatement / real lib/hash = 0.93-1.01 (1 thread, -march=native, "
