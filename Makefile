@@ -37,7 +37,7 @@ $(LIBDIR)/lib_md5.o: $(CSRC)/cpu/lib_md5.cpp include/md5.h include/utility.h inc
 $(LIB): $(LIBDIR)/capi.o $(LIBDIR)/lib_hash.o $(LIBDIR)/lib_md5.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 
-oracle:
+oracle: $(LIB)
 	$(MAKE) -C oracle
 
 CPPTESTS := tests/cpp/build/dropin_test tests/cpp/build/sign_test
