@@ -363,7 +363,8 @@ def main():
             "data": "synthetic: generator G(seed=20241008) written in HBM by a HIP kernel",
             "config": {"workload": name, "parts_per_gpu": int(len(lens)),
                        "part_bytes": int(lens[0]) if args.config != "c3" else "5-64 MiB",
-                       "kernel": kname, "grid": info["grid"],
+                       "kernel": kname, "grid": info["grid"], "groups": info["groups"],
+                       "solo_workgroups": info["solo"],
                        "parallelism": f"parts sharded round-robin over {world} GPU(s), no collective"},
             "parity": {"fixtures_checked": checked, "mismatches": int(bad)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

@@ -91,6 +91,10 @@ int s3h_plan_launch_range(s3h_plan_t plan, const void *d_base, uint32_t *d_diges
 /* Introspection: total 64-B compressions, max blocks of any part, chosen kernel, grid size. */
 int s3h_plan_info(s3h_plan_t plan, uint64_t *n, uint64_t *total_blocks, uint64_t *max_blocks,
                   int *kernel, uint32_t *grid);
+/* Workgroup layout: consumer groups of the grid (skew/skewp kernels; 0 for the others) and how
+ * many leading workgroups of the two-group skew kernel run one group on a CU of their own
+ * (the groups of the longest parts of a ragged batch). */
+int s3h_plan_groups(s3h_plan_t plan, uint32_t *groups, uint32_t *solo);
 
 /* Measurement hook (not part of the lib/hash surface): while d_clocks (device memory,
  * 4 x *waves uint64) is set, every launch of a plan on the skew kernel records, per consumer

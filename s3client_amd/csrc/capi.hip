@@ -87,6 +87,7 @@ struct s3h_plan_s {
   uint32_t* d_state = nullptr;  // n*8 chaining words, allocated on first ranged launch
   uint8_t* d_zero = nullptr;    // 256 zero bytes: load target for out-of-range lanes
   int quad_waves = 1;           // skew / quad kernels: consumer waves per workgroup (1-2)
+  uint32_t solo = 0;            // two-group skew grid: leading one-group workgroups (plan_solo)
   uint64_t* d_clocks = nullptr; // clock probe buffer (caller-owned), see s3h_plan_set_clock_probe
 };
 
@@ -118,6 +119,62 @@ int quad_waves(uint64_t n) {
 
 // Slots in descending length order (so block counts descend too, padded or not: the kernels
 // bound a workgroup's loop by its first slot); returns the total compressions.
+int device_cus(int device) {  // cached: the host pipeline asks once per slice
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> cus[kMaxDev] = {};
+  if (device < 0 || device >= kMaxDev) return 0;
+  int c = cus[device].load(std::memory_order_relaxed);
+  if (c == 0) {
+    hipDeviceProp_t prop;
+    c = hipGetDeviceProperties(&prop, device) == hipSuccess ? prop.multiProcessorCount : -1;
+    cus[device].store(c, std::memory_order_relaxed);
+  }
+  return c > 0 ? c : 0;
+}
+
+// Two-group skew grid (2,049-4,096 parts): how many leading workgroups run ONE group.  With
+// all four SIMDs of a CU busy each wave issues 2-3 % slower than with two (C3: 2,280 vs 2,228
+// cycles/block, profiles/r02_exp_c3_solo.jsonl), and a ragged batch's time is set by its
+// longest parts, which sort first.  So the groups of the longest parts get a CU of their own
+// (the launch's LDS pad admits one workgroup per CU) when that shortens the estimated
+// makespan: group g takes (its first slot's blocks) x (1 alone | kPairSlow paired), and
+// workgroups start in grid order on the first CU to free.  Equal-length batches keep 0.
+// kPairSlow: measured 1.023 (C3: 2,280 paired vs 2,228 solo cycles/block) plus a margin, so
+// that the boundary group (the longest paired one) does not become the new critical path.
+constexpr double kPairSlow = 1.04;
+uint32_t plan_solo(const s3h::Slot* slots, uint64_t n, uint64_t cus) {
+  const uint64_t groups = (n + s3h::kQuadChainsPerWave - 1) / s3h::kQuadChainsPerWave;
+  if (cus == 0 || groups < 2) return 0;
+  std::vector<double> gb(groups);
+  for (uint64_t g = 0; g < groups; ++g)
+    gb[g] = double(s3h::nblocks(slots[g * s3h::kQuadChainsPerWave].len));
+  std::vector<double> ends;
+  ends.reserve(cus);
+  auto makespan = [&](uint64_t F) {
+    const uint64_t wgs = F + (groups - F + 1) / 2;
+    auto dur = [&](uint64_t w) { return w < F ? gb[w] : gb[F + 2 * (w - F)] * kPairSlow; };
+    ends.clear();
+    double span = 0;
+    for (uint64_t w = 0; w < wgs && w < cus; ++w) ends.push_back(dur(w));
+    std::make_heap(ends.begin(), ends.end(), std::greater<double>());
+    for (uint64_t w = cus; w < wgs; ++w) {  // later workgroups start as the first CU frees
+      std::pop_heap(ends.begin(), ends.end(), std::greater<double>());
+      ends.back() += dur(w);
+      std::push_heap(ends.begin(), ends.end(), std::greater<double>());
+    }
+    for (double e : ends) span = std::max(span, e);
+    return span;
+  };
+  const double base = makespan(0);
+  double best = base;
+  uint64_t best_f = 0;
+  for (uint64_t F = 1; F <= groups && F <= cus; ++F) {
+    const double m = makespan(F);
+    if (m < best) best = m, best_f = F;
+  }
+  return best < base * 0.995 ? uint32_t(best_f) : 0u;  // a clear gain only
+}
+
 uint64_t sort_slots(const uint64_t* offsets, const uint64_t* lengths, uint64_t n, bool nopad,
                     s3h::Slot* slots, uint32_t* order) {
   std::iota(order, order + n, 0u);
@@ -186,7 +243,16 @@ int plan_geometry(s3h_plan_s* P, const uint64_t* offsets, const uint64_t* length
   P->total_blocks = sort_slots(offsets, lengths, n, false, h_slots, h_order);
   P->max_blocks = s3h::nblocks(h_slots[0].len);
   P->quad_waves = quad_waves(n);
-  P->grid = P->kernel == S3H_KERNEL_PC ? uint32_t((n + 63) / 64)
+  P->solo = 0;
+  if (P->kernel == S3H_KERNEL_SKEW && P->quad_waves == 2) {
+#ifdef S3H_EXP_SOLO  // tools/ experiment builds only: force the solo count
+    P->solo = uint32_t(std::min<uint64_t>(S3H_EXP_SOLO, (n + 7) / 8));
+#else
+    P->solo = plan_solo(h_slots, n, uint64_t(device_cus(P->device)));
+#endif
+  }
+  P->grid = P->solo ? P->solo + uint32_t(((n + 7) / 8 - P->solo + 1) / 2)
+            : P->kernel == S3H_KERNEL_PC ? uint32_t((n + 63) / 64)
             : P->kernel == S3H_KERNEL_PAIR || P->kernel == S3H_KERNEL_SKEWP
                 ? uint32_t((n + s3h::kPairParts - 1) / s3h::kPairParts)
             : P->kernel == S3H_KERNEL_QUAD || P->kernel == S3H_KERNEL_SKEW
@@ -236,8 +302,13 @@ s3h::LaunchArgs make_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests
   A.n = uint32_t(P->n);
   A.flags = flags;
   A.clocks = P->d_clocks;
+  A.solo = P->solo;
   return A;
 }
+
+// Dynamic LDS added to a grid with solo workgroups: 72 KiB of groups + 12 KiB > half of the
+// CU's 160 KiB, so one workgroup per CU and a solo group never shares its CU.
+constexpr uint32_t kSoloLdsPad = 12 * 1024;
 
 int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t* d_state,
                 uint64_t b0, uint64_t b1, uint64_t origin, uint32_t flags, const uint64_t* d_bits,
@@ -258,7 +329,8 @@ int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t
   else if (P->kernel == S3H_KERNEL_SKEW && P->quad_waves == 1)
     hipLaunchKernelGGL(s3h::sha256_skew_kernel<1>, dim3(P->grid), dim3(128), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_SKEW)  // two flag-synchronised groups per workgroup
-    hipLaunchKernelGGL(s3h::sha256_skew_pairs_kernel, dim3(P->grid), dim3(256), 0, stream, A);
+    hipLaunchKernelGGL(s3h::sha256_skew_pairs_kernel, dim3(P->grid), dim3(256),
+                       P->solo ? kSoloLdsPad : 0, stream, A);
   else if (P->kernel == S3H_KERNEL_PC)
     hipLaunchKernelGGL(s3h::sha256_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_QUAD && P->quad_waves == 1)
@@ -288,18 +360,6 @@ int plan_launch(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint64_t
 // then launches the two plans on two streams).
 // The fused grid must fit one workgroup per CU: beyond that its MD5 workgroups (the grid's
 // tail) would only start as SHA-256 ones retire, i.e. run after them.
-int device_cus(int device) {  // cached: the host pipeline asks once per slice
-  constexpr int kMaxDev = 64;
-  static std::atomic<int> cus[kMaxDev] = {};
-  if (device < 0 || device >= kMaxDev) return 0;
-  int c = cus[device].load(std::memory_order_relaxed);
-  if (c == 0) {
-    hipDeviceProp_t prop;
-    c = hipGetDeviceProperties(&prop, device) == hipSuccess ? prop.multiProcessorCount : -1;
-    cus[device].store(c, std::memory_order_relaxed);
-  }
-  return c > 0 ? c : 0;
-}
 
 // How one grid can produce both digests of plan S (SHA-256) and plan M (MD5, same parts in
 // the same order): kDualSplit = sha256_md5_dual_kernel (skew with one consumer per workgroup:
@@ -998,13 +1058,24 @@ int s3h_plan_launch_range(s3h_plan_t P, const void* d_base, uint32_t* d_digests,
   return plan_launch(P, d_base, d_digests, b0, b1, origin, static_cast<hipStream_t>(stream), true);
 }
 
+// Consumer waves (= groups) of a skew/skewp grid; 0 for the kernels without a clock probe.
+static uint32_t consumer_groups(const s3h_plan_s* P) {
+  return P->kernel == S3H_KERNEL_SKEW && P->quad_waves == 2 ? uint32_t((P->n + 7) / 8)
+         : P->kernel == S3H_KERNEL_SKEW || P->kernel == S3H_KERNEL_SKEWP ? P->grid
+                                                                          : 0u;
+}
+
 int s3h_plan_set_clock_probe(s3h_plan_t P, uint64_t* d_clocks, uint32_t* waves) {
   if (!P) return fail(S3H_EINVAL, "null plan");
   P->d_clocks = d_clocks;
-  if (waves)
-    *waves = P->kernel == S3H_KERNEL_SKEW    ? P->grid * uint32_t(P->quad_waves)
-             : P->kernel == S3H_KERNEL_SKEWP ? P->grid
-                                             : 0u;
+  if (waves) *waves = consumer_groups(P);
+  return S3H_OK;
+}
+
+int s3h_plan_groups(s3h_plan_t P, uint32_t* groups, uint32_t* solo) {
+  if (!P) return fail(S3H_EINVAL, "null plan");
+  if (groups) *groups = consumer_groups(P);
+  if (solo) *solo = P->solo;
   return S3H_OK;
 }
 

@@ -67,6 +67,9 @@ struct LaunchArgs {
   // Clock probe (s3h_plan_set_clock_probe; skew kernel): per consumer wave, shader-clock and
   // 100 MHz real-time counters at the start and end of its chain loop.  Null: off.
   uint64_t* clocks;
+  // sha256_skew_pairs_kernel: the first `solo` workgroups run one group each (the longest
+  // parts, on a CU of their own), the rest two.  0 elsewhere.
+  uint32_t solo;
 };
 
 // Compressions the launch sequence runs for a slot of `len` bytes.
@@ -1014,6 +1017,10 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_skew_kernel(LaunchArgs A
 // consume groups 2b and 2b+1, waves 2 and 3 produce for them.  Four waves = one per SIMD, and
 // neither consumer ever waits for the other (with one s_barrier for both, as in
 // sha256_skew_kernel<2>, every step boundary waits for the slower of the two).
+// Solo workgroups (A.solo > 0): with all four SIMDs of a CU busy each wave issues ~3 % slower
+// than with two (4.18 vs 4.06 cycles/instruction), so the host gives the groups of the longest
+// parts -- the ones that set the launch's time -- a workgroup (and, through a dynamic LDS pad
+// that admits one workgroup per CU, a CU) of their own; see capi.hip plan_solo.
 __global__ __launch_bounds__(256) void sha256_skew_pairs_kernel(LaunchArgs A) {
   __shared__ SkewLds<1, false> L[2];
   __shared__ uint32_t flags[2][2];
@@ -1021,7 +1028,10 @@ __global__ __launch_bounds__(256) void sha256_skew_pairs_kernel(LaunchArgs A) {
   __syncthreads();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t g = wave & 1u;
-  skew_body<1, false, true>(A, 2 * blockIdx.x + g, wave >> 1, L[g], flags[g]);
+  const uint32_t b = blockIdx.x;
+  if (b < A.solo && g) return;  // a solo workgroup: waves 1 and 3 have no group
+  skew_body<1, false, true>(A, b < A.solo ? b : A.solo + 2 * (b - A.solo) + g, wave >> 1, L[g],
+                            flags[g]);
 }
 
 // ------------------------------------------------------------- MD5 (producer/consumer)

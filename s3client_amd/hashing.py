@@ -77,8 +77,11 @@ class Plan:
         k, g = ctypes.c_int(), ctypes.c_uint32()
         check(lib().s3h_plan_info(self._h, ctypes.byref(n), ctypes.byref(tb), ctypes.byref(mb),
                                   ctypes.byref(k), ctypes.byref(g)))
+        groups, solo = ctypes.c_uint32(), ctypes.c_uint32()
+        check(lib().s3h_plan_groups(self._h, ctypes.byref(groups), ctypes.byref(solo)))
         return {"n": n.value, "total_blocks": tb.value, "max_blocks": mb.value,
-                "kernel": _native.KERNEL_NAMES[k.value], "grid": g.value}
+                "kernel": _native.KERNEL_NAMES[k.value], "grid": g.value,
+                "groups": groups.value, "solo": solo.value}
 
     def set_clock_probe(self, clocks=None) -> int:
         """Record per-consumer-wave clock counters on later launches (skew kernel only):

@@ -1,7 +1,7 @@
 """BASELINE configs 3 and 4 at full size on one MI355X (pytest -m gpu).
 
-C3 (configs[2]): 4096 parts of U[5,64] MiB (~138 GiB resident in HBM), AUTO -> skew with two
-consumer waves per workgroup (grid 256).  C4 (configs[3]): rank 0's shard of 65,536 x 8 MiB over
+C3 (configs[2]): 4096 parts of U[5,64] MiB (~138 GiB resident in HBM), AUTO -> the two-group
+skew kernel with solo workgroups for the longest parts (grid > 256: capi.hip plan_solo).  C4 (configs[3]): rank 0's shard of 65,536 x 8 MiB over
 8 GPUs -- global parts p = 8k, 8,192 x 8 MiB = 64 GiB -- AUTO -> skewp.  Each batch is checked
 against (i) the lib/hash golden digests of the parts that have fixtures (tests/golden: C3 ids
 incl. the longest and shortest part, C4 ids of rank 0) and (ii) the oracle on 64 randomly
@@ -42,7 +42,9 @@ def test_c3_full_ragged_batch(torch_cuda, oracle, golden):
         s3.generate_parts(data, offs, lens, np.arange(n), SEED)
         with s3.Plan(offs, lens) as plan:
             info = plan.info()
-            assert info["kernel"] == "skew" and info["grid"] == 256, info
+            # 512 groups: two per workgroup, except the solo ones the makespan model adds
+            assert info["kernel"] == "skew" and info["groups"] == 512 and info["solo"] > 0, info
+            assert info["grid"] == info["solo"] + (512 - info["solo"] + 1) // 2, info
             out = torch.empty((n, 8), dtype=torch.int32, device="cuda")
             plan.launch(data, out)
             torch.cuda.synchronize()
@@ -87,5 +89,45 @@ def test_c4_rank0_shard(torch_cuda, oracle, golden):
         slots = np.sort(rng.choice(per, 64, replace=False))
         assert np.array_equal(got[slots], _oracle_sample(torch, oracle, data, offs, lens, slots))
     finally:
+        del data
+        _release(torch)
+
+
+def _ragged_top(rng, n, top, top_len, rest_len):
+    lens = rng.integers(*rest_len, n)
+    lens[:top] = rng.integers(*top_len, top)
+    rng.shuffle(lens)
+    offs = np.concatenate([[0], np.cumsum(lens + 3)[:-1]]).astype(np.uint64)  # misaligned
+    return lens.astype(np.uint64), offs
+
+
+def test_two_group_solo_grid(torch_cuda, oracle):
+    """2,049-4,096 parts whose longest few set the time: the plan gives their groups solo
+    workgroups, an equal-length batch gets none; one launch and resumable
+    ranges (the host path's slices) both bit-exact vs the oracle."""
+    torch = torch_cuda
+    rng = np.random.default_rng(505)
+    for n, top, top_len, rest_len, solo in ((4000, 150, (200_000, 300_000), (0, 40_000), True),
+                                            (2600, 40, (110_000, 112_000), (1, 5_000), True),
+                                            (4096, 0, (0, 1), (8192, 8193), False)):
+        lens, offs = _ragged_top(rng, n, top, top_len, rest_len)
+        host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+        data = torch.from_numpy(host).cuda()
+        want = oracle.batch(host, offs, lens, threads=16)
+        with s3.Plan(offs, lens) as plan:
+            info = plan.info()
+            groups = (n + 7) // 8
+            assert info["kernel"] == "skew" and info["groups"] == groups, info
+            assert (info["solo"] > 0) == solo, info
+            assert info["grid"] == info["solo"] + (groups - info["solo"] + 1) // 2, info
+            one = torch.zeros((n, 8), dtype=torch.int32, device="cuda")
+            plan.launch(data, one)
+            many = torch.zeros((n, 8), dtype=torch.int32, device="cuda")
+            step = 1231
+            for b0 in range(0, info["max_blocks"], step):
+                plan.launch_range(data.data_ptr(), many, b0, b0 + step, 0)
+            torch.cuda.synchronize()
+        assert np.array_equal(one.cpu().numpy().view(np.uint32), want), n
+        assert torch.equal(one, many), n
         del data
         _release(torch)
