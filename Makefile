@@ -20,7 +20,7 @@ all: $(LIB) oracle cpptests
 # s3client_amd/kernel_isa_counts.json).
 OBJDUMP ?= /opt/rocm/lib/llvm/bin/llvm-objdump
 ISA_DIS := build/isa/capi_gfx950.dis
-$(LIBDIR)/capi.o: $(CSRC)/capi.hip $(CSRC)/sha256_kernels.hip $(CSRC)/sha256_device.hpp $(CSRC)/sha256_skew_rounds.inc include/s3hash.h tools/isa_counts.py
+$(LIBDIR)/capi.o: $(CSRC)/capi.hip $(CSRC)/sha256_kernels.hip $(CSRC)/sha256_device.hpp $(CSRC)/sha256_skew_rounds.inc $(CSRC)/sha256_producer_simple.inc include/s3hash.h tools/isa_counts.py
 	@mkdir -p $(LIBDIR) build/isa
 	cd build/isa && $(HIPCC) $(HIPFLAGS) -save-temps -c -o ../../$@ ../../$<
 	$(OBJDUMP) -d --symbolize-operands build/isa/capi-hip-amdgcn-amd-amdhsa-gfx950.o > $(ISA_DIS)

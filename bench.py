@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4"])
     ap.add_argument("--parts-per-gpu", type=int, default=0, help="override batch size")
     ap.add_argument("--part-bytes", type=int, default=0, help="override part size (sweeps)")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "skew", "skewp", "quad", "pair", "pc", "lane"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "skew", "skewp", "skews", "quad", "pair", "pc", "lane"])
     ap.add_argument("--algo", default="sha256", choices=["sha256", "md5"],
                     help="md5: the SURVEY 8(f) Content-MD5/ETag kernel (not the metric)")
     ap.add_argument("--cpu-sample-parts", type=int, default=1024)
@@ -286,7 +286,7 @@ def main():
     # records s_memtime / s_memrealtime around its chain loop -> live shader clock and cycles
     # per block (skew kernel only).
     probe = None
-    if kname in ("skew", "skewp"):
+    if kname in ("skew", "skewp", "skews"):
         clocks = torch.zeros(4 * 4 * info["grid"], dtype=torch.int64, device=dev)
         waves = plan.set_clock_probe(clocks)
         plan.launch(data, digests, stream)

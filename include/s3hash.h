@@ -46,7 +46,8 @@ enum s3h_kernel {
   S3H_KERNEL_PAIR = 3, /* producer/consumer with each chain split over a lane pair (DPP) */
   S3H_KERNEL_QUAD = 4, /* as PAIR, each half-state on a lane quad: 9 instead of 10 VALU/round */
   S3H_KERNEL_SKEW = 5, /* lane quads with the a-quad two rounds behind: 8 VALU/round */
-  S3H_KERNEL_SKEWP = 6 /* the same skewed schedule on lane pairs: 9 VALU/round, 32 chains/wave */
+  S3H_KERNEL_SKEWP = 6, /* the same skewed schedule on lane pairs: 9 VALU/round, 32 chains/wave */
+  S3H_KERNEL_SKEWS = 7  /* SKEW with each producer on its consumer's SIMD: 32 chains per CU */
 };
 
 enum s3h_algo {

@@ -18,8 +18,9 @@ LIB_PATH = os.environ.get("S3H_LIBRARY", LIB_PATH)
 
 S3H_OK, S3H_EINVAL, S3H_ENODEV, S3H_EHIP, S3H_ENOMEM = 0, -1, -2, -3, -4
 KERNEL_AUTO, KERNEL_LANE, KERNEL_PC, KERNEL_PAIR, KERNEL_QUAD, KERNEL_SKEW, KERNEL_SKEWP = 0, 1, 2, 3, 4, 5, 6
+KERNEL_SKEWS = 7
 KERNEL_NAMES = {KERNEL_AUTO: "auto", KERNEL_LANE: "lane", KERNEL_PC: "pc", KERNEL_PAIR: "pair",
-                KERNEL_QUAD: "quad", KERNEL_SKEW: "skew", KERNEL_SKEWP: "skewp"}
+                KERNEL_QUAD: "quad", KERNEL_SKEW: "skew", KERNEL_SKEWP: "skewp", KERNEL_SKEWS: "skews"}
 KERNEL_IDS = {v: k for k, v in KERNEL_NAMES.items()}
 
 # every symbol include/s3hash.h declares (tests check the library exports all of them)

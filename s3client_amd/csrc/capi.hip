@@ -187,10 +187,15 @@ uint64_t sort_slots(const uint64_t* offsets, const uint64_t* lengths, uint64_t n
   return total;
 }
 
-int resolve_kernel(int algo, uint64_t n, int kernel) {
+// `cus`: the device's CUs.  Above 4,096 parts, while one 32-chain workgroup per CU holds the
+// batch (8,192 parts on MI355X: the C4 shard), the shared-SIMD skew kernel runs every chain
+// at the skew kernel's 8 VALU per round with its producer on the same SIMD: C4 shard 493 vs
+// 465 GiB/s for skewp (profiles/r02_bench_c4_skews.jsonl).
+int resolve_kernel(int algo, uint64_t n, int kernel, uint64_t cus) {
   if (algo == S3H_ALGO_MD5) return S3H_KERNEL_PC;  // MD5 has one kernel (4 VALU per step)
   if (kernel != S3H_KERNEL_AUTO) return kernel;
   return n <= kQuadMaxParts    ? S3H_KERNEL_SKEW
+         : n <= 32 * cus       ? S3H_KERNEL_SKEWS
          : n <= kSkewpMaxParts ? S3H_KERNEL_SKEWP
          : n <= kPairMaxParts  ? S3H_KERNEL_PAIR
          : n <= kPcMaxParts    ? S3H_KERNEL_PC
@@ -204,7 +209,7 @@ int check_plan_args(int device, int algo, uint64_t n, int kernel) {
     return fail(S3H_EINVAL, "plan: need 0 < n <= 2^31 (n=%llu)", (unsigned long long)n);
   if (algo == S3H_ALGO_MD5 && kernel != S3H_KERNEL_AUTO && kernel != S3H_KERNEL_PC)
     return fail(S3H_EINVAL, "plan: MD5 supports only the producer/consumer kernel");
-  if (kernel < S3H_KERNEL_AUTO || kernel > S3H_KERNEL_SKEWP)
+  if (kernel < S3H_KERNEL_AUTO || kernel > S3H_KERNEL_SKEWS)
     return fail(S3H_EINVAL, "plan: unknown kernel %d", kernel);
   return check_device(device);
 }
@@ -239,7 +244,7 @@ int plan_geometry(s3h_plan_s* P, const uint64_t* offsets, const uint64_t* length
   if (n > P->cap) return fail(S3H_EINVAL, "plan: %llu parts exceed capacity %llu",
                               (unsigned long long)n, (unsigned long long)P->cap);
   P->n = n;
-  P->kernel = resolve_kernel(P->algo, n, kernel);
+  P->kernel = resolve_kernel(P->algo, n, kernel, uint64_t(device_cus(P->device)));
   P->total_blocks = sort_slots(offsets, lengths, n, false, h_slots, h_order);
   P->max_blocks = s3h::nblocks(h_slots[0].len);
   P->quad_waves = quad_waves(n);
@@ -257,6 +262,7 @@ int plan_geometry(s3h_plan_s* P, const uint64_t* offsets, const uint64_t* length
                 ? uint32_t((n + s3h::kPairParts - 1) / s3h::kPairParts)
             : P->kernel == S3H_KERNEL_QUAD || P->kernel == S3H_KERNEL_SKEW
                 ? uint32_t((n + 8 * P->quad_waves - 1) / (8 * P->quad_waves))
+            : P->kernel == S3H_KERNEL_SKEWS ? uint32_t((n + 31) / 32)
                 : uint32_t((n + 255) / 256);
   HIP_TRY(hipMemcpyAsync(P->d_slots, h_slots, n * sizeof(s3h::Slot), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(P->d_out_idx, h_order, n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
@@ -322,6 +328,10 @@ int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t
     hipLaunchKernelGGL(s3h::sha256_quad_kernel<1>, dim3(P->grid), dim3(128), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_SKEW && b1 - b0 >= (1ull << 31))
     hipLaunchKernelGGL(s3h::sha256_quad_kernel<2>, dim3(P->grid), dim3(192), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_SKEWS && b1 - b0 >= (1ull << 31))
+    hipLaunchKernelGGL(s3h::sha256_quad_kernel<1>, dim3(uint32_t((P->n + 7) / 8)), dim3(128), 0, stream, A);
+  else if (P->kernel == S3H_KERNEL_SKEWS)
+    hipLaunchKernelGGL(s3h::sha256_skew_shared_kernel, dim3(P->grid), dim3(512), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_SKEWP && b1 - b0 >= (1ull << 31))
     hipLaunchKernelGGL(s3h::sha256_pair_kernel, dim3(P->grid), dim3(s3h::kPairThreads), 0, stream, A);
   else if (P->kernel == S3H_KERNEL_SKEWP)
@@ -375,7 +385,9 @@ DualMode dual_mode(const s3h_plan_s* S, const s3h_plan_s* M, uint64_t b0, uint64
   const uint64_t cus = uint64_t(device_cus(S->device));
   if (S->kernel == S3H_KERNEL_SKEW && S->quad_waves == 1 && S->grid + M->grid <= cus)
     return kDualSplit;
-  if (S->kernel == S3H_KERNEL_SKEWP && S->grid <= cus) return kDualGroup;
+  // the group kernel runs skewp geometry: 32 parts per workgroup, like the shared-SIMD kernel
+  if ((S->kernel == S3H_KERNEL_SKEWP || S->kernel == S3H_KERNEL_SKEWS) && S->grid <= cus)
+    return kDualGroup;
   return kDualNone;
 }
 
@@ -1060,7 +1072,8 @@ int s3h_plan_launch_range(s3h_plan_t P, const void* d_base, uint32_t* d_digests,
 
 // Consumer waves (= groups) of a skew/skewp grid; 0 for the kernels without a clock probe.
 static uint32_t consumer_groups(const s3h_plan_s* P) {
-  return P->kernel == S3H_KERNEL_SKEW && P->quad_waves == 2 ? uint32_t((P->n + 7) / 8)
+  return (P->kernel == S3H_KERNEL_SKEW && P->quad_waves == 2) || P->kernel == S3H_KERNEL_SKEWS
+             ? uint32_t((P->n + 7) / 8)
          : P->kernel == S3H_KERNEL_SKEW || P->kernel == S3H_KERNEL_SKEWP ? P->grid
                                                                           : 0u;
 }

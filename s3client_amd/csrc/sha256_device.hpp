@@ -132,6 +132,11 @@ __device__ __forceinline__ uint32_t be_selector(uint32_t sh) {
   return ((sh) << 24) | ((sh + 1) << 16) | ((sh + 2) << 8) | (sh + 3);
 }
 
+// v_perm selector turning {d[j+1]:d[j]} into the little-endian word at byte shift `sh`.
+__device__ __forceinline__ uint32_t le_selector(uint32_t sh) {
+  return ((sh + 3) << 24) | ((sh + 2) << 16) | ((sh + 1) << 8) | sh;
+}
+
 __device__ __forceinline__ void decode_full(const RawBlock& r, uint32_t sel, uint32_t w[16]) {
 #pragma unroll
   for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_perm(r.d[j + 1], r.d[j], sel);

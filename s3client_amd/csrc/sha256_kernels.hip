@@ -715,7 +715,58 @@ __device__ __forceinline__ void flag_wait_ge(uint32_t* f, uint32_t v, bool& aliv
   }
 }
 
-template <int NC, bool PAIR, bool FLAGS>
+#ifdef S3H_EXP_PRODUCER_INC  // tools/ experiment builds only: another generated producer
+#include S3H_EXP_PRODUCER_INC
+#else
+#include "sha256_producer_simple.inc"
+#endif
+
+// The same for a producer that shares its consumer's SIMD (sha256_skew_shared_kernel): that
+// SIMD issues a second wave's v_add_u32, v_xor/or/and_b32 and v_lshrrev_b32 beside the round
+// stream at the lone-wave rate, but not its left shifts, alignbit, perm or add3
+// (tools/ubench_coissue2.hip, profiles/r02_ubench_coissue_*.txt).  The block's byte swap and
+// schedule are therefore one generated asm statement in those classes (tools/gen_producer.py:
+// left shifts as doublings), fed the block's 16 words as little-endian dwords: the raw loads
+// when every lane of the wave reads dword-aligned parts (`aligned`), one v_perm per word
+// otherwise, and the padded tail block (once per part) byte-swapped back with v_perm.
+template <int kRow>
+__device__ __forceinline__ void produce_block_simple(const RawBlock& r, uint32_t sel,
+                                                     const uint8_t* bp, uint64_t len, uint64_t bits,
+                                                     uint64_t blk, uint64_t limit, bool aligned,
+                                                     uint4 (*buf)[kRow], uint32_t lane) {
+  static_assert(kRow * 16 == 144, "tools/gen_producer.py ROW");
+  uint32_t w[16];
+  if (blk >= limit) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = 0;
+  } else if (blk < (len >> 6)) {
+    if (aligned) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = r.d[j];
+    } else {
+      const uint32_t le = le_selector(sel >> 24);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_perm(r.d[j + 1], r.d[j], le);
+    }
+  } else {
+    build_tail(bp, len, bits, blk, w);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
+  }
+  typedef __attribute__((address_space(3))) uint4 lds_uint4;
+  const uint32_t la = uint32_t(reinterpret_cast<uintptr_t>((lds_uint4*)(&buf[0][lane])));
+  uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4], w5 = w[5], w6 = w[6], w7 = w[7],
+           w8 = w[8], w9 = w[9], w10 = w[10], w11 = w[11], w12 = w[12], w13 = w[13], w14 = w[14],
+           w15 = w[15];
+  S3H_PROD_SIMPLE_TEMPS
+  const uint32_t bsel = 0x00010203u;  // v_perm byte swap (tools/gen_producer.py --perm-bswap only)
+  asm volatile(S3H_ALIGN8 S3H_PROD_SIMPLE_ASM : S3H_PROD_SIMPLE_OUTS : [la] "v"(la), [bsel] "v"(bsel)
+               : "memory");
+}
+
+// SIMPLE: the producer is written in the co-issuable instruction classes (it shares its
+// consumer's SIMD: sha256_skew_shared_kernel).
+template <int NC, bool PAIR, bool FLAGS, bool SIMPLE = false>
 __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t group,
                                           const uint32_t role, SkewLds<NC, PAIR>& L,
                                           uint32_t* flags) {
@@ -767,6 +818,15 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
       bh[r] = b0 + h[r];
       bits[r] = slot < A.n ? msg_bits(A, slot, s.len) : 0;
     }
+    // SIMPLE: every lane's part starts dword-aligned (wave-uniform: the s_bswap decode)
+    const bool aligned = SIMPLE && __all(sel[0] == 0x00010203u);
+#define S3H_PRODUCE(RAW, R, BP, BLK, BUF)                                                      \
+  do {                                                                                         \
+    if constexpr (SIMPLE)                                                                      \
+      produce_block_simple(RAW, sel[R], BP, len[R], bits[R], BLK, A.blk_end, aligned, BUF, part[R]); \
+    else                                                                                       \
+      produce_block(RAW, sel[R], BP, len[R], bits[R], BLK, A.blk_end, BUF, part[R]);           \
+  } while (0)
     constexpr uint64_t kStride = 64ull * kBps;
     RawBlock ra[kItems], rb[kItems];
 #pragma unroll
@@ -775,8 +835,7 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
       fetch_full(p[r] + kStride, bh[r] + kBps < fend[r], A.zero, rb[r]);
     }
 #pragma unroll
-    for (uint32_t r = 0; r < kItems; ++r)
-      produce_block(ra[r], sel[r], p[r], len[r], bits[r], bh[r], A.blk_end, lds_wk[0][h[r]], part[r]);
+    for (uint32_t r = 0; r < kItems; ++r) S3H_PRODUCE(ra[r], r, p[r], bh[r], lds_wk[0][h[r]]);
     S3H_SYNC_PRODUCED(1u);
     // Step k goes into buffer k & 1, which held step k - 2: FLAGS waits until the consumer
     // has released that step (the barrier of the other mode orders the same thing).
@@ -788,8 +847,7 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
         S3H_PROD_UNROLL
         for (uint32_t r = 0; r < kItems; ++r) {
           fetch_full(p[r] + kStride * (k + 1), bh[r] + kBps * (k + 1) < fend[r], A.zero, ra[r]);
-          produce_block(rb[r], sel[r], p[r] + kStride * k, len[r], bits[r], bh[r] + kBps * k,
-                        A.blk_end, lds_wk[1][h[r]], part[r]);
+          S3H_PRODUCE(rb[r], r, p[r] + kStride * k, bh[r] + kBps * k, lds_wk[1][h[r]]);
         }
       }
       S3H_SYNC_PRODUCED(uint32_t(k + 1));
@@ -799,14 +857,14 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
         S3H_PROD_UNROLL
         for (uint32_t r = 0; r < kItems; ++r) {
           fetch_full(p[r] + kStride * (k + 2), bh[r] + kBps * (k + 2) < fend[r], A.zero, rb[r]);
-          produce_block(ra[r], sel[r], p[r] + kStride * (k + 1), len[r], bits[r],
-                        bh[r] + kBps * (k + 1), A.blk_end, lds_wk[0][h[r]], part[r]);
+          S3H_PRODUCE(ra[r], r, p[r] + kStride * (k + 1), bh[r] + kBps * (k + 1), lds_wk[0][h[r]]);
         }
       }
       S3H_SYNC_PRODUCED(uint32_t(k + 2));
     }
     return;
   }
+#undef S3H_PRODUCE
 #undef S3H_SYNC_PRODUCED
   // ------------------------------------------------------------------ consumer
 #ifdef S3H_EXP_LONE_CONSUMER  // experiment: only consumer wave 0 works (wrong digests)
@@ -1034,6 +1092,23 @@ __global__ __launch_bounds__(256) void sha256_skew_pairs_kernel(LaunchArgs A) {
                             flags[g]);
 }
 
+// Four (consumer, producer) groups per workgroup with every producer on its consumer's SIMD:
+// waves 0-3 consume groups 4b..4b+3, waves 4-7 produce for them, and a workgroup's wave w runs
+// on SIMD w % 4 (HW_ID, tools/ubench_coissue*.hip), so wave g + 4 shares wave g's SIMD.  The
+// producer is written in the instruction classes that SIMD issues beside the round stream
+// (skew_body SIMPLE), so one CU runs 32 chains at about the skew kernel's per-chain speed --
+// four times the chains of sha256_skew_kernel<1> per CU, without skewp's extra VALU per round.
+// LDS: 4 x 36 KiB = one workgroup per CU.
+__global__ __launch_bounds__(512) void sha256_skew_shared_kernel(LaunchArgs A) {
+  __shared__ SkewLds<1, false> L[4];
+  __shared__ uint32_t flags[4][2];
+  if (threadIdx.x < 8) flags[threadIdx.x >> 1][threadIdx.x & 1] = 0;
+  __syncthreads();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t g = wave & 3u;
+  skew_body<1, false, true, true>(A, 4 * blockIdx.x + g, wave >> 2, L[g], flags[g]);
+}
+
 // ------------------------------------------------------------- MD5 (producer/consumer)
 // Batched MD5 for Content-MD5 / multipart-ETag verification (reference
 // lib/hash/md5.cpp:71-116 for the step function, :158-172 for the padding).  Same
@@ -1041,9 +1116,6 @@ __global__ __launch_bounds__(256) void sha256_skew_pairs_kernel(LaunchArgs A) {
 // handles alignment), pads (64-bit LITTLE-endian bit length) and writes M[g(i)] + K[i] for
 // the 64 steps to LDS; the consumer runs the chain: per step one bitop3 (F/G/H/I), one add3,
 // one alignbit (rotate left) and one add.  State words are the digest words (no byte swap).
-__device__ __forceinline__ uint32_t le_selector(uint32_t sh) {
-  return ((sh + 3) << 24) | ((sh + 2) << 16) | ((sh + 1) << 8) | sh;
-}
 
 __device__ __forceinline__ void md5_tail(const uint8_t* p, uint64_t len, uint64_t bits,
                                          uint64_t blk, uint32_t w[16]) {

@@ -2,7 +2,7 @@
 
 C3 (configs[2]): 4096 parts of U[5,64] MiB (~138 GiB resident in HBM), AUTO -> the two-group
 skew kernel with solo workgroups for the longest parts (grid > 256: capi.hip plan_solo).  C4 (configs[3]): rank 0's shard of 65,536 x 8 MiB over
-8 GPUs -- global parts p = 8k, 8,192 x 8 MiB = 64 GiB -- AUTO -> skewp.  Each batch is checked
+8 GPUs -- global parts p = 8k, 8,192 x 8 MiB = 64 GiB -- AUTO -> skews (and skewp, compared).  Each batch is checked
 against (i) the lib/hash golden digests of the parts that have fixtures (tests/golden: C3 ids
 incl. the longest and shortest part, C4 ids of rank 0) and (ii) the oracle on 64 randomly
 chosen parts copied back from HBM.  Bar: bit-exact."""
@@ -74,11 +74,16 @@ def test_c4_rank0_shard(torch_cuda, oracle, golden):
     data = torch.empty(per * L, dtype=torch.uint8, device="cuda")     # 64 GiB
     try:
         s3.generate_parts(data, offs, lens, ids, SEED)
-        with s3.Plan(offs, lens) as plan:
-            assert plan.info()["kernel"] == "skewp"
+        with s3.Plan(offs, lens) as plan:  # AUTO: shared-SIMD producers, one workgroup per CU
+            assert plan.info()["kernel"] == "skews" and plan.info()["grid"] == per // 32
             out = torch.empty((per, 8), dtype=torch.int32, device="cuda")
             plan.launch(data, out)
             torch.cuda.synchronize()
+        with s3.Plan(offs, lens, kernel="skewp") as plan:  # the lane-pair kernel, same parts
+            out2 = torch.empty((per, 8), dtype=torch.int32, device="cuda")
+            plan.launch(data, out2)
+            torch.cuda.synchronize()
+        assert torch.equal(out, out2)
         got = out.cpu().numpy().view(np.uint32)
         txt = s3.digests_to_text(got)
         fx = [e for e in golden["c2_parts"] + golden["c4_parts"] if e["p"] % world == rank]

@@ -11,7 +11,7 @@ import s3client_amd as s3
 
 pytestmark = pytest.mark.gpu
 SEED = 20241008
-KERNELS = ["skew", "skewp", "quad", "pair", "pc", "lane"]
+KERNELS = ["skew", "skewp", "skews", "quad", "pair", "pc", "lane"]
 
 
 def _dev_buffer(torch, host: np.ndarray):
@@ -69,6 +69,8 @@ def test_kernels_agree_on_many_small_parts(torch_cuda, oracle):
     assert s3.Plan([0] * 40000, [1] * 40000).info()["kernel"] == "pc"
     assert s3.Plan([0] * 1024, [1] * 1024).info()["kernel"] == "skew"
     assert s3.Plan([0] * 10000, [1] * 10000).info()["kernel"] == "skewp"
+    assert s3.Plan([0] * 8192, [1] * 8192).info()["kernel"] == "skews"
+    assert s3.Plan([0] * 4097, [1] * 4097).info()["kernel"] == "skews"
     assert s3.Plan([0] * 30000, [1] * 30000).info()["kernel"] == "pair"
     rng = np.random.default_rng(7)
     n = 70000
@@ -77,7 +79,7 @@ def test_kernels_agree_on_many_small_parts(torch_cuda, oracle):
     host = rng.integers(0, 256, (1 << 20) + 256, dtype=np.uint8)
     data = _dev_buffer(torch_cuda, host)
     a = s3.sha256_batch_device(data, offs, lens, kernel="auto").cpu().numpy().view(np.uint32)
-    for k in ("pc", "pair", "quad", "skew", "skewp"):
+    for k in ("pc", "pair", "quad", "skew", "skewp", "skews"):
         b = s3.sha256_batch_device(data, offs, lens, kernel=k).cpu().numpy().view(np.uint32)
         assert np.array_equal(a, b), k
     idx = rng.choice(n, 500, replace=False)
@@ -378,7 +380,7 @@ def test_dual_digest_group_kernel_device_and_host(torch_cuda, oracle):
     rl[:4] = [0, 55, 56, 64]
     ro = np.cumsum(rng.integers(0, 40, n) + np.concatenate([[0], rl[:-1]]))
     host = rng.integers(0, 256, int(ro[-1] + rl[-1]) + 8, dtype=np.uint8)
-    assert s3.Plan(ro, rl).info()["kernel"] == "skewp"
+    assert s3.Plan(ro, rl).info()["kernel"] == "skews"  # SHA-256 alone; both digests: group kernel
     sha, m5 = s3.sha256_md5_batch_device(_dev_buffer(torch_cuda, host), ro, rl)
     assert np.array_equal(sha.cpu().numpy().view(np.uint32), oracle.batch(host, ro, rl))
     assert np.array_equal(m5.cpu().numpy().view(np.uint32), oracle.md5_batch(host, ro, rl))
@@ -388,7 +390,7 @@ def test_dual_digest_group_kernel_device_and_host(torch_cuda, oracle):
     assert np.array_equal(m5, np.stack([oracle.md5(p.tobytes()) for p in parts]))
 
 
-@pytest.mark.parametrize("n,kernel", [(3000, "skew"), (5000, "skewp")])
+@pytest.mark.parametrize("n,kernel", [(3000, "skew"), (5000, "skewp"), (5000, "skews")])
 def test_flag_synchronised_kernels_resumable(torch_cuda, oracle, n, kernel):
     """The two-group skew kernel (2,049-4,096 parts) and skewp: resumable ranged launches of
     odd block counts == one launch == the oracle (the step counters restart per launch)."""

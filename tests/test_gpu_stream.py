@@ -11,7 +11,7 @@ import pytest
 import s3client_amd as s3
 
 pytestmark = pytest.mark.gpu
-KERNELS = ["skew", "skewp", "quad", "pair", "pc", "lane"]
+KERNELS = ["skew", "skewp", "skews", "quad", "pair", "pc", "lane"]
 
 
 def _schedule(rng, n, rounds, maxlen):

@@ -1,0 +1,81 @@
+"""CPU checks of the shared-SIMD producer (tools/gen_producer.py), the asm statement that
+sha256_skew_shared_kernel's producer wave runs per block: simulated on one lane, its W[t]+K[t]
+drive a plain 64-round compression to hashlib's digest for multi-block messages; the
+committed .inc is the generator's output; and it uses only the instruction classes a SIMD
+issues beside the consumer's round stream (no left shift, alignbit, perm, add3: those would
+stall it -- profiles/r02_ubench_coissue_classes.txt)."""
+import hashlib
+import os
+import random
+import re
+import struct
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import gen_producer  # noqa: E402
+
+M32 = 0xFFFFFFFF
+IV = [0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19]
+
+
+def _rotr(x, n):
+    return ((x >> n) | (x << (32 - n))) & M32
+
+
+def _compress(h, wk):
+    a, b, c, d, e, f, g, hh = h
+    for t in range(64):
+        t1 = (hh + (_rotr(e, 6) ^ _rotr(e, 11) ^ _rotr(e, 25)) + ((e & f) ^ (~e & g)) + wk[t]) & M32
+        t2 = ((_rotr(a, 2) ^ _rotr(a, 13) ^ _rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c))) & M32
+        a, b, c, d, e, f, g, hh = (t1 + t2) & M32, a, b, c, (d + t1) & M32, e, f, g
+    return [(x + y) & M32 for x, y in zip(h, [a, b, c, d, e, f, g, hh])]
+
+
+def _padded(msg):
+    return msg + b"\x80" + b"\0" * ((55 - len(msg)) % 64) + struct.pack(">Q", 8 * len(msg))
+
+
+@pytest.mark.parametrize("n", [0, 3, 55, 56, 64, 119, 200, 1000])
+def test_producer_drives_compression_to_hashlib(n):
+    rng = random.Random(n)
+    msg = bytes(rng.randrange(256) for _ in range(n))
+    p = _padded(msg)
+    h = IV
+    for i in range(0, len(p), 64):
+        blk = p[i:i + 64]
+        le = [int.from_bytes(blk[4 * j:4 * j + 4], "little") for j in range(16)]  # as loaded
+        out = gen_producer.simulate(le)
+        assert len(out) == 64
+        h = _compress(h, [out[(t // 4) * gen_producer.ROW + (t % 4) * 4] for t in range(64)])
+    assert h == list(struct.unpack(">8I", hashlib.sha256(msg).digest()))
+
+
+def test_committed_inc_is_generated(tmp_path):
+    out = tmp_path / "p.inc"
+    gen_producer.emit_inc(str(out))
+    with open(os.path.join(ROOT, "s3client_amd", "csrc", "sha256_producer_simple.inc")) as f:
+        assert f.read() == out.read_text()
+
+
+def test_only_coissuable_instruction_classes():
+    with open(os.path.join(ROOT, "s3client_amd", "csrc", "sha256_producer_simple.inc")) as f:
+        ops = re.findall(r'"([a-z_0-9]+) ', f.read())
+    allowed = {"v_add_u32", "v_xor_b32", "v_or_b32", "v_and_b32", "v_lshrrev_b32", "v_bitop3_b32",
+               "ds_write_b32", "s_waitcnt"}
+    assert set(ops) <= allowed, set(ops) - allowed
+    # doublings dominate: every left shift of the schedule and the byte swap is v_add_u32 x, x
+    assert ops.count("v_add_u32") > 1800 and ops.count("ds_write_b32") == 64
+
+
+@pytest.mark.parametrize("variant", [{"perm": True}, {"lds": True}])
+def test_experiment_variants_compute_the_same_schedule(variant):
+    """The v_perm and LDS-pipe byte-swap variants (experiments, profiles/r02_exp_producer_*)."""
+    rng = random.Random(9)
+    for _ in range(10):
+        blk = bytes(rng.randrange(256) for _ in range(64))
+        le = [int.from_bytes(blk[4 * j:4 * j + 4], "little") for j in range(16)]
+        out = gen_producer.simulate(le, **variant)
+        assert [out[gen_producer.wk_offset(t)] for t in range(64)] == gen_producer.reference_wk(blk)

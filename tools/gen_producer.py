@@ -1,0 +1,269 @@
+#!/usr/bin/env python3
+"""Generator (and simulator) of the SIMPLE-class SHA-256 message-schedule producer.
+
+A producer wave that shares its consumer's SIMD (sha256_skew_shared_kernel) only gets issue
+slots for the instruction classes the SIMD runs beside the consumer's round stream:
+v_add_u32, v_xor/or/and_b32, v_lshrrev_b32 (and, most of the time, v_bitop3_b32) -- not left
+shifts, alignbit, perm, add3 (tools/ubench_coissue2.hip, profiles/r02_ubench_coissue_*.txt).
+This module emits ONE block's producer work in those classes as a single asm statement:
+
+    in : w0..w15 = the block's 16 message dwords as loaded (little-endian bytes; the asm
+         byte-swaps them), la = this lane's LDS address of W+K row 0 of its (buffer, block, part)
+    out: 64 x ds_write_b32 of W[t] + K[t] at la + (t / 4) * ROW + (t % 4) * 4
+
+    bswap(x)   = x >> 24 | (x >> 8) & 0xff00 | (x << 8) & 0xff0000 | x << 24
+    sigma0(x)  = (x >> 7 ^ x >> 18 ^ x >> 3) ^ L0(x),  L0(x) = x << 25 ^ x << 14
+    sigma1(y)  = (y >> 17 ^ y >> 19 ^ y >> 10) ^ L1(y), L1(y) = y << 15 ^ y << 13
+
+with every left shift made of doublings (v_add_u32 x, x, x): per word d13 = x << 13 (13),
+d14 = 2 d13, d15 = 2 d14, d25 = 2^10 d15; L1 = d15 ^ d13 (words 14..61), L0 = d25 ^ d14
+(words 1..48).  Word t's doubling chain is interleaved with word t+1's expansion (one
+instruction each, alternately) so that no instruction waits on the one before it.
+
+Registers: W ring w[t % 16] (the inputs), L0 ring l0_[t % 16], L1 ring l1_[t % 4], doubling
+temporaries c0-c2, expansion / byte-swap temporaries s0-s3, W+K ring k[t % 8] (a value is
+rewritten 8 words after its ds_write).
+
+`emit_inc` writes s3client_amd/csrc/sha256_producer_simple.inc; `simulate` runs the same op
+list on Python integers (tests/test_producer_schedule.py checks it against hashlib-derived
+W+K and the instruction classes).
+"""
+import argparse
+import os
+
+M32 = 0xFFFFFFFF
+K256 = [
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2]
+ROW = 9 * 16   # bytes between W+K rows in LDS: SkewLds<1,false> row = kCols (9) x uint4
+
+W = [f"w{i}" for i in range(16)]
+L0 = [f"l0_{i}" for i in range(16)]
+L1 = [f"l1_{i}" for i in range(4)]
+KR = [f"k{i}" for i in range(8)]
+TEMPS = ["c0", "c1", "c2", "c3", "c4", "c5", "s0", "s1", "s2", "s3"]
+# op tuples: ("add", d, a, b) ("xor", d, a, b) ("or", d, a, b) ("and", d, a, imm)
+#            ("shr", d, imm, a) ("xor3", d, a, b, c) ("addk", d, a, imm) ("dsw", src, offset)
+SIMPLE_OPS = {"add", "xor", "or", "and", "shr", "addk"}   # bitop3 (xor3) is the partial class
+
+
+def lefts(t):
+    """Doublings of word t and its L1 (words 14..61) / L0 (words 1..48); temporaries c0-c2 for
+    even words, c3-c5 for odd ones (two consecutive words' chains may interleave)."""
+    need0, need1 = 1 <= t <= 48, 14 <= t <= 61
+    if not (need0 or need1):
+        return []
+    x = W[t % 16]
+    a, b, c = ("c0", "c1", "c2") if t % 2 == 0 else ("c3", "c4", "c5")
+    ops = [("add", a, x, x)] + [("add", a, a, a)] * 12                    # d13
+    ops += [("add", b, a, a), ("add", c, b, b)]                           # d14, d15
+    if need1:
+        ops.append(("xor", L1[t % 4], c, a))
+    if need0:
+        ops += [("add", a, c, c)] + [("add", a, a, a)] * 9                 # d25
+        ops.append(("xor", L0[t % 16], a, b))
+    return ops
+
+
+def wk_offset(t):
+    return (t // 4) * ROW + (t % 4) * 4
+
+
+def lds_bswap():
+    """EXPERIMENT (--lds-bswap; slower, not shipped): byte swap of the 16 loaded words on the
+    LDS pipe: each word's bytes written in reverse order (ds_write_b8 writes bits 7:0,
+    ds_write_b8_d16_hi bits 23:16; x >> 8 supplies the other two) into this lane's own W+K rows
+    0-3 and read back as one dword -- 16 VALU instead of ~400.  Measured on the C4 shard:
+    2,435 vs 2,245 cycles/block (profiles/r02_exp_producer_bswap.jsonl): the producer's 64
+    lanes are 8 blocks x 8 parts and the blocks lie 576 dwords apart (= 0 mod 64 banks), so
+    every byte write is an 8-way bank conflict and the extra 80 LDS ops per block saturate the
+    LDS pipe the consumers read from."""
+    ops = [("shr", L0[j], 8, W[j]) for j in range(16)]
+    for j in range(16):
+        o = wk_offset(j)
+        ops += [("dsw8", W[j], o + 3), ("dsw8hi", W[j], o + 1), ("dsw8", L0[j], o + 2),
+                ("dsw8hi", L0[j], o)]
+    ops += [("dsr", W[j], wk_offset(j)) for j in range(16)]
+    ops.append(("wait",))
+    return ops
+
+
+def bswap(t, perm=False):
+    """w[t] (little-endian load) -> big-endian word, in place (perm: one v_perm_b32, which the
+    shared SIMD issues only in the consumer's non-VALU cycles)."""
+    x = W[t]
+    if perm:
+        return [("perm", x, x)]
+    return ([("add", "s0", x, x)] + [("add", "s0", "s0", "s0")] * 7 +      # s0 = x << 8
+            [("add", "s1", "s0", "s0")] + [("add", "s1", "s1", "s1")] * 15 +   # s1 = x << 24
+            [("and", "s0", "s0", 0xFF0000), ("shr", "s2", 24, x), ("or", "s0", "s0", "s1"),
+             ("shr", "s3", 8, x), ("and", "s3", "s3", 0xFF00), ("or", "s2", "s2", "s3"),
+             ("or", x, "s0", "s2")])
+
+
+def expansion(t):
+    """W[t] = sigma1(W[t-2]) + W[t-7] + sigma0(W[t-15]) + W[t-16], t >= 16."""
+    x, y = W[(t - 15) % 16], W[(t - 2) % 16]
+    return [("shr", "s0", 7, x), ("shr", "s1", 18, x), ("shr", "s2", 3, x),
+            ("xor3", "s0", "s0", "s1", "s2"), ("xor", "s0", "s0", L0[(t - 15) % 16]),
+            ("shr", "s1", 17, y), ("shr", "s2", 19, y), ("shr", "s3", 10, y),
+            ("xor3", "s1", "s1", "s2", "s3"), ("xor", "s1", "s1", L1[(t - 2) % 4]),
+            ("add", "s0", "s0", "s1"), ("add", "s1", W[(t - 7) % 16], W[t % 16]),
+            ("add", W[t % 16], "s0", "s1")]
+
+
+def merge(a, b):
+    out = []
+    for i in range(max(len(a), len(b))):
+        if i < len(a):
+            out.append(a[i])
+        if i < len(b):
+            out.append(b[i])
+    return out
+
+
+def block_ops(perm=False, lds=False):
+    """lds: byte swap on the LDS pipe (lds_bswap); otherwise in VALU doublings (or v_perm)."""
+    ops = lds_bswap() if lds else []
+    for t in range(64):
+        if lds and t < 16:
+            # no expansion yet: words 1..14's doubling chains interleave pairwise
+            if t % 2 == 0 and 2 <= t <= 14:
+                ops += merge(lefts(t - 1), lefts(t))
+        else:
+            e = bswap(t, perm) if t < 16 else expansion(t)
+            ops += merge(lefts(t - 1) if t >= 1 else [], e)
+        ops += [("addk", KR[t % 8], W[t % 16], K256[t]), ("dsw", KR[t % 8], wk_offset(t))]
+    return ops
+
+
+def asm_text(ops):
+    lines = []
+    for op in ops:
+        k = op[0]
+        if k == "add":
+            lines.append(f"v_add_u32 %[{op[1]}], %[{op[2]}], %[{op[3]}]")
+        elif k == "xor":
+            lines.append(f"v_xor_b32 %[{op[1]}], %[{op[2]}], %[{op[3]}]")
+        elif k == "or":
+            lines.append(f"v_or_b32 %[{op[1]}], %[{op[2]}], %[{op[3]}]")
+        elif k == "and":
+            lines.append(f"v_and_b32 %[{op[1]}], 0x{op[3]:x}, %[{op[2]}]")
+        elif k == "shr":
+            lines.append(f"v_lshrrev_b32 %[{op[1]}], {op[2]}, %[{op[3]}]")
+        elif k == "xor3":
+            lines.append(f"v_bitop3_b32 %[{op[1]}], %[{op[2]}], %[{op[3]}], %[{op[4]}] bitop3:0x96")
+        elif k == "addk":
+            lines.append(f"v_add_u32 %[{op[1]}], 0x{op[3]:08x}, %[{op[2]}]")
+        elif k == "dsw":
+            lines.append(f"ds_write_b32 %[la], %[{op[1]}] offset:{op[2]}")
+        elif k == "perm":
+            lines.append(f"v_perm_b32 %[{op[1]}], %[{op[2]}], %[{op[2]}], %[bsel]")
+        elif k == "dsw8":
+            lines.append(f"ds_write_b8 %[la], %[{op[1]}] offset:{op[2]}")
+        elif k == "dsw8hi":
+            lines.append(f"ds_write_b8_d16_hi %[la], %[{op[1]}] offset:{op[2]}")
+        elif k == "dsr":
+            lines.append(f"ds_read_b32 %[{op[1]}], %[la] offset:{op[2]}")
+        elif k == "wait":
+            lines.append("s_waitcnt lgkmcnt(0)")
+        else:
+            raise ValueError(op)
+    lines.append("s_waitcnt lgkmcnt(0)")
+    return lines
+
+
+def simulate(words_le, ops=None, perm=False, lds=False):
+    """Run the op list on one lane: words_le = 16 little-endian-loaded dwords; returns
+    {byte offset: value} of the W+K ds_write_b32s.  LDS is simulated bytewise (initially junk)."""
+    regs = {W[i]: words_le[i] & M32 for i in range(16)}
+    out = {}
+    mem = bytearray(b"\xa5" * (16 * ROW))
+    for op in ops or block_ops(perm, lds):
+        k = op[0]
+        g = lambda r: regs[r]
+        if k == "add":
+            regs[op[1]] = (g(op[2]) + g(op[3])) & M32
+        elif k == "xor":
+            regs[op[1]] = g(op[2]) ^ g(op[3])
+        elif k == "or":
+            regs[op[1]] = g(op[2]) | g(op[3])
+        elif k == "and":
+            regs[op[1]] = g(op[2]) & op[3]
+        elif k == "shr":
+            regs[op[1]] = g(op[3]) >> op[2]
+        elif k == "xor3":
+            regs[op[1]] = g(op[2]) ^ g(op[3]) ^ g(op[4])
+        elif k == "addk":
+            regs[op[1]] = (g(op[2]) + op[3]) & M32
+        elif k == "dsw":
+            out[op[2]] = regs[op[1]]
+            mem[op[2]:op[2] + 4] = regs[op[1]].to_bytes(4, "little")
+        elif k == "dsw8":
+            mem[op[2]] = regs[op[1]] & 0xFF
+        elif k == "dsw8hi":
+            mem[op[2]] = (regs[op[1]] >> 16) & 0xFF
+        elif k == "dsr":
+            regs[op[1]] = int.from_bytes(mem[op[2]:op[2] + 4], "little")
+        elif k == "perm":
+            regs[op[1]] = int.from_bytes(g(op[2]).to_bytes(4, "little"), "big")
+    return out
+
+
+def reference_wk(block: bytes):
+    """FIPS 180-4 schedule: W[t] + K[t] of one 64-byte block (sha256.cpp:116-123)."""
+    rotr = lambda x, n: ((x >> n) | (x << (32 - n))) & M32
+    w = [int.from_bytes(block[4 * i:4 * i + 4], "big") for i in range(16)]
+    for t in range(16, 64):
+        s0 = rotr(w[t - 15], 7) ^ rotr(w[t - 15], 18) ^ (w[t - 15] >> 3)
+        s1 = rotr(w[t - 2], 17) ^ rotr(w[t - 2], 19) ^ (w[t - 2] >> 10)
+        w.append((w[t - 16] + s0 + w[t - 7] + s1) & M32)
+    return [(w[t] + K256[t]) & M32 for t in range(64)]
+
+
+def emit_inc(path, perm=False, lds=False):
+    ops = block_ops(perm, lds)
+    body = asm_text(ops)
+    n_valu = sum(1 for o in ops if not o[0].startswith(("ds", "wait")))
+    n_lds = sum(1 for o in ops if o[0].startswith("ds"))
+    hdr = [
+        "// GENERATED by tools/gen_producer.py -- do not edit.  One block of the SIMPLE-class",
+        "// SHA-256 message-schedule producer (byte swap, sigma0/sigma1 with left shifts as",
+        f"// doublings, W+K to LDS): {n_valu} VALU + {n_lds} LDS instructions.",
+        "#pragma once",
+        "#define S3H_PROD_SIMPLE_ASM \\",
+    ]
+    lines = [f'  "{l}\\n\\t" \\' for l in body]
+    lines[-1] = lines[-1][:-2]
+    decl = ("#define S3H_PROD_SIMPLE_TEMPS uint32_t " + ", ".join(L0 + L1 + KR + TEMPS) + ";")
+    outs = ", ".join([f'[{r}] "+v"({r})' for r in W] + [f'[{r}] "=&v"({r})' for r in L0 + L1 + KR + TEMPS])
+    with open(path, "w") as f:
+        f.write("\n".join(hdr + lines) + "\n\n")
+        f.write(decl + "\n")
+        f.write(f"#define S3H_PROD_SIMPLE_OUTS {outs}\n")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "s3client_amd",
+                                                  "csrc", "sha256_producer_simple.inc"))
+    ap.add_argument("--perm-bswap", action="store_true", help="byte swap with v_perm (experiment)")
+    ap.add_argument("--lds-bswap", action="store_true", help="byte swap on the LDS pipe (experiment)")
+    args = ap.parse_args()
+    lds = args.lds_bswap
+    emit_inc(args.out, args.perm_bswap, lds)
+    ops = block_ops(args.perm_bswap, lds)
+    kinds = {}
+    for o in ops:
+        kinds[o[0]] = kinds.get(o[0], 0) + 1
+    print(f"wrote {args.out}: {len(ops)} ops {kinds}")
+
+
+if __name__ == "__main__":
+    main()

@@ -23,6 +23,7 @@ KERNELS = {
     "skew": ("_ZN3s3h18sha256_skew_kernelILi1ELb0EEEvNS_10LaunchArgsE", 8),
     "skew_nc2": ("_ZN3s3h24sha256_skew_pairs_kernelENS_10LaunchArgsE", 8),
     "skewp": ("_ZN3s3h18sha256_skew_kernelILi1ELb1EEEvNS_10LaunchArgsE", 4),
+    "skews": ("_ZN3s3h25sha256_skew_shared_kernelENS_10LaunchArgsE", 8),
 }
 INSTR = re.compile(r"^\t([a-z_][a-z0-9_]*)")
 LABEL = re.compile(r"^[0-9a-f]+ <(L[0-9]+)>:")
