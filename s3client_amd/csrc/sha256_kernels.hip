@@ -32,6 +32,9 @@
 
 // Compile-time experiment parameters (tools/ builds only: `make exp`; the product build uses
 // these defaults).
+#ifndef S3H_EXP_SKEW_BLK_PAD
+#define S3H_EXP_SKEW_BLK_PAD 0  // skew layout: uint4 of LDS padding per block (SkewGeom)
+#endif
 #ifndef S3H_EXP_SKEW_BPS_NC2
 #define S3H_EXP_SKEW_BPS_NC2 8  // skew NC=2: blocks per producer step
 #endif
@@ -690,10 +693,17 @@ struct SkewGeom {
   // fewer for wider groups, whose producer would spill.
   static constexpr uint32_t kBps = PAIR ? 4 : NC >= 4 ? 2 : NC == 2 ? S3H_EXP_SKEW_BPS_NC2 : 8;
   static constexpr uint32_t kCols = kParts + 1;  // column kParts holds ones (read by the a-quads)
+  // uint4s of padding after each block's 16 rows (skew layout).  A block is 16 x 9 uint4 =
+  // 576 dwords = 0 mod 64 banks, so the producer's lanes (8 parts x 8 blocks) write each W+K
+  // word 8-way bank-conflicted; 8 uint4 (128 B) would halve that, but the C4 shard runs the same
+  // 2,243.6 cycles/block either way (profiles/r02_exp_skews_lds.jsonl): kept at 0.
+  static constexpr uint32_t kBlkPad = PAIR ? 0 : S3H_EXP_SKEW_BLK_PAD;
+  static constexpr uint32_t kBlkStride = 16 * kCols + kBlkPad;  // uint4 between blocks
 };
+// wk[buffer][block of the step][row * kCols + part] (+ kBlkPad after each block)
 template <int NC, bool PAIR>
 struct SkewLds {
-  uint4 wk[2][SkewGeom<NC, PAIR>::kBps][16][SkewGeom<NC, PAIR>::kCols];
+  uint4 wk[2][SkewGeom<NC, PAIR>::kBps][SkewGeom<NC, PAIR>::kBlkStride];
 };
 
 constexpr uint32_t kFlagSpinLimit = 1u << 24;  // x s_sleep 1 (64 clocks): ~0.45 s
@@ -776,6 +786,8 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
   constexpr uint32_t kLanes = kParts * kBps;
   constexpr uint32_t kItems = kLanes / 64;  // == NC
   auto& lds_wk = L.wk;
+  // the 16 x kCols rows of block h of buffer b
+  auto rows = [&](uint32_t b, uint32_t h) { return reinterpret_cast<uint4 (*)[kCols]>(lds_wk[b][h]); };
   bool alive = true;  // FLAGS: false after a timed-out wait (flag_wait_ge)
   // FLAGS: flags[0] = producer steps published, flags[1] = consumer steps released
 #define S3H_SYNC_PRODUCED(m)                 \
@@ -797,7 +809,7 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
   if (role == NC) {
     // ---------------------------------------------------------------- producer
     for (uint32_t i = lane; i < 2 * kBps * 16; i += 64)
-      lds_wk[i / (kBps * 16)][(i / 16) % kBps][i % 16][kParts] = make_uint4(1u, 1u, 1u, 1u);
+      lds_wk[i / (kBps * 16)][(i / 16) % kBps][(i % 16) * kCols + kParts] = make_uint4(1u, 1u, 1u, 1u);
     // Item r of this lane = (part, block h of the step); consecutive lanes take consecutive
     // blocks of one part (coalesced 512-byte runs).
     const uint8_t* p[kItems];
@@ -835,7 +847,7 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
       fetch_full(p[r] + kStride, bh[r] + kBps < fend[r], A.zero, rb[r]);
     }
 #pragma unroll
-    for (uint32_t r = 0; r < kItems; ++r) S3H_PRODUCE(ra[r], r, p[r], bh[r], lds_wk[0][h[r]]);
+    for (uint32_t r = 0; r < kItems; ++r) S3H_PRODUCE(ra[r], r, p[r], bh[r], rows(0, h[r]));
     S3H_SYNC_PRODUCED(1u);
     // Step k goes into buffer k & 1, which held step k - 2: FLAGS waits until the consumer
     // has released that step (the barrier of the other mode orders the same thing).
@@ -847,7 +859,7 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
         S3H_PROD_UNROLL
         for (uint32_t r = 0; r < kItems; ++r) {
           fetch_full(p[r] + kStride * (k + 1), bh[r] + kBps * (k + 1) < fend[r], A.zero, ra[r]);
-          S3H_PRODUCE(rb[r], r, p[r] + kStride * k, bh[r] + kBps * k, lds_wk[1][h[r]]);
+          S3H_PRODUCE(rb[r], r, p[r] + kStride * k, bh[r] + kBps * k, rows(1, h[r]));
         }
       }
       S3H_SYNC_PRODUCED(uint32_t(k + 1));
@@ -857,7 +869,7 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
         S3H_PROD_UNROLL
         for (uint32_t r = 0; r < kItems; ++r) {
           fetch_full(p[r] + kStride * (k + 2), bh[r] + kBps * (k + 2) < fend[r], A.zero, rb[r]);
-          S3H_PRODUCE(ra[r], r, p[r] + kStride * (k + 1), bh[r] + kBps * (k + 1), lds_wk[0][h[r]]);
+          S3H_PRODUCE(ra[r], r, p[r] + kStride * (k + 1), bh[r] + kBps * (k + 1), rows(0, h[r]));
         }
       }
       S3H_SYNC_PRODUCED(uint32_t(k + 2));
@@ -907,8 +919,8 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
   uint32_t q1, q2, q3, sl, cm, tt;
   // Per-lane LDS base (buffer 0, block 0, row 0, own column): block and buffer offsets are
   // immediates of the 16 ds_read_b128 that fetch one block's W+K.
-  const uint4* lbase = &lds_wk[0][0][0][ahalf ? kParts : part];
-  constexpr uint32_t kBlkStride = 16 * kCols, kBufStride = kBps * 16 * kCols;
+  const uint4* lbase = &lds_wk[0][0][ahalf ? kParts : part];
+  constexpr uint32_t kBlkStride = G::kBlkStride, kBufStride = kBps * G::kBlkStride;
   auto load = [&](uint32_t (&w)[64], const uint4* src) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {

@@ -80,10 +80,10 @@ def lds_bswap():
     LDS pipe: each word's bytes written in reverse order (ds_write_b8 writes bits 7:0,
     ds_write_b8_d16_hi bits 23:16; x >> 8 supplies the other two) into this lane's own W+K rows
     0-3 and read back as one dword -- 16 VALU instead of ~400.  Measured on the C4 shard:
-    2,435 vs 2,245 cycles/block (profiles/r02_exp_producer_bswap.jsonl): the producer's 64
-    lanes are 8 blocks x 8 parts and the blocks lie 576 dwords apart (= 0 mod 64 banks), so
-    every byte write is an 8-way bank conflict and the extra 80 LDS ops per block saturate the
-    LDS pipe the consumers read from."""
+    2,434 vs 2,244 cycles/block, with or without LDS padding that halves the producer's bank
+    conflicts (profiles/r02_exp_producer_bswap.jsonl, r02_exp_skews_lds.jsonl): the shader
+    clock rises (2.28 vs 2.18 GHz, fewer VALU) but the consumer's ds_reads, which it waits for
+    twice per block, queue behind the producer's 80 extra LDS ops."""
     ops = [("shr", L0[j], 8, W[j]) for j in range(16)]
     for j in range(16):
         o = wk_offset(j)
