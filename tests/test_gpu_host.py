@@ -155,3 +155,24 @@ def test_sharded_host_batch_on_repeated_device(torch_cuda, oracle):
     assert np.array_equal(s3.sha256_batch_host_on(parts[:2], [0, 0, 0, 0]), want[:2])
     with pytest.raises(s3.S3HashError):
         s3.sha256_batch_host_on(parts, [0, 99])
+
+
+def test_host_batch_shared_simd_kernel_range(torch_cuda, oracle):
+    """4,097-8,192 parts (AUTO = the shared-SIMD skew kernel, one 32-part workgroup per CU)
+    from pinned memory at a constant stride (2-D copies, 256 KiB slices) and from pageable
+    parts (staged slices): every slice is a resumable launch of that kernel."""
+    torch = torch_cuda
+    assert s3.Plan([0] * 4500, [1] * 4500).info()["kernel"] == "skews"
+    rng = np.random.default_rng(53)
+    n, stride = 4500, 600_000  # 3 slices per part
+    pinned = torch.empty(n * stride, dtype=torch.uint8, pin_memory=True)
+    h = pinned.numpy()
+    h[:] = np.frombuffer(rng.bytes(h.size), dtype=np.uint8)
+    views = [h[i * stride: i * stride + stride] for i in range(n)]
+    want = oracle.batch(h, [i * stride for i in range(n)], [stride] * n, threads=16)
+    assert np.array_equal(s3.sha256_batch_host(views), want)
+    lens = rng.integers(0, 70000, 5000)
+    buf = rng.integers(0, 256, int(lens.sum()) + 64, dtype=np.uint8)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    views = [buf[o:o + L] for o, L in zip(offs, lens)]
+    assert np.array_equal(s3.sha256_batch_host(views), oracle.batch(buf, offs, lens, threads=16))
