@@ -471,12 +471,16 @@ def c4_shard(args, s3, torch, dist, dev, rank, world, local, backend, steps: int
     del data, out
     torch.cuda.empty_cache()
     gib_gpu = per * L * steps / 2**30
+    algo = per * (L + 32)  # bytes read once + digests written, per GPU per launch
     return {"workload": f"C4: {per} x 8 MiB per GPU, {per * world} parts over {world} GPUs "
                         "(part p on rank p % N)",
             "kernel": kernel, "steps": steps,
             "per_gpu_GiBps": [round(gib_gpu / t, 3) for t in per_rank],
             "aggregate_GiBps": round(gib_gpu * world / max(max(per_rank), wall), 3),
             "ms_per_step_max_rank": round(1e3 * max(per_rank) / steps, 3),
+            # per GPU: algorithmic HBM bytes per launch / launch time vs the 8 TB/s HBM roof
+            "hbm_roofline_frac_per_gpu": [round(algo * steps / t / 1e9 / HBM_PEAK_GBS, 5)
+                                          for t in per_rank],
             "parity": {"fixtures_checked": int(badt[1]), "mismatches": int(badt[0])}}
 
 
