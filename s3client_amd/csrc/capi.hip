@@ -165,14 +165,21 @@ uint32_t plan_solo(const s3h::Slot* slots, uint64_t n, uint64_t cus) {
     for (double e : ends) span = std::max(span, e);
     return span;
   };
-  const double base = makespan(0);
-  double best = base;
-  uint64_t best_f = 0;
-  for (uint64_t F = 1; F <= groups && F <= cus; ++F) {
-    const double m = makespan(F);
-    if (m < best) best = m, best_f = F;
+  // Candidate: the fewest solo groups after which no paired group outlasts the longest solo
+  // one (durations descend, so a binary search); halved while workgroups beyond one per CU
+  // (the grid's shortest) would end later than that.  A few simulations instead of one per F:
+  // this runs on every host-path call.
+  const uint64_t lim = std::min<uint64_t>(groups, cus);
+  uint64_t lo = 1, hi = lim;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) / 2;
+    if (mid < groups && gb[mid] * kPairSlow > gb[0]) lo = mid + 1;
+    else hi = mid;
   }
-  return best < base * 0.995 ? uint32_t(best_f) : 0u;  // a clear gain only
+  const double base = makespan(0);
+  for (uint64_t F = lo; F >= 1; F /= 2)
+    if (makespan(F) < base * 0.995) return uint32_t(F);  // a clear gain only
+  return 0;
 }
 
 uint64_t sort_slots(const uint64_t* offsets, const uint64_t* lengths, uint64_t n, bool nopad,
