@@ -1104,21 +1104,36 @@ __global__ __launch_bounds__(256) void sha256_skew_pairs_kernel(LaunchArgs A) {
                             flags[g]);
 }
 
-// Four (consumer, producer) groups per workgroup with every producer on its consumer's SIMD:
-// waves 0-3 consume groups 4b..4b+3, waves 4-7 produce for them, and a workgroup's wave w runs
-// on SIMD w % 4 (HW_ID, tools/ubench_coissue*.hip), so wave g + 4 shares wave g's SIMD.  The
-// producer is written in the instruction classes that SIMD issues beside the round stream
+// Four (consumer, producer) groups per workgroup with every producer on its consumer's SIMD.
+// The producer is written in the instruction classes that SIMD issues beside the round stream
 // (skew_body SIMPLE), so one CU runs 32 chains at about the skew kernel's per-chain speed --
 // four times the chains of sha256_skew_kernel<1> per CU, without skewp's extra VALU per round.
-// LDS: 4 x 36 KiB = one workgroup per CU.
+// Pairing by SIMD: every wave publishes its SIMD (HW_ID); on each SIMD the lower wave consumes
+// and the higher one produces group = that SIMD.  The dispatcher places wave w on SIMD w % 4
+// (tools/ubench_coissue*.hip), i.e. waves g and g + 4 -- the static fallback used if a
+// placement ever is not two waves per SIMD.  LDS: 4 x 36 KiB = one workgroup per CU.
 __global__ __launch_bounds__(512) void sha256_skew_shared_kernel(LaunchArgs A) {
   __shared__ SkewLds<1, false> L[4];
   __shared__ uint32_t flags[4][2];
-  if (threadIdx.x < 8) flags[threadIdx.x >> 1][threadIdx.x & 1] = 0;
-  __syncthreads();
+  __shared__ uint32_t simd_of[8];
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t g = wave & 3u;
-  skew_body<1, false, true, true>(A, 4 * blockIdx.x + g, wave >> 2, L[g], flags[g]);
+  if (threadIdx.x < 8) flags[threadIdx.x >> 1][threadIdx.x & 1] = 0;
+  if ((threadIdx.x & 63u) == 0)
+    simd_of[wave] = (__builtin_amdgcn_s_getreg(4 | (31 << 11)) >> 4) & 3u;  // HW_REG_HW_ID.SIMD_ID
+  __syncthreads();
+  uint32_t per_simd[4] = {0, 0, 0, 0}, rank = 0;
+  const uint32_t mine = __builtin_amdgcn_readfirstlane(simd_of[wave]);
+#pragma unroll
+  for (uint32_t w = 0; w < 8; ++w) {
+    const uint32_t s = __builtin_amdgcn_readfirstlane(simd_of[w]);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) per_simd[k] += s == k;
+    rank += (w < wave && s == mine);
+  }
+  const bool paired = per_simd[0] == 2 && per_simd[1] == 2 && per_simd[2] == 2 && per_simd[3] == 2;
+  const uint32_t g = paired ? mine : wave & 3u;
+  const uint32_t role = paired ? rank : wave >> 2;
+  skew_body<1, false, true, true>(A, 4 * blockIdx.x + g, role, L[g], flags[g]);
 }
 
 // ------------------------------------------------------------- MD5 (producer/consumer)
