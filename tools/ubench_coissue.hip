@@ -10,6 +10,11 @@
 //   2 VOP3 3-source mix      3 VOP2 mix + one ds_write_b128 per 16 VALU (producer-like)
 //   4 VOP2 mix with v_perm (byte swap) per 8            5 the consumer stream itself
 // Every wave records its SIMD (HW_ID) so pairs are matched by (CU, SIMD), not by index.
+// Result (profiles/r02_ubench_coissue*.txt): every partner here was starved -- but each of these
+// streams contains "complex" instructions (left shifts, alignbit, perm, add3, DPP).  The
+// per-class sweep in tools/ubench_coissue2.hip shows that partners made only of simple ones
+// (add/sub, xor/or/and, right shifts, mov) DO issue beside the round stream at the lone-wave
+// rate; sha256_skew_shared_kernel's producer is built on that.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/ubench_coissue tools/ubench_coissue.hip
 #include <hip/hip_runtime.h>
 
