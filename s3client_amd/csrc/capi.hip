@@ -887,6 +887,11 @@ int plan_refill(s3h_plan_s* P, const uint64_t* offsets, const uint64_t* lengths,
                 s3h::Slot* h_slots, uint32_t* h_order, hipStream_t s) {
   P->total_blocks = sort_slots(offsets, lengths, P->n, nopad, h_slots, h_order);
   P->max_blocks = nopad ? h_slots[0].len >> 6 : s3h::nblocks(h_slots[0].len);
+  if (P->kernel == S3H_KERNEL_SKEW && P->quad_waves == 2) {  // two-group grid: re-plan solos
+    P->solo = plan_solo(h_slots, P->n, uint64_t(device_cus(P->device)));
+    const uint64_t groups = (P->n + 7) / 8;
+    P->grid = uint32_t(P->solo + (groups - P->solo + 1) / 2);
+  }
   HIP_TRY(hipMemcpyAsync(P->d_slots, h_slots, P->n * sizeof(s3h::Slot), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(P->d_out_idx, h_order, P->n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   return S3H_OK;

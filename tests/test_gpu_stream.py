@@ -130,3 +130,9 @@ def test_stream_many_messages_pc_lane_policy(torch_cuda, oracle):
     for i in idx:
         m = base1[o1[i]:o1[i] + lens1[i]].tobytes() + base2[o2[i]:o2[i] + lens2[i]].tobytes()
         assert np.array_equal(got[i], oracle.sha256(m)), i
+
+
+def test_stream_two_group_grid_ragged_updates(torch_cuda, oracle):
+    """3,000 messages (AUTO = the two-group skew kernel): every update re-sorts the plans and
+    re-plans the solo workgroups for that update's ragged chunk lengths (plan_refill)."""
+    _check_stream(oracle, "sha256", "auto", n=3000, rounds=3, maxlen=20000, seed=13, finals=1)
