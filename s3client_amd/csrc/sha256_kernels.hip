@@ -768,10 +768,23 @@ __device__ __forceinline__ void produce_block_simple(const RawBlock& r, uint32_t
   uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4], w5 = w[5], w6 = w[6], w7 = w[7],
            w8 = w[8], w9 = w[9], w10 = w[10], w11 = w[11], w12 = w[12], w13 = w[13], w14 = w[14],
            w15 = w[15];
+#ifdef S3H_EXP_PROD_ROWS  // experiment: one asm statement and one ds_write_b128 per W+K row
+  uint32_t l0_0 = 0, l0_1 = 0, l0_2 = 0, l0_3 = 0, l0_4 = 0, l0_5 = 0, l0_6 = 0, l0_7 = 0, l0_8 = 0,
+           l0_9 = 0, l0_10 = 0, l0_11 = 0, l0_12 = 0, l0_13 = 0, l0_14 = 0, l0_15 = 0, l1_0 = 0,
+           l1_1 = 0, l1_2 = 0, l1_3 = 0, c0, c1, c2, c3, c4, c5, s0, s1, s2, s3, rk0, rk1, rk2, rk3;
+  (void)la;
+#define S3H_ROW(q)                                                                        \
+  asm volatile(S3H_ALIGN8 S3H_PROD_ROW_##q : S3H_PROD_ROW_OUTS);                         \
+  buf[q][lane] = make_uint4(rk0, rk1, rk2, rk3);
+  S3H_ROW(0) S3H_ROW(1) S3H_ROW(2) S3H_ROW(3) S3H_ROW(4) S3H_ROW(5) S3H_ROW(6) S3H_ROW(7)
+  S3H_ROW(8) S3H_ROW(9) S3H_ROW(10) S3H_ROW(11) S3H_ROW(12) S3H_ROW(13) S3H_ROW(14) S3H_ROW(15)
+#undef S3H_ROW
+#else
   S3H_PROD_SIMPLE_TEMPS
   const uint32_t bsel = 0x00010203u;  // v_perm byte swap (tools/gen_producer.py --perm-bswap only)
   asm volatile(S3H_ALIGN8 S3H_PROD_SIMPLE_ASM : S3H_PROD_SIMPLE_OUTS : [la] "v"(la), [bsel] "v"(bsel)
                : "memory");
+#endif
 }
 
 // SIMPLE: the producer is written in the co-issuable instruction classes (it shares its

@@ -119,3 +119,6 @@ def test_kernel_isa_counts_match_the_built_code_object(tmp_path):
     k = shipped["kernels"]
     assert 540 < k["skew"]["instr_per_block"] < 550 and 600 < k["skewp"]["instr_per_block"] < 615
     assert k["skew"]["per_block"]["lds"] == 16.0
+    # the shared-SIMD kernel's consumer is the flag-synchronised skew consumer (the producer
+    # beside it runs on the same SIMD and is not in this loop)
+    assert abs(k["skews"]["instr_per_block"] - k["skew_nc2"]["instr_per_block"]) < 1.0

@@ -249,14 +249,50 @@ def emit_inc(path, perm=False, lds=False):
         f.write(f"#define S3H_PROD_SIMPLE_OUTS {outs}\n")
 
 
+def emit_rows_inc(path, lds=False):
+    """EXPERIMENT: the same op list as 16 asm statements, one per W+K row (t = 4q..4q+3), each
+    leaving the row's four W+K words in outputs rk0..rk3 for one ds_write_b128 issued by the
+    compiler (16 LDS writes per block instead of 64)."""
+    ops = block_ops(False, lds)
+    rows, cur, t = [], [], 0
+    for op in ops:
+        if op[0] == "dsw":
+            continue
+        if op[0] == "addk":
+            idx = K256.index(op[3]) if op[3] in K256 else None
+            op = ("addk", f"rk{len([o for o in cur if o[0] == 'addk'])}", op[2], op[3])
+        cur.append(op)
+        if op[0] == "addk" and sum(1 for o in cur if o[0] == "addk") == 4:
+            rows.append(cur)
+            cur = []
+    assert len(rows) == 16 and not cur
+    hdr = ["// GENERATED by tools/gen_producer.py --rows (experiment).", "#pragma once"]
+    out = []
+    for q, r in enumerate(rows):
+        body = asm_text(r)[:-1]  # no trailing s_waitcnt
+        lines = [f'  "{l}\\n\\t" \\' for l in body]
+        lines[-1] = lines[-1][:-2]
+        out.append(f"#define S3H_PROD_ROW_{q} \\\n" + "\n".join(lines))
+    ring = ", ".join([f'[{r}] "+v"({r})' for r in W + L0 + L1] +
+                     [f'[{r}] "=&v"({r})' for r in TEMPS] + [f'[rk{i}] "=&v"(rk{i})' for i in range(4)])
+    with open(path, "w") as f:
+        f.write("\n".join(hdr) + "\n\n" + "\n\n".join(out) + "\n\n")
+        f.write(f"#define S3H_PROD_ROW_OUTS {ring}\n")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "s3client_amd",
                                                   "csrc", "sha256_producer_simple.inc"))
     ap.add_argument("--perm-bswap", action="store_true", help="byte swap with v_perm (experiment)")
     ap.add_argument("--lds-bswap", action="store_true", help="byte swap on the LDS pipe (experiment)")
+    ap.add_argument("--rows", action="store_true", help="one asm statement per W+K row (experiment)")
     args = ap.parse_args()
     lds = args.lds_bswap
+    if args.rows:
+        emit_rows_inc(args.out, lds)
+        print(f"wrote {args.out} (rows)")
+        return
     emit_inc(args.out, args.perm_bswap, lds)
     ops = block_ops(args.perm_bswap, lds)
     kinds = {}
