@@ -252,7 +252,8 @@ def emit_inc(path, perm=False, lds=False):
 def emit_rows_inc(path, lds=False):
     """EXPERIMENT: the same op list as 16 asm statements, one per W+K row (t = 4q..4q+3), each
     leaving the row's four W+K words in outputs rk0..rk3 for one ds_write_b128 issued by the
-    compiler (16 LDS writes per block instead of 64)."""
+    compiler (16 LDS writes per block instead of 64).  Measured: no change on the C4 shard
+    (2,250 vs 2,246-2,271 cycles/block, profiles/r02_exp_skews_lds.jsonl)."""
     ops = block_ops(False, lds)
     rows, cur, t = [], [], 0
     for op in ops:
