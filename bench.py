@@ -303,15 +303,7 @@ def main():
 
     # parity spot-check of the last timed step's digests against the reference fixtures
     gd = digests.cpu().numpy().view(np.uint32)
-    with open(os.path.join(ROOT, "tests", "golden", "sha256_golden.json")) as f:
-        gold = json.load(f)
-    fixtures = {e["p"]: e["digest"] for e in gold["c2_parts"]}
-    if args.config == "c3":
-        fixtures = {e["p"]: e["digest"] for e in gold["c3_parts"]}
-    if args.algo == "md5":
-        fixtures = {e["p"]: e["digest"] for e in gold["md5"]["c2_parts"]} if args.config != "c3" else {}
-    if args.part_bytes:
-        fixtures = {}
+    fixtures = golden_fixtures(args.config, args.algo, args.part_bytes)
     checked = bad = 0
     for slot, p in enumerate(ids):
         want = fixtures.get(int(p))
@@ -507,7 +499,7 @@ def host_mode(args, s3, torch, dist, data, ids, lens, offs, world, rank, name):
         out, m5 = run()
         times.append(time.perf_counter() - t0)
     wall = float(np.mean(times))
-    bad = _fixture_mismatches(s3, ids, out, m5)
+    bad = _fixture_mismatches(s3, ids, out, m5, args.config, args.part_bytes)
     if rank == 0:
         what = "SHA-256 + MD5 (one H2D pass)" if dual else "SHA-256"
         print(json.dumps({"metric": f"host-resident (H2D-inclusive) {what} GiB/s", "value":
@@ -518,15 +510,28 @@ def host_mode(args, s3, torch, dist, data, ids, lens, offs, world, rank, name):
     return 0
 
 
-def _fixture_mismatches(s3, ids, sha, m5=None) -> int:
-    """Digests of the C2 parts that have committed golden fixtures, compared with them."""
+def golden_fixtures(cfg: str, algo: str, part_bytes: int = 0) -> dict:
+    """{global part id: hex digest} of the committed lib/hash fixtures that apply to this
+    workload's parts: generator-G 8 MiB parts (C2 / C4 ids; MD5: the C2 ids) or the C3 parts
+    (SHA-256 only); none for a --part-bytes override."""
+    if part_bytes:
+        return {}
     with open(os.path.join(ROOT, "tests", "golden", "sha256_golden.json")) as f:
         gold = json.load(f)
-    fixtures = {e["p"]: e["digest"] for e in gold["c2_parts"]}
+    if algo == "md5":
+        src = [] if cfg == "c3" else gold["md5"]["c2_parts"]
+    else:
+        src = gold["c3_parts"] if cfg == "c3" else gold["c2_parts"] + gold["c4_parts"]
+    return {e["p"]: e["digest"] for e in src}
+
+
+def _fixture_mismatches(s3, ids, sha, m5=None, cfg: str = "c2", part_bytes: int = 0) -> int:
+    """Digests of the workload's parts that have committed golden fixtures, compared with them."""
+    fixtures = golden_fixtures(cfg, "sha256", part_bytes)
     bad = sum(s3.hash_to_text(sha[s]) != fixtures[int(p)] for s, p in enumerate(ids)
               if int(p) in fixtures)
     if m5 is not None:
-        mf = {e["p"]: e["digest"] for e in gold["md5"]["c2_parts"]}
+        mf = golden_fixtures(cfg, "md5", part_bytes)
         bad += sum(s3.digests_to_text(m5[s:s + 1], 4)[0] != mf[int(p)] for s, p in enumerate(ids)
                    if int(p) in mf)
     return int(bad)
@@ -544,7 +549,7 @@ def dual_mode(args, s3, torch, data, ids, lens, offs, rank, name, stream):
         times.append(time.perf_counter() - t0)
     wall = float(np.mean(times))
     bad = _fixture_mismatches(s3, ids, sha.cpu().numpy().view(np.uint32),
-                              m5.cpu().numpy().view(np.uint32))
+                              m5.cpu().numpy().view(np.uint32), args.config, args.part_bytes)
     if rank == 0:
         print(json.dumps({"metric": "device-resident SHA-256 + MD5 GiB/s (both digests)",
                           "value": round(float(lens.sum()) / 2**30 / wall, 3), "unit": "GiB/s",
@@ -578,10 +583,7 @@ def stream_mode(args, s3, torch, data, ids, lens, offs, rank, name, stream):
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / max(1, args.steps)
     gd = out.cpu().numpy().view(np.uint32)
-    with open(os.path.join(ROOT, "tests", "golden", "sha256_golden.json")) as f:
-        gold = json.load(f)
-    src = gold["c2_parts"] if algo == "sha256" else gold["md5"]["c2_parts"]
-    fixtures = {e["p"]: e["digest"] for e in src} if not args.part_bytes else {}
+    fixtures = golden_fixtures(args.config, algo, args.part_bytes)
     checked = [int(p) for p in ids if int(p) in fixtures]
     bad = sum(s3.hash_to_text(gd[s]) != fixtures[int(p)]
               for s, p in enumerate(ids) if int(p) in fixtures)

@@ -392,9 +392,15 @@ DualMode dual_mode(const s3h_plan_s* S, const s3h_plan_s* M, uint64_t b0, uint64
   const uint64_t cus = uint64_t(device_cus(S->device));
   if (S->kernel == S3H_KERNEL_SKEW && S->quad_waves == 1 && S->grid + M->grid <= cus)
     return kDualSplit;
-  // the group kernel runs skewp geometry: 32 parts per workgroup, like the shared-SIMD kernel
-  if ((S->kernel == S3H_KERNEL_SKEWP || S->kernel == S3H_KERNEL_SKEWS) && S->grid <= cus)
-    return kDualGroup;
+  // the group kernel runs skewp geometry (32 parts per workgroup) whatever S's own kernel:
+  // the skewp / shared-SIMD ranges and the two-group skew range (2,049-4,096 parts, whose
+  // two-stream form runs MD5 workgroups on CUs already running SHA-256 ones)
+  const bool group_ok = S->kernel == S3H_KERNEL_SKEWP || S->kernel == S3H_KERNEL_SKEWS ||
+                        (S->kernel == S3H_KERNEL_SKEW && S->quad_waves == 2);
+#ifdef S3H_EXP_NO_GROUP_NC2  // tools/ experiment builds only: round-2 behaviour
+  if (S->kernel == S3H_KERNEL_SKEW) return kDualNone;
+#endif
+  if (group_ok && (S->n + 31) / 32 <= cus) return kDualGroup;
   return kDualNone;
 }
 
@@ -412,8 +418,8 @@ int dual_launch(s3h_plan_s* S, s3h_plan_s* M, const void* d_base, uint32_t* d_sh
   const s3h::LaunchArgs B = make_args(M, d_base, d_md5, ranged ? M->d_state : nullptr, b0, b1,
                                       origin, 0, nullptr);
   if (mode == kDualGroup)
-    hipLaunchKernelGGL(s3h::sha256_md5_group_kernel<true>, dim3(S->grid), dim3(192), 0, stream,
-                       A, B);
+    hipLaunchKernelGGL(s3h::sha256_md5_group_kernel<true>, dim3(uint32_t((S->n + 31) / 32)),
+                       dim3(192), 0, stream, A, B);
   else
     hipLaunchKernelGGL(s3h::sha256_md5_dual_kernel<false>, dim3(S->grid + M->grid), dim3(128), 0,
                        stream, A, B, uint32_t(S->grid));

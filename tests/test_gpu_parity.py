@@ -339,10 +339,11 @@ def test_dual_digest_device_c2_subset(torch_cuda, oracle, golden):
 
 
 def test_dual_digest_device_fallback_and_fused_ragged(torch_cuda, oracle):
-    """Ragged batches on both dual-digest routes: 300 parts (fused grid, skew) and 2,500 parts
-    (skew NC=2 is not fused: MD5 on a forked side stream), each vs the oracle."""
+    """Ragged batches on all three dual-digest routes: 300 parts (fused split grid, skew), 2,000
+    parts (too many workgroups for one split grid: MD5 on a forked side stream) and 2,500 parts
+    (two-group skew range: the group kernel's skewp geometry), each vs the oracle."""
     rng = np.random.default_rng(33)
-    for n in (300, 2500):
+    for n in (300, 2000, 2500):
         rl = rng.integers(0, 9000, n)
         ro = np.cumsum(rng.integers(0, 70, n) + np.concatenate([[0], rl[:-1]]))
         host = rng.integers(0, 256, int(ro[-1] + rl[-1]) + 8, dtype=np.uint8)
