@@ -390,13 +390,16 @@ DualMode dual_mode(const s3h_plan_s* S, const s3h_plan_s* M, uint64_t b0, uint64
       S->n != M->n)
     return kDualNone;
   const uint64_t cus = uint64_t(device_cus(S->device));
+#ifndef S3H_EXP_NO_SPLIT  // tools/ experiment builds only: never the split grid
   if (S->kernel == S3H_KERNEL_SKEW && S->quad_waves == 1 && S->grid + M->grid <= cus)
     return kDualSplit;
+#endif
   // the group kernel runs skewp geometry (32 parts per workgroup) whatever S's own kernel:
   // the skewp / shared-SIMD ranges and the two-group skew range (2,049-4,096 parts, whose
   // two-stream form runs MD5 workgroups on CUs already running SHA-256 ones)
+  // (and skew plans whose split grid would not fit: 1,821-2,048 parts)
   const bool group_ok = S->kernel == S3H_KERNEL_SKEWP || S->kernel == S3H_KERNEL_SKEWS ||
-                        (S->kernel == S3H_KERNEL_SKEW && S->quad_waves == 2);
+                        S->kernel == S3H_KERNEL_SKEW;
 #ifdef S3H_EXP_NO_GROUP_NC2  // tools/ experiment builds only: round-2 behaviour
   if (S->kernel == S3H_KERNEL_SKEW) return kDualNone;
 #endif

@@ -97,6 +97,15 @@ __device__ __forceinline__ void schedule_wk(const uint32_t w16[16], uint32_t wk[
   for (int t = 0; t < 64; ++t) wk[t] = w[t] + S3H_K(t);
 }
 
+// Length a producer lane decodes with.  A lane without a part (its slot is past n in the
+// last, partial group) loads the zero page like any block outside a part; a length past every
+// block keeps it on the full-block decode -- with its true length 0 it would take the
+// padded-tail branch every block, and, the wave being SIMT, so would the whole wave
+// (1,800 x 8 MiB SHA-256 + MD5: 2.9x slower; profiles/r02_exp_dual_partial_groups.jsonl).
+__device__ __forceinline__ uint64_t decode_len(bool has_part, uint64_t len) {
+  return has_part ? len : (1ull << 62);
+}
+
 // Raw fetch of one FULL 64-byte block whose first byte is at `p` (any alignment).
 // Loads the 17 dwords covering it from the dword-aligned address below `p`; the 17th is
 // only touched when p is not dword aligned, so no dword without a part byte is read.

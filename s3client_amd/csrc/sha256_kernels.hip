@@ -217,23 +217,24 @@ __global__ __launch_bounds__(kPcThreads) void sha256_pc_kernel(LaunchArgs A) {
     const uint32_t sel = be_selector(uint32_t(reinterpret_cast<uintptr_t>(p) & 3));
     const uint64_t fend = fetch_end(s.len, A.blk_end);
     const uint64_t bits = valid ? msg_bits(A, slot, s.len) : 0;
+    const uint64_t dl = decode_len(valid, s.len);
     RawBlock ra, rb;
     fetch_full(p, b0 < fend, A.zero, ra);
     fetch_full(p + 64, b0 + 1 < fend, A.zero, rb);
-    produce_block(ra, sel, p, s.len, bits, b0, A.blk_end, lds_wk[0], lane);
+    produce_block(ra, sel, p, dl, bits, b0, A.blk_end, lds_wk[0], lane);
     __syncthreads();
     for (uint64_t k = 1; k <= iters; k += 2) {
       // odd step: block b0+k from rb into buffer 1; refill ra with block b0+k+1
       if (k < iters) {
         fetch_full(p + 64 * (k + 1), b0 + k + 1 < fend, A.zero, ra);
-        produce_block(rb, sel, p + 64 * k, s.len, bits, b0 + k, A.blk_end, lds_wk[1], lane);
+        produce_block(rb, sel, p + 64 * k, dl, bits, b0 + k, A.blk_end, lds_wk[1], lane);
       }
       __syncthreads();
       if (k + 1 > iters) break;
       // even step: block b0+k+1 from ra into buffer 0; refill rb with block b0+k+2
       if (k + 1 < iters) {
         fetch_full(p + 64 * (k + 2), b0 + k + 2 < fend, A.zero, rb);
-        produce_block(ra, sel, p + 64 * (k + 1), s.len, bits, b0 + k + 1, A.blk_end, lds_wk[0], lane);
+        produce_block(ra, sel, p + 64 * (k + 1), dl, bits, b0 + k + 1, A.blk_end, lds_wk[0], lane);
       }
       __syncthreads();
     }
@@ -352,21 +353,22 @@ __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A)
     const uint64_t fend = fetch_end(s.len, A.blk_end);
     const uint64_t bh = b0 + half;  // this lane's first block
     const uint64_t bits = slot < A.n ? msg_bits(A, slot, s.len) : 0;
+    const uint64_t dl = decode_len(slot < A.n, s.len);
     RawBlock ra, rb;
     fetch_full(p, bh < fend, A.zero, ra);
     fetch_full(p + 128, bh + 2 < fend, A.zero, rb);
-    produce_block(ra, sel, p, s.len, bits, bh, A.blk_end, lds_wk[0][half], part);
+    produce_block(ra, sel, p, dl, bits, bh, A.blk_end, lds_wk[0][half], part);
     __syncthreads();
     for (uint64_t k = 1; k <= steps; k += 2) {
       if (k < steps) {
         fetch_full(p + 128 * (k + 1), bh + 2 * (k + 1) < fend, A.zero, ra);
-        produce_block(rb, sel, p + 128 * k, s.len, bits, bh + 2 * k, A.blk_end, lds_wk[1][half], part);
+        produce_block(rb, sel, p + 128 * k, dl, bits, bh + 2 * k, A.blk_end, lds_wk[1][half], part);
       }
       __syncthreads();
       if (k + 1 > steps) break;
       if (k + 1 < steps) {
         fetch_full(p + 128 * (k + 2), bh + 2 * (k + 2) < fend, A.zero, rb);
-        produce_block(ra, sel, p + 128 * (k + 1), s.len, bits, bh + 2 * (k + 1), A.blk_end, lds_wk[0][half], part);
+        produce_block(ra, sel, p + 128 * (k + 1), dl, bits, bh + 2 * (k + 1), A.blk_end, lds_wk[0][half], part);
       }
       __syncthreads();
     }
@@ -528,22 +530,23 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_quad_kernel(LaunchArgs A
     const uint64_t fend = fetch_end(s.len, A.blk_end);
     const uint64_t bh = b0 + h;
     const uint64_t bits = slot < A.n ? msg_bits(A, slot, s.len) : 0;
+    const uint64_t dl = decode_len(slot < A.n, s.len);
     constexpr uint64_t kStride = 64ull * kBps;
     RawBlock ra, rb;
     fetch_full(p, bh < fend, A.zero, ra);
     fetch_full(p + kStride, bh + kBps < fend, A.zero, rb);
-    produce_block(ra, sel, p, s.len, bits, bh, A.blk_end, lds_wk[0][h], part);
+    produce_block(ra, sel, p, dl, bits, bh, A.blk_end, lds_wk[0][h], part);
     __syncthreads();
     for (uint64_t k = 1; k <= steps; k += 2) {
       if (k < steps) {
         fetch_full(p + kStride * (k + 1), bh + kBps * (k + 1) < fend, A.zero, ra);
-        produce_block(rb, sel, p + kStride * k, s.len, bits, bh + kBps * k, A.blk_end, lds_wk[1][h], part);
+        produce_block(rb, sel, p + kStride * k, dl, bits, bh + kBps * k, A.blk_end, lds_wk[1][h], part);
       }
       __syncthreads();
       if (k + 1 > steps) break;
       if (k + 1 < steps) {
         fetch_full(p + kStride * (k + 2), bh + kBps * (k + 2) < fend, A.zero, rb);
-        produce_block(ra, sel, p + kStride * (k + 1), s.len, bits, bh + kBps * (k + 1), A.blk_end, lds_wk[0][h], part);
+        produce_block(ra, sel, p + kStride * (k + 1), dl, bits, bh + kBps * (k + 1), A.blk_end, lds_wk[0][h], part);
       }
       __syncthreads();
     }
@@ -838,7 +841,7 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
       if (slot < A.n) s = A.slots[slot];
       p[r] = A.base + s.off + 64ull * (b0 + h[r] - A.blk_origin);
       sel[r] = be_selector(uint32_t(reinterpret_cast<uintptr_t>(A.base + s.off) & 3));
-      len[r] = s.len;
+      len[r] = decode_len(slot < A.n, s.len);
       fend[r] = fetch_end(s.len, A.blk_end);
       bh[r] = b0 + h[r];
       bits[r] = slot < A.n ? msg_bits(A, slot, s.len) : 0;
@@ -1346,7 +1349,7 @@ __device__ __forceinline__ void md5_self_body(const LaunchArgs& A, const uint32_
       if (J >= iters) goto md5_done;
       fetch_full(p + 64 * (J + kDepth), b0 + J + kDepth < fend, A.zero, ring[(u + kDepth) % kRing]);
       uint32_t w[16];
-      md5_decode(ring[u], sel, p + 64 * J, s.len, bits, b0 + J, A.blk_end, w);
+      md5_decode(ring[u], sel, p + 64 * J, decode_len(valid, s.len), bits, b0 + J, A.blk_end, w);
       hash_words(w, J);
     }
   }
@@ -1391,16 +1394,17 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
     const uint32_t sel = le_selector(uint32_t(reinterpret_cast<uintptr_t>(p) & 3));
     const uint64_t fend = fetch_end(s.len, A.blk_end);
     const uint64_t bits = valid ? msg_bits(A, slot, s.len) : 0;
+    const uint64_t dl = decode_len(valid, s.len);
     RawBlock ra, rb, rc;
     fetch_full(p, b0 < fend, A.zero, ra);
     fetch_full(p + 64, b0 + 1 < fend, A.zero, rb);
     fetch_full(p + 128, b0 + 2 < fend, A.zero, rc);
-    md5_produce(ra, sel, p, s.len, bits, b0, A.blk_end, lds_km[0], lane);
+    md5_produce(ra, sel, p, dl, bits, b0, A.blk_end, lds_km[0], lane);
     __syncthreads();
 #define S3H_MD5_PSTEP(J, NEXT, CUR)                                                        \
     if ((J) < iters) {                                                                     \
       fetch_full(p + 64 * ((J) + 2), b0 + (J) + 2 < fend, A.zero, NEXT);                    \
-      md5_produce(CUR, sel, p + 64 * (J), s.len, bits, b0 + (J), A.blk_end, lds_km[(J) & 1], lane); \
+      md5_produce(CUR, sel, p + 64 * (J), dl, bits, b0 + (J), A.blk_end, lds_km[(J) & 1], lane); \
     }                                                                                      \
     __syncthreads();                                                                       \
     if ((J) + 1 > iters) break;
