@@ -383,13 +383,16 @@ int plan_launch(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint64_t
 // S's workgroups then M's, all within one workgroup per CU); kDualGroup =
 // sha256_md5_group_kernel (skewp: each workgroup runs a SHA-256 group and a self-fed MD5 wave
 // over the same 32 parts, S->grid <= one per CU); kDualNone = two launches on two streams.
-enum DualMode { kDualNone = 0, kDualSplit = 1, kDualGroup = 2 };
+enum DualMode { kDualNone = 0, kDualSplit = 1, kDualGroup = 2, kDualGroupSkew = 3 };
 
 DualMode dual_mode(const s3h_plan_s* S, const s3h_plan_s* M, uint64_t b0, uint64_t b1) {
   if (M->algo != S3H_ALGO_MD5 || S->algo != S3H_ALGO_SHA256 || b1 - b0 >= (1ull << 31) ||
       S->n != M->n)
     return kDualNone;
   const uint64_t cus = uint64_t(device_cus(S->device));
+#ifdef S3H_EXP_GROUP_SKEW  // tools/ experiment builds only: skew-layout group kernel
+  if (S->kernel == S3H_KERNEL_SKEW && S->quad_waves == 1 && S->grid <= cus) return kDualGroupSkew;
+#endif
 #ifndef S3H_EXP_NO_SPLIT  // tools/ experiment builds only: never the split grid
   if (S->kernel == S3H_KERNEL_SKEW && S->quad_waves == 1 && S->grid + M->grid <= cus)
     return kDualSplit;
@@ -422,6 +425,9 @@ int dual_launch(s3h_plan_s* S, s3h_plan_s* M, const void* d_base, uint32_t* d_sh
                                       origin, 0, nullptr);
   if (mode == kDualGroup)
     hipLaunchKernelGGL(s3h::sha256_md5_group_kernel<true>, dim3(uint32_t((S->n + 31) / 32)),
+                       dim3(192), 0, stream, A, B);
+  else if (mode == kDualGroupSkew)
+    hipLaunchKernelGGL(s3h::sha256_md5_group_kernel<false>, dim3(uint32_t((S->n + 7) / 8)),
                        dim3(192), 0, stream, A, B);
   else
     hipLaunchKernelGGL(s3h::sha256_md5_dual_kernel<false>, dim3(S->grid + M->grid), dim3(128), 0,
