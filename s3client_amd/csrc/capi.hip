@@ -397,10 +397,13 @@ DualMode dual_mode(const s3h_plan_s* S, const s3h_plan_s* M, uint64_t b0, uint64
   if (S->kernel == S3H_KERNEL_SKEW && S->quad_waves == 1 && S->grid + M->grid <= cus)
     return kDualSplit;
 #endif
+  // skew plans whose split grid does not fit (1,821-2,048 parts on 256 CUs): each skew group
+  // with a self-fed MD5 wave over the same 8 parts, one workgroup per CU -- both digests in
+  // ~125 ms for 8 MiB parts vs 140 on the skewp group kernel (profiles/r02_exp_dual_group_skew.jsonl)
+  if (S->kernel == S3H_KERNEL_SKEW && S->quad_waves == 1 && S->grid <= cus) return kDualGroupSkew;
   // the group kernel runs skewp geometry (32 parts per workgroup) whatever S's own kernel:
   // the skewp / shared-SIMD ranges and the two-group skew range (2,049-4,096 parts, whose
   // two-stream form runs MD5 workgroups on CUs already running SHA-256 ones)
-  // (and skew plans whose split grid would not fit: 1,821-2,048 parts)
   const bool group_ok = S->kernel == S3H_KERNEL_SKEWP || S->kernel == S3H_KERNEL_SKEWS ||
                         S->kernel == S3H_KERNEL_SKEW;
 #ifdef S3H_EXP_NO_GROUP_NC2  // tools/ experiment builds only: round-2 behaviour

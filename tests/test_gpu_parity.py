@@ -339,9 +339,10 @@ def test_dual_digest_device_c2_subset(torch_cuda, oracle, golden):
 
 
 def test_dual_digest_device_fallback_and_fused_ragged(torch_cuda, oracle):
-    """Ragged batches on all three dual-digest routes: 300 parts (fused split grid, skew), 2,000
-    parts (too many workgroups for one split grid: MD5 on a forked side stream) and 2,500 parts
-    (two-group skew range: the group kernel's skewp geometry), each vs the oracle."""
+    """Ragged batches on the dual-digest routes: 300 parts (split grid: skew workgroups then MD5
+    workgroups), 2,000 parts (the split grid would not fit one workgroup per CU: skew groups
+    each with a self-fed MD5 wave) and 2,500 parts (two-group skew range: the group kernel's
+    skewp geometry), each vs the oracle."""
     rng = np.random.default_rng(33)
     for n in (300, 2000, 2500):
         rl = rng.integers(0, 9000, n)
