@@ -728,6 +728,11 @@ __device__ __forceinline__ void flag_wait_ge(uint32_t* f, uint32_t v, bool& aliv
   }
 }
 
+// The generated producer's v_mul_f32 left shifts need f32 denormals kept on input and output
+// (the default: .amdhsa_float_denorm_mode_32 3, checked by tests/test_producer_schedule.py).
+#if defined(__FAST_MATH__) || defined(__AMDGCN_FLUSH_DENORMALS__)
+#error "sha256_producer_simple.inc needs f32 denormals: do not build with fast-math / FTZ"
+#endif
 #ifdef S3H_EXP_PRODUCER_INC  // tools/ experiment builds only: another generated producer
 #include S3H_EXP_PRODUCER_INC
 #else
@@ -735,11 +740,13 @@ __device__ __forceinline__ void flag_wait_ge(uint32_t* f, uint32_t v, bool& aliv
 #endif
 
 // The same for a producer that shares its consumer's SIMD (sha256_skew_shared_kernel): that
-// SIMD issues a second wave's v_add_u32, v_xor/or/and_b32 and v_lshrrev_b32 beside the round
-// stream at the lone-wave rate, but not its left shifts, alignbit, perm or add3
-// (tools/ubench_coissue2.hip, profiles/r02_ubench_coissue_*.txt).  The block's byte swap and
-// schedule are therefore one generated asm statement in those classes (tools/gen_producer.py:
-// left shifts as doublings), fed the block's 16 words as little-endian dwords: the raw loads
+// SIMD issues a second wave's v_add_u32, v_xor/or/and_b32, v_lshrrev_b32 and f32 add/mul
+// beside the round stream at the lone-wave rate, but not its left shifts, alignbit, perm or
+// add3 (tools/ubench_coissue2.hip, profiles/r02_ubench_coissue_*.txt).  The block's byte swap
+// and schedule are therefore one generated asm statement in those classes
+// (tools/gen_producer.py: each left shift is one v_mul_f32 by 2^k on a denormal bit pattern --
+// exact because f32 denormals are preserved, see below -- plus doublings), fed the block's 16
+// words as little-endian dwords: the raw loads
 // when every lane of the wave reads dword-aligned parts (`aligned`), one v_perm per word
 // otherwise, and the padded tail block (once per part) byte-swapped back with v_perm.
 template <int kRow>

@@ -1,9 +1,10 @@
 """CPU checks of the shared-SIMD producer (tools/gen_producer.py), the asm statement that
 sha256_skew_shared_kernel's producer wave runs per block: simulated on one lane, its W[t]+K[t]
 drive a plain 64-round compression to hashlib's digest for multi-block messages; the
-committed .inc is the generator's output; and it uses only the instruction classes a SIMD
+committed .inc is the generator's output; it uses only the instruction classes a SIMD
 issues beside the consumer's round stream (no left shift, alignbit, perm, add3: those would
-stall it -- profiles/r02_ubench_coissue_classes.txt)."""
+stall it -- profiles/r02_ubench_coissue_classes*.txt); and the kernel that runs it keeps f32
+denormals, which its v_mul_f32 left shifts need."""
 import hashlib
 import os
 import random
@@ -38,10 +39,14 @@ def _padded(msg):
     return msg + b"\x80" + b"\0" * ((55 - len(msg)) % 64) + struct.pack(">Q", 8 * len(msg))
 
 
-@pytest.mark.parametrize("n", [0, 3, 55, 56, 64, 119, 200, 1000])
-def test_producer_drives_compression_to_hashlib(n):
+@pytest.mark.parametrize("n,fill", [(0, None), (3, None), (55, None), (56, None), (64, None),
+                                    (119, None), (200, None), (1000, None), (640, 0xFF),
+                                    (640, 0x80), (640, 0x7F), (640, 0x01)])
+def test_producer_drives_compression_to_hashlib(n, fill):
+    """fill: constant bytes, the extremes of the masked denormal multiplies (mulf_ok asserts
+    every product stays below 2^24)."""
     rng = random.Random(n)
-    msg = bytes(rng.randrange(256) for _ in range(n))
+    msg = bytes(rng.randrange(256) if fill is None else fill for _ in range(n))
     p = _padded(msg)
     h = IV
     for i in range(0, len(p), 64):
@@ -64,15 +69,31 @@ def test_only_coissuable_instruction_classes():
     with open(os.path.join(ROOT, "s3client_amd", "csrc", "sha256_producer_simple.inc")) as f:
         ops = re.findall(r'"([a-z_0-9]+) ', f.read())
     allowed = {"v_add_u32", "v_xor_b32", "v_or_b32", "v_and_b32", "v_lshrrev_b32", "v_bitop3_b32",
-               "ds_write_b32", "s_waitcnt"}
+               "v_mul_f32", "ds_write_b32", "s_waitcnt"}
     assert set(ops) <= allowed, set(ops) - allowed
-    # doublings dominate: every left shift of the schedule and the byte swap is v_add_u32 x, x
-    assert ops.count("v_add_u32") > 1800 and ops.count("ds_write_b32") == 64
+    # left shifts: one denormal v_mul_f32 + doublings (v_add_u32 x, x) each
+    assert ops.count("v_mul_f32") == 93 and ops.count("ds_write_b32") == 64
+    assert 2100 < len(ops) - 65 < 2300
 
 
-@pytest.mark.parametrize("variant", [{"perm": True}, {"lds": True}])
+def test_shared_kernel_keeps_f32_denormals():
+    """v_mul_f32 on a denormal bit pattern is a left shift only if f32 denormals are neither
+    flushed on input nor on output: .amdhsa_float_denorm_mode_32 3 in the built code object."""
+    s_file = os.path.join(ROOT, "build", "isa", "capi-hip-amdgcn-amd-amdhsa-gfx950.s")
+    if not os.path.exists(s_file):
+        pytest.skip("no build/isa (make builds it)")
+    text = open(s_file).read()
+    m = re.search(r"\.amdhsa_kernel _ZN3s3h25sha256_skew_shared_kernel\w*\n(.*?)\.end_amdhsa_kernel", text, re.S)
+    assert m, "skews kernel descriptor not found"
+    assert re.search(r"\.amdhsa_float_denorm_mode_32 3\b", m.group(1))
+
+
+@pytest.mark.parametrize("variant", [{"perm": True}, {"lds": True}, {"mulf": False, "merge3": False},
+                                     {"perm": True, "mulf": False, "merge3": False},
+                                     {"lds": True, "mulf": False, "merge3": False}])
 def test_experiment_variants_compute_the_same_schedule(variant):
-    """The v_perm and LDS-pipe byte-swap variants (experiments, profiles/r02_exp_producer_*)."""
+    """The v_perm and LDS-pipe byte-swap variants and the doublings-only first version
+    (experiments, profiles/r02_exp_producer_*)."""
     rng = random.Random(9)
     for _ in range(10):
         blk = bytes(rng.randrange(256) for _ in range(64))

@@ -3,26 +3,34 @@
 
 A producer wave that shares its consumer's SIMD (sha256_skew_shared_kernel) only gets issue
 slots for the instruction classes the SIMD runs beside the consumer's round stream:
-v_add_u32, v_xor/or/and_b32, v_lshrrev_b32 (and, most of the time, v_bitop3_b32) -- not left
-shifts, alignbit, perm, add3 (tools/ubench_coissue2.hip, profiles/r02_ubench_coissue_*.txt).
-This module emits ONE block's producer work in those classes as a single asm statement:
+v_add_u32, v_xor/or/and_b32, v_lshrrev_b32, v_add/sub/mul/fmac_f32 (and, most of the time,
+v_bitop3_b32) -- not left shifts, alignbit, perm, add3, cvt, integer multiplies or 16-bit ops
+(tools/ubench_coissue2.hip, profiles/r02_ubench_coissue_*.txt).  This module emits ONE
+block's producer work in those classes as a single asm statement:
 
     in : w0..w15 = the block's 16 message dwords as loaded (little-endian bytes; the asm
          byte-swaps them), la = this lane's LDS address of W+K row 0 of its (buffer, block, part)
     out: 64 x ds_write_b32 of W[t] + K[t] at la + (t / 4) * ROW + (t % 4) * 4
 
     bswap(x)   = x >> 24 | (x >> 8) & 0xff00 | (x << 8) & 0xff0000 | x << 24
-    sigma0(x)  = (x >> 7 ^ x >> 18 ^ x >> 3) ^ L0(x),  L0(x) = x << 25 ^ x << 14
-    sigma1(y)  = (y >> 17 ^ y >> 19 ^ y >> 10) ^ L1(y), L1(y) = y << 15 ^ y << 13
+    sigma0(x)  = (x >> 7 ^ x >> 18 ^ x >> 3) ^ x << 25 ^ x << 14
+    sigma1(y)  = (y >> 17 ^ y >> 19 ^ y >> 10) ^ y << 15 ^ y << 13
 
-with every left shift made of doublings (v_add_u32 x, x, x): per word d13 = x << 13 (13),
-d14 = 2 d13, d15 = 2 d14, d25 = 2^10 d15; L1 = d15 ^ d13 (words 14..61), L0 = d25 ^ d14
-(words 1..48).  Word t's doubling chain is interleaved with word t+1's expansion (one
-instruction each, alternately) so that no instruction waits on the one before it.
+Left shifts without a left-shift instruction: `v_mul_f32 d, 2^k, m` on a bit pattern m < 2^23
+(a denormal) is exactly m << k while the result stays below 2^24 (mulf_ok), and the rest of a
+shift is doublings (v_add_u32 x, x, x).  Per word: d13 = ((x & 0x7ffff) * 2^5) doubled 8 times,
+d14 = 2 d13, d15 = 2 d14, d25 = 2^10 d15 (words 1..48); sigma's second v_bitop3 xor3 folds
+d25 ^ d14 (sigma0) or d15 ^ d13 (sigma1).  Byte swap: (x & 0xff00) * 2^8 gives byte 1's
+place; x << 24 = ((x & 0xff) * 2^16) doubled 8 times.  2,188 VALU + 64 LDS writes per block
+(the first round-2 producer, doublings only and separate L0/L1 xors: 2,675 VALU; C4 shard
+470 -> 499 GiB/s on one box, profiles/r02_exp_producer_mulf.jsonl).  Word t's doubling chain
+is interleaved with word t+1's expansion (one instruction each, alternately) so that no
+instruction waits on the one before it.
 
-Registers: W ring w[t % 16] (the inputs), L0 ring l0_[t % 16], L1 ring l1_[t % 4], doubling
-temporaries c0-c2, expansion / byte-swap temporaries s0-s3, W+K ring k[t % 8] (a value is
-rewritten 8 words after its ds_write).
+Registers: W ring w[t % 16] (the inputs), d25 ring l0_[t % 16], d14 ring l0b_[t % 16], d13
+ring l1_[t % 4], d15 ring l1b_[t % 4], expansion / byte-swap temporaries s0-s3, W+K ring
+k[t % 8] (a value is rewritten 8 words after its ds_write).  --doublings restores the
+first version (L0 / L1 xor rings, temporaries c0-c5).
 
 `emit_inc` writes s3client_amd/csrc/sha256_producer_simple.inc; `simulate` runs the same op
 list on Python integers (tests/test_producer_schedule.py checks it against hashlib-derived
@@ -47,21 +55,35 @@ W = [f"w{i}" for i in range(16)]
 L0 = [f"l0_{i}" for i in range(16)]
 L1 = [f"l1_{i}" for i in range(4)]
 KR = [f"k{i}" for i in range(8)]
+L0B = [f"l0b_{i}" for i in range(16)]   # merge3 only: d14 beside d25 (L0), d15 beside d13 (L1)
+L1B = [f"l1b_{i}" for i in range(4)]
 TEMPS = ["c0", "c1", "c2", "c3", "c4", "c5", "s0", "s1", "s2", "s3"]
 # op tuples: ("add", d, a, b) ("xor", d, a, b) ("or", d, a, b) ("and", d, a, imm)
 #            ("shr", d, imm, a) ("xor3", d, a, b, c) ("addk", d, a, imm) ("dsw", src, offset)
-SIMPLE_OPS = {"add", "xor", "or", "and", "shr", "addk"}   # bitop3 (xor3) is the partial class
+SIMPLE_OPS = {"add", "xor", "or", "and", "shr", "addk", "mulf"}   # bitop3 (xor3) is the partial class
 
 
-def lefts(t):
+def lefts(t, mulf=False, merge3=False):
     """Doublings of word t and its L1 (words 14..61) / L0 (words 1..48); temporaries c0-c2 for
-    even words, c3-c5 for odd ones (two consecutive words' chains may interleave)."""
+    even words, c3-c5 for odd ones (two consecutive words' chains may interleave).
+    merge3: no L0/L1 xors; the shifted words stay in rings (d13 in L1, d14 in L0B, d15 in L1B,
+    d25 in L0) and sigma's second v_bitop3 xor3 folds both."""
     need0, need1 = 1 <= t <= 48, 14 <= t <= 61
     if not (need0 or need1):
         return []
     x = W[t % 16]
+    if merge3:
+        a, b, c, d = L1[t % 4], L0B[t % 16], L1B[t % 4], L0[t % 16]
+        ops = [("and", a, x, 0x7FFFF), ("mulf", a, a, 5)] + [("add", a, a, a)] * 8   # d13
+        ops += [("add", b, a, a), ("add", c, b, b)]                                     # d14, d15
+        if need0:
+            ops += [("add", d, c, c)] + [("add", d, d, d)] * 9                           # d25
+        return ops
     a, b, c = ("c0", "c1", "c2") if t % 2 == 0 else ("c3", "c4", "c5")
-    ops = [("add", a, x, x)] + [("add", a, a, a)] * 12                    # d13
+    if mulf:   # (x & 0x7ffff) << 5 by one denormal multiply, then 8 doublings
+        ops = [("and", a, x, 0x7FFFF), ("mulf", a, a, 5)] + [("add", a, a, a)] * 8
+    else:
+        ops = [("add", a, x, x)] + [("add", a, a, a)] * 12                # d13
     ops += [("add", b, a, a), ("add", c, b, b)]                           # d14, d15
     if need1:
         ops.append(("xor", L1[t % 4], c, a))
@@ -69,6 +91,15 @@ def lefts(t):
         ops += [("add", a, c, c)] + [("add", a, a, a)] * 9                 # d25
         ops.append(("xor", L0[t % 16], a, b))
     return ops
+
+
+def mulf_ok(m, k):
+    """v_mul_f32 d, 2^k, m on the bit pattern m: with f32 denormals preserved (the code object's
+    .amdhsa_float_denorm_mode_32 3), m < 2^23 is the denormal m * 2^-149, and the product
+    m * 2^(k-149) is exact; while m << k < 2^24 it lies in the denormal range or the first
+    normal binade, whose spacing is also 2^-149, so its bit pattern is exactly m << k."""
+    assert 0 <= m < 1 << 23 and (m << k) < 1 << 24, (m, k)
+    return m << k
 
 
 def wk_offset(t):
@@ -94,12 +125,17 @@ def lds_bswap():
     return ops
 
 
-def bswap(t, perm=False):
+def bswap(t, perm=False, mulf=False):
     """w[t] (little-endian load) -> big-endian word, in place (perm: one v_perm_b32, which the
     shared SIMD issues only in the consumer's non-VALU cycles)."""
     x = W[t]
     if perm:
         return [("perm", x, x)]
+    if mulf:   # (x << 8) & 0xff0000 in one denormal multiply; x << 24 = 8 doublings of (x & 0xff) << 16
+        return ([("and", "s0", x, 0xFF00), ("and", "s1", x, 0xFF), ("mulf", "s0", "s0", 8),
+                 ("mulf", "s1", "s1", 16)] + [("add", "s1", "s1", "s1")] * 8 +
+                [("shr", "s2", 24, x), ("or", "s0", "s0", "s1"), ("shr", "s3", 8, x),
+                 ("and", "s3", "s3", 0xFF00), ("or", "s2", "s2", "s3"), ("or", x, "s0", "s2")])
     return ([("add", "s0", x, x)] + [("add", "s0", "s0", "s0")] * 7 +      # s0 = x << 8
             [("add", "s1", "s0", "s0")] + [("add", "s1", "s1", "s1")] * 15 +   # s1 = x << 24
             [("and", "s0", "s0", 0xFF0000), ("shr", "s2", 24, x), ("or", "s0", "s0", "s1"),
@@ -107,9 +143,16 @@ def bswap(t, perm=False):
              ("or", x, "s0", "s2")])
 
 
-def expansion(t):
+def expansion(t, merge3=False):
     """W[t] = sigma1(W[t-2]) + W[t-7] + sigma0(W[t-15]) + W[t-16], t >= 16."""
     x, y = W[(t - 15) % 16], W[(t - 2) % 16]
+    if merge3:
+        return [("shr", "s0", 7, x), ("shr", "s1", 18, x), ("shr", "s2", 3, x),
+                ("xor3", "s0", "s0", "s1", "s2"), ("xor3", "s0", "s0", L0[(t - 15) % 16], L0B[(t - 15) % 16]),
+                ("shr", "s1", 17, y), ("shr", "s2", 19, y), ("shr", "s3", 10, y),
+                ("xor3", "s1", "s1", "s2", "s3"), ("xor3", "s1", "s1", L1[(t - 2) % 4], L1B[(t - 2) % 4]),
+                ("add", "s0", "s0", "s1"), ("add", "s1", W[(t - 7) % 16], W[t % 16]),
+                ("add", W[t % 16], "s0", "s1")]
     return [("shr", "s0", 7, x), ("shr", "s1", 18, x), ("shr", "s2", 3, x),
             ("xor3", "s0", "s0", "s1", "s2"), ("xor", "s0", "s0", L0[(t - 15) % 16]),
             ("shr", "s1", 17, y), ("shr", "s2", 19, y), ("shr", "s3", 10, y),
@@ -128,17 +171,18 @@ def merge(a, b):
     return out
 
 
-def block_ops(perm=False, lds=False):
-    """lds: byte swap on the LDS pipe (lds_bswap); otherwise in VALU doublings (or v_perm)."""
+def block_ops(perm=False, lds=False, mulf=True, merge3=True):
+    """lds: byte swap on the LDS pipe (lds_bswap); otherwise in VALU doublings (or v_perm).
+    mulf: part of each left shift by a v_mul_f32 on a denormal bit pattern (mulf_ok)."""
     ops = lds_bswap() if lds else []
     for t in range(64):
         if lds and t < 16:
             # no expansion yet: words 1..14's doubling chains interleave pairwise
             if t % 2 == 0 and 2 <= t <= 14:
-                ops += merge(lefts(t - 1), lefts(t))
+                ops += merge(lefts(t - 1, mulf, merge3), lefts(t, mulf, merge3))
         else:
-            e = bswap(t, perm) if t < 16 else expansion(t)
-            ops += merge(lefts(t - 1) if t >= 1 else [], e)
+            e = bswap(t, perm, mulf) if t < 16 else expansion(t, merge3)
+            ops += merge(lefts(t - 1, mulf, merge3) if t >= 1 else [], e)
         ops += [("addk", KR[t % 8], W[t % 16], K256[t]), ("dsw", KR[t % 8], wk_offset(t))]
     return ops
 
@@ -161,6 +205,8 @@ def asm_text(ops):
             lines.append(f"v_bitop3_b32 %[{op[1]}], %[{op[2]}], %[{op[3]}], %[{op[4]}] bitop3:0x96")
         elif k == "addk":
             lines.append(f"v_add_u32 %[{op[1]}], 0x{op[3]:08x}, %[{op[2]}]")
+        elif k == "mulf":
+            lines.append(f"v_mul_f32 %[{op[1]}], 0x{(127 + op[3]) << 23:08x}, %[{op[2]}]")
         elif k == "dsw":
             lines.append(f"ds_write_b32 %[la], %[{op[1]}] offset:{op[2]}")
         elif k == "perm":
@@ -179,13 +225,13 @@ def asm_text(ops):
     return lines
 
 
-def simulate(words_le, ops=None, perm=False, lds=False):
+def simulate(words_le, ops=None, perm=False, lds=False, mulf=True, merge3=True):
     """Run the op list on one lane: words_le = 16 little-endian-loaded dwords; returns
     {byte offset: value} of the W+K ds_write_b32s.  LDS is simulated bytewise (initially junk)."""
     regs = {W[i]: words_le[i] & M32 for i in range(16)}
     out = {}
     mem = bytearray(b"\xa5" * (16 * ROW))
-    for op in ops or block_ops(perm, lds):
+    for op in ops or block_ops(perm, lds, mulf, merge3):
         k = op[0]
         g = lambda r: regs[r]
         if k == "add":
@@ -202,6 +248,8 @@ def simulate(words_le, ops=None, perm=False, lds=False):
             regs[op[1]] = g(op[2]) ^ g(op[3]) ^ g(op[4])
         elif k == "addk":
             regs[op[1]] = (g(op[2]) + op[3]) & M32
+        elif k == "mulf":
+            regs[op[1]] = mulf_ok(g(op[2]), op[3])
         elif k == "dsw":
             out[op[2]] = regs[op[1]]
             mem[op[2]:op[2] + 4] = regs[op[1]].to_bytes(4, "little")
@@ -227,22 +275,25 @@ def reference_wk(block: bytes):
     return [(w[t] + K256[t]) & M32 for t in range(64)]
 
 
-def emit_inc(path, perm=False, lds=False):
-    ops = block_ops(perm, lds)
+def emit_inc(path, perm=False, lds=False, mulf=True, merge3=True):
+    ops = block_ops(perm, lds, mulf, merge3)
     body = asm_text(ops)
     n_valu = sum(1 for o in ops if not o[0].startswith(("ds", "wait")))
     n_lds = sum(1 for o in ops if o[0].startswith("ds"))
     hdr = [
         "// GENERATED by tools/gen_producer.py -- do not edit.  One block of the SIMPLE-class",
         "// SHA-256 message-schedule producer (byte swap, sigma0/sigma1 with left shifts as",
-        f"// doublings, W+K to LDS): {n_valu} VALU + {n_lds} LDS instructions.",
+        "// denormal v_mul_f32 and doublings -- needs f32 denormals preserved --, W+K to LDS):",
+        f"// {n_valu} VALU + {n_lds} LDS instructions.",
         "#pragma once",
         "#define S3H_PROD_SIMPLE_ASM \\",
     ]
     lines = [f'  "{l}\\n\\t" \\' for l in body]
     lines[-1] = lines[-1][:-2]
-    decl = ("#define S3H_PROD_SIMPLE_TEMPS uint32_t " + ", ".join(L0 + L1 + KR + TEMPS) + ";")
-    outs = ", ".join([f'[{r}] "+v"({r})' for r in W] + [f'[{r}] "=&v"({r})' for r in L0 + L1 + KR + TEMPS])
+    used = {r for o in ops for r in o[1:] if isinstance(r, str)}
+    temps = [r for r in L0 + L0B + L1 + L1B + KR + TEMPS if r in used]
+    decl = ("#define S3H_PROD_SIMPLE_TEMPS uint32_t " + ", ".join(temps) + ";")
+    outs = ", ".join([f'[{r}] "+v"({r})' for r in W] + [f'[{r}] "=&v"({r})' for r in temps])
     with open(path, "w") as f:
         f.write("\n".join(hdr + lines) + "\n\n")
         f.write(decl + "\n")
@@ -254,7 +305,7 @@ def emit_rows_inc(path, lds=False):
     leaving the row's four W+K words in outputs rk0..rk3 for one ds_write_b128 issued by the
     compiler (16 LDS writes per block instead of 64).  Measured: no change on the C4 shard
     (2,250 vs 2,246-2,271 cycles/block, profiles/r02_exp_skews_lds.jsonl)."""
-    ops = block_ops(False, lds)
+    ops = block_ops(False, lds, False, False)
     rows, cur, t = [], [], 0
     for op in ops:
         if op[0] == "dsw":
@@ -288,14 +339,17 @@ def main():
     ap.add_argument("--perm-bswap", action="store_true", help="byte swap with v_perm (experiment)")
     ap.add_argument("--lds-bswap", action="store_true", help="byte swap on the LDS pipe (experiment)")
     ap.add_argument("--rows", action="store_true", help="one asm statement per W+K row (experiment)")
+    ap.add_argument("--doublings", action="store_true",
+                    help="the first version: doublings only, L0/L1 xors (experiment)")
     args = ap.parse_args()
     lds = args.lds_bswap
     if args.rows:
         emit_rows_inc(args.out, lds)
         print(f"wrote {args.out} (rows)")
         return
-    emit_inc(args.out, args.perm_bswap, lds)
-    ops = block_ops(args.perm_bswap, lds)
+    fast = not args.doublings
+    emit_inc(args.out, args.perm_bswap, lds, fast, fast)
+    ops = block_ops(args.perm_bswap, lds, fast, fast)
     kinds = {}
     for o in ops:
         kinds[o[0]] = kinds.get(o[0], 0) + 1

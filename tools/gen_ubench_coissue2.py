@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Generates tools/ubench_coissue2.hip: wave A (one per SIMD) runs a consumer-like stream, wave B
+"""Generates tools/ubench_coissue2.hip (optional argv[1]: comma-separated B streams to run
+beside A = skew_round): wave A (one per SIMD) runs a consumer-like stream, wave B
 (a partner on the same SIMD) a candidate producer stream; reports both waves' cycles per
 instruction, lone and paired, with and without s_setprio 3 on A."""
 # skew round (gen_skew.py round_ops opcode sequence) on rotating state s0..s3, x0/x1
@@ -92,6 +93,26 @@ for name, tmpl in [("bfrev", "v_bfrev_b32 %[{d}], %[{a}]"), ("not", "v_not_b32 %
                    ("lshrrev_reg", "v_lshrrev_b32 %[{d}], %[{b}], %[{a}]"), ("min_u32", "v_min_u32 %[{d}], %[{a}], %[{b}]"),
                    ("cvt_f32_u32", "v_cvt_f32_u32 %[{d}], %[{a}]"), ("subrev", "v_subrev_u32 %[{d}], %[{a}], %[{b}]")]:
     B_STREAMS[name] = pure(tmpl)
+# round 2, candidates for left shifts / byte placement without doublings
+for name, tmpl in [("mul_lo_u32", "v_mul_lo_u32 %[{d}], %[{a}], %[{b}]"), ("mul_hi_u32", "v_mul_hi_u32 %[{d}], %[{a}], %[{b}]"),
+                   ("ldexp_f32", "v_ldexp_f32 %[{d}], %[{a}], %[{b}]"), ("exp_f32", "v_exp_f32 %[{d}], %[{a}]"),
+                   ("cvt_f32_ubyte0", "v_cvt_f32_ubyte0 %[{d}], %[{a}]"), ("cvt_u32_f32", "v_cvt_u32_f32 %[{d}], %[{a}]"),
+                   ("max_u32", "v_max_u32 %[{d}], %[{a}], %[{b}]"), ("cndmask", "v_cndmask_b32 %[{d}], %[{a}], %[{b}], vcc"),
+                   ("sub_f32", "v_sub_f32 %[{d}], %[{a}], %[{b}]"), ("lshlrev_b16", "v_lshlrev_b16 %[{d}], %[{b}], %[{a}]"),
+                   ("add_u16", "v_add_u16 %[{d}], %[{a}], %[{b}]"), ("mul_f32_lit", "v_mul_f32 %[{d}], 0x42000000, %[{a}]"),
+                   ("fmac_f32", "v_fmac_f32 %[{d}], %[{a}], %[{b}]"), ("mul_legacy", "v_mul_legacy_f32 %[{d}], %[{a}], %[{b}]"),
+                   ("ashr_reg", "v_ashrrev_i32 %[{d}], %[{b}], %[{a}]"), ("bfe_u32", "v_bfe_u32 %[{d}], %[{a}], 8, 8"),
+                   ("mul_lo_u16", "v_mul_lo_u16 %[{d}], %[{a}], %[{b}]"), ("max_f32", "v_max_f32 %[{d}], %[{a}], %[{b}]"),
+                   ("subrev_f32", "v_subrev_f32 %[{d}], %[{a}], %[{b}]"), ("mov_dpp", "v_mov_b32_dpp %[{d}], %[{a}] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")]:
+    B_STREAMS[name] = pure(tmpl)
+for name, op in [("pk_mul_f32", "v_pk_mul_f32"), ("pk_add_f32", "v_pk_add_f32"), ("pk_fma_f32", "v_pk_fma_f32"),
+                 ("lshlrev_b64", "v_lshlrev_b64")]:
+    if name == "lshlrev_b64":
+        B_STREAMS[name] = [f"v_lshlrev_b64 %[p{i%4}], 7, %[p{(i+1)%4}]" for i in range(128)]
+    elif name == "pk_fma_f32":
+        B_STREAMS[name] = [f"{op} %[p{i%4}], %[p{(i+1)%4}], %[p{(i+2)%4}], %[p{i%4}]" for i in range(128)]
+    else:
+        B_STREAMS[name] = [f"{op} %[p{i%4}], %[p{(i+1)%4}], %[p{(i+2)%4}]" for i in range(128)]
 # 64-bit right shift of a {x, x} pair -> rotr in the low word: pairs (b0,b1), (b2,b3), ...
 B_STREAMS["lshrrev_b64"] = [f"v_lshrrev_b64 %[p{i%4}], 7, %[p{(i+1)%4}]" for i in range(128)]
 def expansion2(i):
@@ -146,7 +167,7 @@ for i, n in enumerate(bn):
     elif n == "skew_round":
         out.append(f"  {kw} (TB == {i}) {{ per = {len(ROUND)}; return run_a<0>(iters, am, mk, w, lane); }}")
     else:
-        regs = ["p0", "p1", "p2", "p3"] if n == "lshrrev_b64" else B_REGS
+        regs = ["p0", "p1", "p2", "p3"] if n in ("lshrrev_b64", "lshlrev_b64") or n.startswith("pk_") and n.endswith("f32") else B_REGS
         out.append(f"  {kw} (TB == {i}) {{ per = {len(B_STREAMS[n])}; for (int i = 0; i < iters; ++i) {asm_block(B_STREAMS[n], regs)} }}")
 out.append("  return " + " ^ ".join(f"b{i}" for i in range(8)) + " ^ u0 ^ uint32_t(p0 ^ p1 ^ p2 ^ p3);\n}")
 out.append('''
@@ -198,8 +219,10 @@ int run(const char* tag) {
 }
 int main() {''')
 out.append('  if (run<0, 0, true>("(warm-up, clocks ramping)")) return 1;')
-for ta in range(2):
-    for tb in [bn.index(x) for x in ("none", "add_u32", "producer_2c", "producer_2c_perm", "producer_lshl")]:
+import sys
+PAIRS = sys.argv[1].split(",") if len(sys.argv) > 1 else ["none", "add_u32", "producer_2c", "producer_2c_perm", "producer_lshl"]
+for ta in ([1] if len(sys.argv) > 1 else range(2)):   # with a list: A = skew_round only
+    for tb in [bn.index(x) for x in PAIRS]:
         for prio in ("true",):
             out.append(f'  if (run<{ta}, {tb}, {prio}>("")) return 1;')
 out.append("  return 0;\n}")
