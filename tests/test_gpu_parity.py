@@ -63,6 +63,30 @@ def test_random_ragged_vs_oracle(torch_cuda, oracle, kernel):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("kernel", ["skews", "skew"])
+def test_constant_byte_parts(torch_cuda, kernel):
+    """Constant-byte parts (0x00, 0x01, 0x7f, 0x80, 0xff, 0xa5) at misalignments 0 and 3: the
+    extremes of the shared-SIMD producer's denormal v_mul_f32 left shifts (tools/gen_producer.py
+    mulf_ok), checked against hashlib."""
+    import hashlib
+    fills, lens = (0x00, 0x01, 0x7F, 0x80, 0xFF, 0xA5), (64, 1000, 65536 + 55, (1 << 20) + 13)
+    offs, want, pos, chunks = [], [], 0, []
+    for mis in (0, 3):
+        for f in fills:
+            for L in lens:
+                pos += (-pos) % 64 + mis
+                offs.append(pos)
+                chunks.append((pos, L, f))
+                want.append(hashlib.sha256(bytes([f]) * L).hexdigest())
+                pos += L
+    host = np.zeros(pos + 64, dtype=np.uint8)
+    for o, L, f in chunks:
+        host[o:o + L] = f
+    got = s3.digests_to_text(_run(torch_cuda, host, offs, [c[1] for c in chunks], kernel))
+    bad = [(c[2], c[1], c[0] % 4) for c, g, w in zip(chunks, got, want) if g != w]
+    assert not bad, bad[:10]
+
+
 def test_kernels_agree_on_many_small_parts(torch_cuda, oracle):
     """n > 65536 exercises the AUTO switch to the fused kernel; overlapping parts allowed."""
     assert s3.Plan([0] * 70000, [1] * 70000).info()["kernel"] == "lane"
