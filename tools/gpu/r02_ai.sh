@@ -1,6 +1,8 @@
 #!/bin/bash
 # Round-2 GPU pass AI: C3 solo workgroups on the barrier body (S3H_EXP_SOLO_BARRIER, experiment
 # build) vs the product's flag-synchronised body, alternating on one box.
+# (The experiment, removed after this measurement: in sha256_skew_pairs_kernel, for b < A.solo,
+# skew_body<1, false, false>(A, b, wave >> 1, L[0], nullptr) instead of the flag body.)
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
