@@ -196,8 +196,9 @@ uint64_t sort_slots(const uint64_t* offsets, const uint64_t* lengths, uint64_t n
 
 // `cus`: the device's CUs.  Above 4,096 parts, while one 32-chain workgroup per CU holds the
 // batch (8,192 parts on MI355X: the C4 shard), the shared-SIMD skew kernel runs every chain
-// at the skew kernel's 8 VALU per round with its producer on the same SIMD: C4 shard 493 vs
-// 465 GiB/s for skewp (profiles/r02_bench_c4_skews.jsonl).
+// at the skew kernel's 8 VALU per round with its producer on the same SIMD: C4 shard 500 vs
+// 469 GiB/s for skewp on one box (profiles/r02_bench_c4_skews_mulf.jsonl), at about twice the
+// board power (r02_smi_c4_power.txt; INTEGRATION.md: pass S3H_KERNEL_SKEWP to trade it back).
 int resolve_kernel(int algo, uint64_t n, int kernel, uint64_t cus) {
   if (algo == S3H_ALGO_MD5) return S3H_KERNEL_PC;  // MD5 has one kernel (4 VALU per step)
   if (kernel != S3H_KERNEL_AUTO) return kernel;
