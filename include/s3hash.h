@@ -61,7 +61,8 @@ int s3h_api_version(void);
 /* Free the host path's cached per-device contexts.  Between s3h_*_batch_host /
  * s3h_sha256_file_parts / s3h_verify_batch_host calls each device keeps its streams, plans,
  * digest buffers, at most 1 GiB of HBM ring (larger rings are freed when the call returns)
- * and at most 96 MiB of pinned staging; s3h_trim releases all of it for idle devices. */
+ * and at most 96 MiB of pinned staging (384 MiB after s3h_sha256_file_parts); s3h_trim
+ * releases all of it for idle devices. */
 int s3h_trim(void);
 /* Number of visible HIP devices; S3H_ENODEV (and *count = 0) when there is none. */
 int s3h_device_count(int *count);
@@ -144,7 +145,9 @@ int s3h_sha256_batch_host_on(const uint8_t *const *parts, const uint64_t *length
  * `path` -- the (file, offset, size) parts that S3Api::UploadFilePart sends
  * (lib/src/api/multipart_upload.cpp:216-223 -> WebClient::UploadFile, webclient.cpp:331-355),
  * i.e. a batched sha256::sha256_file (lib/hash/sha256.cpp:183-233) over ranges.  Host threads
- * pread each slice straight into the pinned staging ring (no mmap, no intermediate copy).
+ * pread each slice straight into the pinned staging ring (no intermediate copy); its slots
+ * are 128 MiB (32 KiB slices up to 4,096 parts per device), so the per-slice syscall does not
+ * dominate.
  * S3H_EINVAL when the file cannot be opened or is shorter than a part.  Blocking. */
 int s3h_sha256_file_parts(const char *path, const uint64_t *offsets, const uint64_t *lengths,
                           uint64_t n, uint32_t *digests, int ndevices, uint64_t slice_bytes);

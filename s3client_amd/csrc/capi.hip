@@ -515,6 +515,9 @@ constexpr int kHostRing = 3;
 constexpr int kHostMaxAlgo = 2;
 constexpr uint64_t kStageSlot = 32ull << 20;     // pinned staging bytes per ring slot
 constexpr uint64_t kKeepRingBytes = 1ull << 30;  // largest HBM ring kept between calls
+// File ranges stage with one pread per part per slice, whose syscall costs more than it moves
+// below ~32 KiB: their slots are 128 MiB (32 KiB slices up to 4,096 parts per device).
+constexpr uint64_t kFileStageSlot = 128ull << 20;
 
 // Where a shard's part bytes come from: host memory (pinned or pageable) or byte ranges of an
 // open file (read with pread straight into the pinned staging ring).
@@ -767,7 +770,7 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
   bool direct_pageable = staged && parts && n * 64 > kStageSlot;
   if (direct_pageable) staged = false;
   if (slice == 0)
-    slice = staged ? std::max<uint64_t>(64, kStageSlot / n / 64 * 64)
+    slice = staged ? std::max<uint64_t>(64, (parts ? kStageSlot : kFileStageSlot) / n / 64 * 64)
             : uniform ? (256ull << 10) : (2ull << 20);
   const uint64_t longest = *std::max_element(lens.begin(), lens.end());
   slice = std::min(slice, std::max<uint64_t>(64, (longest + 63) / 64 * 64));  // no idle slot bytes
