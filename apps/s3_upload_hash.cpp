@@ -6,8 +6,13 @@
 // (upload.cpp:60 passes no payloadHash).  This tool computes the same part geometry, hashes
 // every part in ONE batched GPU call (libs3hash.so, host-resident path: H2D included), and
 // emits the signed UploadPart headers each part would carry, with the real digest in
-// x-amz-content-sha256.  No network I/O (libcurl headers, Lyra and MinIO are not available
-// in this environment): `--print-headers` shows what would be sent.
+// x-amz-content-sha256.  `--print-headers` shows what would be sent.  `--send` PUTs every
+// part with those headers to a plain-HTTP loopback endpoint (config 5: libcurl's headers and
+// MinIO are absent from this image, so the endpoint is tests/s3_mock_server.py, which checks
+// each body's SHA-256 against x-amz-content-sha256 and verifies the SigV4 signature): each job
+// thread hashes (per-job mode) and PUTs its own parts in order, as upload.cpp:136-140 runs
+// UploadParts, and the timed pass is then hash + upload.  Only UploadPart requests are sent
+// (no CreateMultipartUpload / CompleteMultipartUpload XML), one connection per part.
 //
 // Part sources (how the bytes reach the hash, mirroring the reference's two upload paths):
 //   --source file    UploadFile (upload.cpp:113-149): parts are (file, offset, size) ranges as
@@ -22,14 +27,19 @@
 //                    upload.cpp:136-140 runs UploadParts), instead of one call for all parts.
 //
 //   s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory] [--per-job]
-//                  [--cpu] [--verify] [--print-headers] [--devices N] [--repeat R]
+//                  [--cpu] [--verify] [--print-headers] [--send] [--devices N] [--repeat R]
 //                  [--endpoint URL --bucket B --key K --access A --secret S --upload-id ID]
 #include <fcntl.h>
+#include <netdb.h>
 #include <sys/mman.h>
+#include <sys/sendfile.h>
+#include <sys/socket.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <chrono>
+#include <csignal>
 #include <future>
 #include <cstdio>
 #include <cstdlib>
@@ -68,6 +78,59 @@ std::vector<Part> geometry(uint64_t size, int jobs, int parts_per_job) {
   return out;
 }
 
+// One UploadPart request over plain HTTP/1.1 (Connection: close): the signed headers, then
+// the body from memory or, for file parts, by sendfile from the open file (what libcurl's
+// read callback does in WebClient::UploadFile, webclient.cpp:331-355).  Returns the HTTP
+// status, or -1 on a socket error.
+int put_part(const std::string& host, const std::string& port, const std::string& target,
+             const s3h::sigv4::Map& headers, const uint8_t* mem, int fd, uint64_t off,
+             uint64_t size) {
+  addrinfo hints{}, *ai = nullptr;
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  if (getaddrinfo(host.c_str(), port.c_str(), &hints, &ai) != 0 || !ai) return -1;
+  const int sock = socket(ai->ai_family, ai->ai_socktype, ai->ai_protocol);
+  const bool connected = sock >= 0 && connect(sock, ai->ai_addr, ai->ai_addrlen) == 0;
+  freeaddrinfo(ai);
+  if (!connected) {
+    if (sock >= 0) close(sock);
+    return -1;
+  }
+  auto send_all = [&](const void* p, size_t n) {
+    const char* c = static_cast<const char*>(p);
+    while (n > 0) {
+      const ssize_t w = send(sock, c, n, MSG_NOSIGNAL);
+      if (w <= 0) return false;
+      c += w;
+      n -= size_t(w);
+    }
+    return true;
+  };
+  std::string req = "PUT " + target + " HTTP/1.1\r\n";
+  for (const auto& kv : headers) req += kv.first + ": " + kv.second + "\r\n";
+  req += "Connection: close\r\n\r\n";
+  bool ok = send_all(req.data(), req.size());
+  if (ok && mem) {
+    ok = send_all(mem, size);
+  } else if (ok) {
+    off_t o = off_t(off);
+    for (uint64_t left = size; ok && left > 0;) {
+      const ssize_t w = sendfile(sock, fd, &o, left);
+      ok = w > 0;
+      if (ok) left -= uint64_t(w);
+    }
+  }
+  std::string resp;
+  char buf[4096];
+  for (ssize_t r; ok && resp.find("\r\n") == std::string::npos &&
+                  (r = recv(sock, buf, sizeof buf, 0)) > 0;)
+    resp.append(buf, size_t(r));
+  close(sock);
+  int code = -1;
+  if (ok && std::sscanf(resp.c_str(), "HTTP/%*d.%*d %d", &code) != 1) code = -1;
+  return code;
+}
+
 double now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -75,7 +138,7 @@ double now() {
 void usage() {
   std::fprintf(stderr,
                "usage: s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory]\n"
-               "       [--per-job] [--cpu] [--verify] [--print-headers] [--endpoint URL --bucket B\n"
+               "       [--per-job] [--cpu] [--verify] [--print-headers] [--send] [--endpoint URL --bucket B\n"
                "        --key K --access A --secret S --upload-id ID] [--devices N] [--repeat R]\n");
 }
 
@@ -86,7 +149,7 @@ int main(int argc, char** argv) {
   std::string access = "ACCESS", secret = "SECRET", upload_id = "UPLOAD-ID";
   std::string source = "file";
   int jobs = 1, ppj = 1, devices = 0, repeat = 1;
-  bool cpu = false, verify = false, print_headers = false, per_job = false;
+  bool cpu = false, verify = false, print_headers = false, per_job = false, send_parts = false;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -99,6 +162,7 @@ int main(int argc, char** argv) {
     else if (a == "--cpu") cpu = true;
     else if (a == "--verify") verify = true;
     else if (a == "--print-headers") print_headers = true;
+    else if (a == "--send") send_parts = true;
     else if (a == "--endpoint") endpoint = next();
     else if (a == "--bucket") bucket = next();
     else if (a == "--key") key = next();
@@ -111,6 +175,7 @@ int main(int argc, char** argv) {
     else if (a == "--per-job") per_job = true;
     else { usage(); return 2; }
   }
+  std::signal(SIGPIPE, SIG_IGN);  // a closed connection fails its PUT (sendfile has no MSG_NOSIGNAL)
   if (file.empty() || jobs < 1 || ppj < 1 || repeat < 1 ||
       (source != "file" && source != "mmap" && source != "memory")) { usage(); return 2; }
 
@@ -161,54 +226,88 @@ int main(int argc, char** argv) {
     }
     init_s = now() - ti;
   }
-  // One hash pass over all parts: the CPU drop-in on one std::thread per job (as upload.cpp
-  // runs its jobs), or one batched GPU call.
-  auto hash_pass = [&]() -> bool {
-    if (cpu) {
-      std::vector<std::thread> pool;
-      for (int j = 0; j < jobs; ++j)
-        pool.emplace_back([&, j] {
-          for (size_t i = 0; i < parts.size(); ++i)
-            if (parts[i].job == j) {
-              uint32_t h[8];
-              sha256::sha256(ptrs[i], lens[i], h);
-              char t[65];
-              sha256::hash_to_text(h, t);
-              hex[i] = t;
-            }
-        });
-      for (auto& t : pool) t.join();
-      return true;
+  // Signed UploadPart headers of part i: its digest in x-amz-content-sha256 instead of
+  // UNSIGNED-PAYLOAD (aws_sign.cpp:236-237); the memory path forwards it too, where the
+  // reference's DoUploadPart drops it (multipart_upload.cpp:131-136).
+  auto part_config = [&](size_t i) {
+    s3h::sigv4::SignConfig c;
+    c.access = access;
+    c.secret = secret;
+    c.endpoint = endpoint;
+    c.method = "PUT";
+    c.bucket = bucket;
+    c.key = key;
+    c.payloadHash = hex[i];
+    // partNumber = i + 1 (multipart_upload.cpp:79, :126)
+    c.parameters = {{"partNumber", std::to_string(parts[i].number + 1)}, {"uploadId", upload_id}};
+    c.headers = {{"content-length", std::to_string(parts[i].size)}};
+    return c;
+  };
+  std::string host, port;
+  if (send_parts) {  // http://HOST:PORT only (loopback, no TLS)
+    const size_t h0 = endpoint.find("://"), c = endpoint.rfind(':');
+    if (endpoint.rfind("http://", 0) != 0 || c == std::string::npos || c <= h0 + 3) {
+      std::fprintf(stderr, "--send needs --endpoint http://HOST:PORT\n");
+      return 2;
     }
-    // GPU: the parts of `idx` through the chosen source, hex digests into hex[idx[k]]
-    auto gpu = [&](const std::vector<size_t>& idx) {
-      std::vector<const uint8_t*> p;
-      std::vector<uint64_t> l, o;
-      for (size_t i : idx) {
-        p.push_back(ptrs[i]);
-        l.push_back(lens[i]);
-        o.push_back(offs[i]);
-      }
-      const std::vector<std::string> h = source == "file"
-                                             ? sha256::file_part_hashes(file, o, l, devices)
-                                             : sha256::payload_hashes(p, l, devices);
-      for (size_t k = 0; k < idx.size(); ++k) hex[idx[k]] = h[k];
-    };
+    host = endpoint.substr(h0 + 3, c - h0 - 3);
+    port = endpoint.substr(c + 1);
+  }
+  std::atomic<int> put_failed{0};
+  auto put = [&](size_t i) {
+    const s3h::sigv4::SignConfig c = part_config(i);
+    const std::string target = "/" + bucket + "/" + key + "?" + s3h::sigv4::UrlEncode(c.parameters);
+    const uint8_t* mem = source == "file" ? nullptr : ptrs[i];
+    if (put_part(host, port, target, s3h::sigv4::SignHeaders(c), mem, fd, offs[i], lens[i]) != 200)
+      ++put_failed;
+  };
+  std::vector<std::vector<size_t>> job_parts(jobs);
+  for (size_t i = 0; i < parts.size(); ++i) job_parts[parts[i].job].push_back(i);
+  auto cpu_hash = [&](size_t i) {
+    uint32_t h[8];
+    sha256::sha256(ptrs[i], lens[i], h);
+    char t[65];
+    sha256::hash_to_text(h, t);
+    hex[i] = t;
+  };
+  // GPU: the parts of `idx` through the chosen source, hex digests into hex[idx[k]]
+  auto gpu = [&](const std::vector<size_t>& idx) {
+    std::vector<const uint8_t*> p;
+    std::vector<uint64_t> l, o;
+    for (size_t i : idx) {
+      p.push_back(ptrs[i]);
+      l.push_back(lens[i]);
+      o.push_back(offs[i]);
+    }
+    const std::vector<std::string> h = source == "file"
+                                           ? sha256::file_part_hashes(file, o, l, devices)
+                                           : sha256::payload_hashes(p, l, devices);
+    for (size_t k = 0; k < idx.size(); ++k) hex[idx[k]] = h[k];
+  };
+  // One pass over all parts.  Job threads as upload.cpp:136-140 runs them: the CPU drop-in
+  // hashes each part of its job (and, with --send, PUTs it right after); on the GPU either one
+  // batched call for all parts (then the jobs PUT) or, --per-job, one concurrent batch call per
+  // job, each job then PUTting its own parts.
+  auto hash_pass = [&]() -> bool {
     try {
-      if (per_job) {  // one concurrent batch call per job, like upload.cpp:136-140
-        std::vector<std::future<void>> fut;
-        for (int j = 0; j < jobs; ++j) {
-          std::vector<size_t> idx;
-          for (size_t i = 0; i < parts.size(); ++i)
-            if (parts[i].job == j) idx.push_back(i);
-          if (!idx.empty()) fut.push_back(std::async(std::launch::async, gpu, idx));
-        }
-        for (auto& f : fut) f.get();
-      } else {
+      if (!cpu && !per_job) {
         std::vector<size_t> all(parts.size());
         for (size_t i = 0; i < all.size(); ++i) all[i] = i;
         gpu(all);
+        if (!send_parts) return true;
       }
+      std::vector<std::future<void>> fut;
+      for (int j = 0; j < jobs; ++j) {
+        if (job_parts[j].empty()) continue;
+        fut.push_back(std::async(std::launch::async, [&, j] {
+          if (!cpu && per_job) gpu(job_parts[j]);
+          for (size_t i : job_parts[j]) {
+            if (cpu) cpu_hash(i);
+            if (send_parts) put(i);
+          }
+        }));
+      }
+      for (auto& f : fut) f.get();
     } catch (const std::exception& e) {
       std::fprintf(stderr, "%s\n", e.what());
       return false;
@@ -241,33 +340,22 @@ int main(int argc, char** argv) {
                 (unsigned long long)parts[i].offset, (unsigned long long)parts[i].size,
                 hex[i].c_str());
   if (print_headers)
-    for (size_t i = 0; i < parts.size(); ++i) {
-      s3h::sigv4::SignConfig c;
-      c.access = access;
-      c.secret = secret;
-      c.endpoint = endpoint;
-      c.method = "PUT";
-      c.bucket = bucket;
-      c.key = key;
-      // instead of UNSIGNED-PAYLOAD (aws_sign.cpp:236-237); the memory path forwards it too,
-      // where the reference's DoUploadPart drops it (multipart_upload.cpp:131-136)
-      c.payloadHash = hex[i];
-      // partNumber = i + 1 (multipart_upload.cpp:79, :126)
-      c.parameters = {{"partNumber", std::to_string(parts[i].number + 1)}, {"uploadId", upload_id}};
-      c.headers = {{"content-length", std::to_string(parts[i].size)}};
-      for (const auto& kv : s3h::sigv4::SignHeaders(c))
+    for (size_t i = 0; i < parts.size(); ++i)
+      for (const auto& kv : s3h::sigv4::SignHeaders(part_config(i)))
         std::printf("# part %d %s: %s\n", parts[i].number, kv.first.c_str(), kv.second.c_str());
-    }
-  const std::string what = cpu ? std::string("cpu lib/hash drop-in")
-                               : "gpu batch (H2D included, source " + source +
-                                     (per_job ? ", one call per job" : ", one call") + ")";
+  std::string what = cpu ? std::string("cpu lib/hash drop-in")
+                         : "gpu batch (H2D included, source " + source +
+                               (per_job ? ", one call per job" : ", one call") + ")";
+  if (send_parts) what = "upload (hash + PUT to " + endpoint + ", " + std::to_string(jobs) + " jobs), " + what;
   std::fprintf(stderr, "%s: %zu parts, %.3f GiB in %.3f s = %.3f GiB/s%s", what.c_str(), parts.size(),
                double(size) / (1 << 30), dt, double(size) / (1 << 30) / dt,
                verify ? (mismatches ? ", VERIFY FAILED" : ", verified vs CPU") : "");
+  if (send_parts)
+    std::fprintf(stderr, " (%d of %zu PUTs not 200)", put_failed.load(), parts.size() * size_t(repeat));
   if (repeat > 1) std::fprintf(stderr, " (pass %d of %d; first pass %.3f s)", repeat, repeat, first);
   if (!cpu) std::fprintf(stderr, " (GPU runtime start-up before it: %.3f s)", init_s);
   std::fprintf(stderr, "\n");
   munmap(const_cast<uint8_t*>(data), size);
   close(fd);
-  return mismatches ? 1 : 0;
+  return mismatches || put_failed.load() ? 1 : 0;
 }

@@ -447,7 +447,7 @@ int dual_launch(s3h_plan_s* S, s3h_plan_s* M, const void* d_base, uint32_t* d_sh
 class CopyPool {
  public:
   explicit CopyPool(unsigned workers) {
-    for (unsigned i = 0; i < workers; ++i) threads_.emplace_back([this] { loop(); });
+    for (unsigned i = 0; i < workers; ++i) threads_.emplace_back([this, i] { loop(i); });
   }
   ~CopyPool() {
     {
@@ -457,13 +457,16 @@ class CopyPool {
     cv_.notify_all();
     for (auto& t : threads_) t.join();
   }
-  // fn(i) for every i in [0, n), on the workers and the calling thread; returns when done.
-  void run(uint64_t n, const std::function<void(uint64_t)>& fn) {
+  unsigned size() const { return unsigned(threads_.size()); }
+  // fn(i) for every i in [0, n), on the first `active` workers and the calling thread; returns
+  // when done.
+  void run(uint64_t n, const std::function<void(uint64_t)>& fn, unsigned active) {
     {
       std::lock_guard<std::mutex> l(m_);
       fn_ = &fn;
       n_ = n;
       next_ = 0;
+      active_ = active;
       busy_ = threads_.size();
       ++gen_;
     }
@@ -478,16 +481,18 @@ class CopyPool {
   void work() {
     for (uint64_t i; (i = next_.fetch_add(1)) < n_;) (*fn_)(i);
   }
-  void loop() {
+  void loop(unsigned index) {
     uint64_t seen = 0;
     for (;;) {
+      bool mine;
       {
         std::unique_lock<std::mutex> l(m_);
         cv_.wait(l, [&] { return stop_ || gen_ != seen; });
         if (stop_) return;
         seen = gen_;
+        mine = index < active_;
       }
-      work();
+      if (mine) work();
       std::lock_guard<std::mutex> l(m_);
       if (--busy_ == 0) done_.notify_one();
     }
@@ -498,6 +503,7 @@ class CopyPool {
   const std::function<void(uint64_t)>* fn_ = nullptr;
   std::atomic<uint64_t> next_{0};
   uint64_t n_ = 0, gen_ = 0;
+  unsigned active_ = 0;
   size_t busy_ = 0;
   bool stop_ = false;
 };
@@ -509,32 +515,51 @@ class CopyPool {
 // after file; creating and freeing these per call cost ~8 ms of a 27 ms call on a 512 MiB
 // file, profiles/r01_app_upload_hash.txt).  Buffers only grow; an HBM ring above
 // kKeepRingBytes is freed when the call returns, so a cached context holds at most
-// kKeepRingBytes of HBM plus 3 x kStageSlot of pinned memory; s3h_trim() frees idle contexts.
-// A call that finds the device's context busy (a concurrent caller) builds a private one.
+// kKeepRingBytes of HBM plus its staging; s3h_trim() frees idle contexts.  Concurrent calls on
+// one device each take a context of their own from the device's idle list (HostCtxCache).
 constexpr int kHostRing = 3;
 constexpr int kHostMaxAlgo = 2;
 constexpr uint64_t kStageSlot = 32ull << 20;     // pinned staging bytes per ring slot
 constexpr uint64_t kKeepRingBytes = 1ull << 30;  // largest HBM ring kept between calls
+// Further idle contexts of a device (concurrent callers) keep at most these; up to kIdleCtx.
+constexpr uint64_t kKeepRingBytes2 = 256ull << 20, kKeepStageBytes2 = 96ull << 20;
+constexpr size_t kIdleCtx = 16;
 // File ranges stage with one pread per part per slice, whose syscall costs more than it moves
-// below ~32 KiB: their slots are 128 MiB (32 KiB slices up to 4,096 parts per device).
+// below ~32 KiB: their slices are at least 32 KiB up to 4,096 parts per device (slots of up
+// to 128 MiB), 128 MiB / n beyond.
 constexpr uint64_t kFileStageSlot = 128ull << 20;
 
-// Where a shard's part bytes come from: host memory (pinned or pageable) or byte ranges of an
-// open file (read with pread straight into the pinned staging ring).
+// One part of a merged batch (concurrent callers, below): host memory or a file range.
+struct PartRef {
+  const uint8_t* mem;
+  int fd;
+  uint64_t off;
+};
+
+// Where a shard's part bytes come from: host memory (pinned or pageable), byte ranges of an
+// open file (read with pread straight into the pinned staging ring), or per-part references
+// (a batch merged from concurrent calls whose sources differ).
 struct PartSource {
-  const uint8_t* const* parts = nullptr;  // memory parts, or null for a file
+  const uint8_t* const* parts = nullptr;  // memory parts, or null for a file / refs
   int fd = -1;                            // file parts: part i = [file_off[i], +lengths[i])
   const uint64_t* file_off = nullptr;
+  const PartRef* refs = nullptr;
+  PartRef ref(uint64_t i) const {
+    if (parts) return {parts[i], -1, 0};
+    if (refs) return refs[i];
+    return {nullptr, fd, file_off[i]};
+  }
   bool fill(uint64_t i, uint64_t byte0, uint64_t cnt, uint8_t* dst) const {
-    if (parts) {
-      std::memcpy(dst, parts[i] + byte0, cnt);
+    const PartRef r = ref(i);
+    if (r.mem) {
+      std::memcpy(dst, r.mem + byte0, cnt);
       return true;
     }
     for (uint64_t done = 0; done < cnt;) {
-      const ssize_t r = pread(fd, dst + done, cnt - done, off_t(file_off[i] + byte0 + done));
-      if (r < 0 && errno == EINTR) continue;
-      if (r <= 0) return false;  // error or a part past the end of the file
-      done += uint64_t(r);
+      const ssize_t r2 = pread(r.fd, dst + done, cnt - done, off_t(r.off + byte0 + done));
+      if (r2 < 0 && errno == EINTR) continue;
+      if (r2 <= 0) return false;  // error or a part past the end of the file
+      done += uint64_t(r2);
     }
     return true;
   }
@@ -542,11 +567,10 @@ struct PartSource {
 
 struct HostCtx {
   int device = 0;
-  bool busy = false;
+  unsigned share = 1;  // calls on this device when this one started (copy threads are split)
   hipStream_t copy_s = nullptr, hash_s[kHostMaxAlgo] = {};
   hipEvent_t copied[kHostRing] = {}, hashed[kHostRing][kHostMaxAlgo] = {};
   std::unique_ptr<CopyPool> pool;
-  unsigned pool_workers = 0;
   s3h_plan_s* plan[kHostMaxAlgo] = {};
   uint32_t* d_dig[kHostMaxAlgo] = {};
   uint64_t dig_bytes[kHostMaxAlgo] = {};
@@ -590,11 +614,8 @@ struct HostCtx {
   hipError_t ensure_digests(int a, uint64_t bytes) {
     return grow_dev(reinterpret_cast<uint8_t**>(&d_dig[a]), &dig_bytes[a], bytes);
   }
-  CopyPool* ensure_pool(unsigned workers) {
-    if (!pool || pool_workers != workers) {
-      pool.reset(new CopyPool(workers));
-      pool_workers = workers;
-    }
+  CopyPool* ensure_pool(unsigned workers) {  // grows only; run() chooses how many take part
+    if (!pool || pool->size() < workers) pool.reset(new CopyPool(workers));
     return pool.get();
   }
   // plan[a] for algorithm `algo` with room for n parts (reallocated only to grow)
@@ -621,11 +642,18 @@ struct HostCtx {
     for (hipStream_t st : hash_s)
       if (st) (void)hipStreamSynchronize(st);
   }
-  void release_large() {  // after a call: do not keep a large HBM ring
-    if (ring_bytes > kKeepRingBytes) {
+  // After a call: do not keep a large HBM ring; a context kept beside another idle one keeps
+  // at most a small ring and staging.
+  void release_large(bool secondary) {
+    if (ring_bytes > (secondary ? kKeepRingBytes2 : kKeepRingBytes)) {
       (void)hipFree(ring);
       ring = nullptr;
       ring_bytes = 0;
+    }
+    if (secondary && stage_bytes > kKeepStageBytes2) {
+      (void)hipHostFree(stage);
+      stage = nullptr;
+      stage_bytes = 0;
     }
   }
   ~HostCtx() {
@@ -650,40 +678,53 @@ struct HostCtx {
   }
 };
 
+// Per device: the idle contexts (most recently used first out) and the number of calls
+// running.  Concurrent callers -- upload.cpp:136-140's std::async jobs, each hashing its own
+// parts -- each take an idle context or build one, and return it when done, so the next round
+// of concurrent calls reuses streams, plans, rings and copy threads instead of allocating them
+// (up to kIdleCtx per device).
 struct HostCtxCache {
+  struct Dev {
+    std::vector<HostCtx*> idle;
+    unsigned running = 0;
+  };
   std::mutex m;
-  std::vector<HostCtx*> v;  // indexed by device
-  // The device's cached context, or a private one while another call holds it.
+  std::vector<Dev> v;  // indexed by device
   HostCtx* acquire(int device) {
     std::lock_guard<std::mutex> l(m);
-    if (v.size() <= size_t(device)) v.resize(device + 1, nullptr);
-    HostCtx*& c = v[device];
-    if (!c) {
+    if (v.size() <= size_t(device)) v.resize(device + 1);
+    Dev& d = v[device];
+    HostCtx* c = nullptr;
+    if (!d.idle.empty()) {
+      c = d.idle.back();
+      d.idle.pop_back();
+    } else {
       c = new HostCtx();
       c->device = device;
     }
-    if (c->busy) {
-      auto* p = new HostCtx();
-      p->device = device;
-      return p;
-    }
-    c->busy = true;
+    c->share = ++d.running;
     return c;
   }
-  // ok: the call succeeded (keep the cached context); a failed call drops its context.
+  // ok: the call succeeded (keep the context); a failed call drops its context.
   void release(HostCtx* c, bool ok) {
-    {
-      DeviceGuard g(c->device);
-      c->release_large();
-    }
+    bool keep, secondary;
     {
       std::lock_guard<std::mutex> l(m);
-      if (size_t(c->device) < v.size() && v[c->device] == c) {
-        if (ok) {
-          c->busy = false;
-          return;
-        }
-        v[c->device] = nullptr;
+      Dev& d = v[c->device];
+      --d.running;
+      keep = ok && d.idle.size() < kIdleCtx;
+      secondary = !d.idle.empty();
+    }
+    if (keep) {
+      {
+        DeviceGuard g(c->device);
+        c->release_large(secondary);
+      }
+      std::lock_guard<std::mutex> l(m);
+      Dev& d = v[c->device];
+      if (d.idle.size() < kIdleCtx) {
+        d.idle.push_back(c);
+        return;
       }
     }
     delete c;
@@ -692,11 +733,10 @@ struct HostCtxCache {
     std::vector<HostCtx*> idle;
     {
       std::lock_guard<std::mutex> l(m);
-      for (HostCtx*& c : v)
-        if (c && !c->busy) {
-          idle.push_back(c);
-          c = nullptr;
-        }
+      for (Dev& d : v) {
+        idle.insert(idle.end(), d.idle.begin(), d.idle.end());
+        d.idle.clear();
+      }
     }
     for (HostCtx* c : idle) delete c;
   }
@@ -770,7 +810,8 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
   bool direct_pageable = staged && parts && n * 64 > kStageSlot;
   if (direct_pageable) staged = false;
   if (slice == 0)
-    slice = staged ? std::max<uint64_t>(64, (parts ? kStageSlot : kFileStageSlot) / n / 64 * 64)
+    slice = staged ? std::max<uint64_t>(std::max<uint64_t>(64, kStageSlot / n / 64 * 64),
+                                        parts ? 0 : std::min<uint64_t>(32 << 10, kFileStageSlot / n / 64 * 64))
             : uniform ? (256ull << 10) : (2ull << 20);
   const uint64_t longest = *std::max_element(lens.begin(), lens.end());
   slice = std::min(slice, std::max<uint64_t>(64, (longest + 63) / 64 * 64));  // no idle slot bytes
@@ -809,9 +850,12 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
     max_blocks = std::max(max_blocks, C.plan[a]->max_blocks);
   }
   CopyPool* pool = nullptr;
+  unsigned workers = 0;
   if (staged) {
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     pool = C.ensure_pool(std::min(15u, std::max(2u, hw / unsigned(sh.ndevices)) - 1));
+    // concurrent calls on this device split the copy threads (and the caller's thread helps)
+    workers = std::max(1u, (pool->size() + 1) / std::max(1u, C.share)) - 1;
   }
   const uint64_t bps = slice / 64;  // blocks per slice
   s3h_plan_s* P0 = C.plan[0];
@@ -839,7 +883,7 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
         const uint64_t len = lens[j];
         if (byte0 < len && !src.fill(sh.parts[j], byte0, std::min(slice, len - byte0), hslot + j * slice))
           bad.store(true, std::memory_order_relaxed);
-      });
+      }, workers);
       if (bad.load()) { rc = fail(S3H_EINVAL, "reading a part failed (file shorter than a part?)"); break; }
       e = hipMemcpyAsync(slot_base, hslot, slot_bytes, hipMemcpyHostToDevice, C.copy_s);
       if (e != hipSuccess) rc = fail(S3H_EHIP, "H2D staged: %s", hipGetErrorString(e));
@@ -1047,6 +1091,160 @@ int stream_final(s3h_stream_s* S, uint32_t* d_digests, hipStream_t s) {
 
 }  // namespace
 
+namespace {
+
+// ------------------------------------------------------------------ concurrent callers
+// upload.cpp:136-140 hashes from cfg.jobs std::async threads, each call covering only its own
+// job's parts.  Run as they come, 16 such calls of 32 parts put 16 small grids on the
+// process's few hardware queues (GPU_MAX_HW_QUEUES, 4 by default), which run them a few at a
+// time: 4 GiB in 16 x 32 parts of 8 MiB took 1.3-1.4 s against 0.124 s for one call with all
+// 512 parts.  So the calls of one device meet in a queue: the first caller (the leader) takes
+// every pending request with the same algorithms and slice size and runs them as ONE shard --
+// parts from memory and file ranges mixed -- then scatters the digests back; calls that arrive
+// meanwhile form the next batch.  Once calls have been seen to overlap (within the last
+// second), a leader first gathers the rest of the burst: it waits until as many calls are
+// pending as the largest recent burst, until none arrived for kGatherQuiet, or kGatherMax.
+struct HostReq {
+  const int* algos;
+  int nalgo;
+  const PartSource* src;
+  const uint64_t* lengths;
+  uint32_t* const* digests;
+  const HostShard* sh;
+  uint64_t slice;
+  int rc = S3H_OK;
+  std::string err;
+  bool done = false;
+};
+
+struct DevQueue {
+  std::mutex m;
+  std::condition_variable cv;
+  std::vector<HostReq*> pending;
+  bool leader = false;
+  double last_overlap = -1e9;  // when a call last found another one on this device
+  size_t burst = 0;            // largest batch of the recent bursts
+};
+
+constexpr double kGatherQuiet = 300e-6, kGatherMax = 3e-3;
+
+DevQueue& dev_queue(int device) {
+  static std::mutex m;
+  static std::vector<std::unique_ptr<DevQueue>>* qs = new std::vector<std::unique_ptr<DevQueue>>();
+  std::lock_guard<std::mutex> l(m);
+  if (qs->size() <= size_t(device)) qs->resize(device + 1);
+  if (!(*qs)[device]) (*qs)[device].reset(new DevQueue());
+  return *(*qs)[device];
+}
+
+bool same_work(const HostReq& a, const HostReq& b) {
+  if (a.nalgo != b.nalgo || a.slice != b.slice) return false;
+  for (int k = 0; k < a.nalgo; ++k)
+    if (a.algos[k] != b.algos[k]) return false;
+  return true;
+}
+
+// One context, one shard: a single request as it is, several merged into one part list.
+void run_batch(const std::vector<HostReq*>& batch) {
+  const HostReq& f = *batch[0];
+  HostCtx* C = host_ctx_cache().acquire(f.sh->device);
+  int rc;
+  if (batch.size() == 1) {
+    rc = run_host_shard(*C, *f.sh, f.algos, f.nalgo, *f.src, f.lengths, f.digests, f.slice);
+  } else {
+    uint64_t m = 0;
+    bool mem = true;
+    HostShard sh{f.sh->device, 1, {}};
+    for (const HostReq* r : batch) {
+      m += r->sh->parts.size();
+      mem = mem && r->src->parts;
+      sh.ndevices = std::max(sh.ndevices, r->sh->ndevices);
+    }
+    std::vector<uint64_t> lens(m);
+    std::vector<const uint8_t*> ptrs(mem ? m : 0);
+    std::vector<PartRef> refs(mem ? 0 : m);
+    sh.parts.resize(m);
+    uint64_t k = 0;
+    for (const HostReq* r : batch)
+      for (uint64_t g : r->sh->parts) {
+        lens[k] = r->lengths[g];
+        if (mem) ptrs[k] = r->src->parts[g];
+        else refs[k] = r->src->ref(g);
+        sh.parts[k] = k;
+        ++k;
+      }
+    PartSource src;
+    if (mem) src.parts = ptrs.data();
+    else src.refs = refs.data();
+    std::vector<uint32_t> out[kHostMaxAlgo];
+    uint32_t* outp[kHostMaxAlgo] = {};
+    for (int a = 0; a < f.nalgo; ++a) {
+      out[a].resize(m * digest_words(f.algos[a]));
+      outp[a] = out[a].data();
+    }
+    rc = run_host_shard(*C, sh, f.algos, f.nalgo, src, lens.data(), outp, f.slice);
+    k = 0;
+    for (const HostReq* r : batch) {
+      for (uint64_t g : r->sh->parts) {
+        for (int a = 0; a < f.nalgo && rc == S3H_OK; ++a) {
+          const uint32_t dw = digest_words(f.algos[a]);
+          std::memcpy(r->digests[a] + dw * g, outp[a] + dw * k, dw * 4);
+        }
+        ++k;
+      }
+    }
+  }
+  const std::string err = rc ? g_err : std::string();
+  host_ctx_cache().release(C, rc == S3H_OK);
+  for (HostReq* r : batch) {
+    r->rc = rc;
+    r->err = err;
+  }
+}
+
+// Runs `r` (in a batch with the device's other pending calls); returns when it is done.
+void submit(HostReq& r) {
+  DevQueue& q = dev_queue(r.sh->device);
+  std::unique_lock<std::mutex> l(q.m);
+  q.pending.push_back(&r);
+  if (q.leader || q.pending.size() > 1) q.last_overlap = wall_s();
+  q.cv.notify_all();  // a gathering leader counts arrivals
+  q.cv.wait(l, [&] { return r.done || !q.leader; });
+  if (r.done) return;
+  q.leader = true;
+  const double t0 = wall_s();
+  if (t0 - q.last_overlap >= 1.0) q.burst = 0;
+  for (double t_arr = t0; q.burst > 1 && q.pending.size() < q.burst;) {
+    const size_t had = q.pending.size();
+    q.cv.wait_for(l, std::chrono::duration<double>(kGatherQuiet / 3));
+    const double t = wall_s();
+    if (q.pending.size() != had) t_arr = t;
+    if (t - t_arr > kGatherQuiet || t - t0 > kGatherMax) break;
+  }
+  while (!r.done && !q.pending.empty()) {
+    q.burst = std::max(q.burst, q.pending.size());
+    std::vector<HostReq*> batch;
+    HostReq* first = q.pending.front();
+    for (auto it = q.pending.begin(); it != q.pending.end();) {
+      if (same_work(*first, **it)) {
+        batch.push_back(*it);
+        it = q.pending.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    l.unlock();
+    run_batch(batch);
+    l.lock();
+    for (HostReq* b : batch) b->done = true;
+    q.cv.notify_all();
+  }
+  q.leader = false;  // a waiting caller takes over what is still pending
+  q.cv.notify_all();
+}
+
+}  // namespace
+
 extern "C" {
 
 const char* s3h_last_error(void) { return g_err.c_str(); }
@@ -1164,6 +1362,7 @@ int s3h_md5_batch_device(int device, const void* d_base, const uint64_t* offsets
 
 // Shard s (of nshards) gets parts i with i % nshards == s and runs on device devs[s]; a device
 // may appear more than once (its shards run concurrently, each on its own context).
+
 static int batch_host_on(const int* algos, int nalgo, const PartSource& src,
                          const uint64_t* lengths, uint64_t n, uint32_t* const* digests,
                          const std::vector<int>& devs, uint64_t slice_bytes) {
@@ -1186,10 +1385,10 @@ static int batch_host_on(const int* algos, int nalgo, const PartSource& src,
   std::vector<int> rcs(nshards, S3H_OK);
   std::vector<std::string> errs(nshards);
   auto run = [&](int k) {
-    HostCtx* C = host_ctx_cache().acquire(shards[k].device);
-    rcs[k] = run_host_shard(*C, shards[k], algos, nalgo, src, lengths, digests, slice_bytes);
-    if (rcs[k]) errs[k] = g_err;
-    host_ctx_cache().release(C, rcs[k] == S3H_OK);
+    HostReq r{algos, nalgo, &src, lengths, digests, &shards[k], slice_bytes};
+    submit(r);
+    rcs[k] = r.rc;
+    errs[k] = r.err;
   };
   if (nshards == 1) {
     run(0);

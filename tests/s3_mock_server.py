@@ -1,0 +1,134 @@
+#!/usr/bin/env python3
+"""Loopback S3 UploadPart endpoint for BASELINE config 5 (test infrastructure, not product).
+
+MinIO and the libcurl headers are absent from this image, so config 5 (apps/parallel_upload.cpp
+end-to-end against MinIO on loopback) runs against this stand-in instead.  It accepts what
+`apps/s3_upload_hash --send` PUTs -- S3Api::UploadPart / UploadFilePart requests
+(`PUT /{bucket}/{key}?partNumber=N&uploadId=ID`, lib/src/api/multipart_upload.cpp:71-156) --
+and checks each one the way an S3 server would:
+
+* the body's SHA-256 (Python hashlib, independent of this repo's code) equals the
+  `x-amz-content-sha256` header (400 XAmzContentSHA256Mismatch otherwise), and
+* the SigV4 `Authorization` header verifies: the canonical request is rebuilt from the
+  received method, path, query and the headers named in SignedHeaders, as
+  lib/src/aws_sign.cpp:226-308 builds it (403 SignatureDoesNotMatch otherwise).
+
+A verified part gets 200 with `ETag: "<md5 of body>"` (what S3 returns for UploadPart).
+`GET /stats` returns JSON counts.  Run: `s3_mock_server.py --port 0 --port-file F` (prints
+the bound port).  Nothing is stored."""
+import argparse
+import hashlib
+import hmac
+import json
+import threading
+import urllib.parse
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+_UNRESERVED = "-_.~"
+
+
+def _enc(s: str) -> str:  # url_utility.cpp:70-90: alnum and -_.~ kept, the rest %XX (upper)
+    return "".join(c if (c.isascii() and c.isalnum()) or c in _UNRESERVED
+                   else "".join(f"%{b:02X}" for b in c.encode()) for c in s)
+
+
+def _hm(key: bytes, msg: str) -> bytes:
+    return hmac.new(key, msg.encode(), hashlib.sha256).digest()
+
+
+def expected_signature(secret, method, path, query, headers, signed, payload, date, scope):
+    """SigV4 as aws_sign.cpp:226-308 computes it (sorted query, 'name:value' header lines)."""
+    params = urllib.parse.parse_qsl(query, keep_blank_values=True)
+    cq = "&".join(f"{_enc(k)}={_enc(v)}" for k, v in sorted(params))
+    block = "".join(f"{h}:{headers.get(h, '')}\n" for h in signed)
+    creq = f"{method.upper()}\n{path}\n{cq}\n{block}\n{';'.join(signed)}\n{payload}"
+    to_sign = ("AWS4-HMAC-SHA256\n" + date + "\n" + scope + "\n"
+               + hashlib.sha256(creq.encode()).hexdigest())
+    day, region, service, _ = scope.split("/")
+    key = _hm(_hm(_hm(_hm(("AWS4" + secret).encode(), day), region), service), "aws4_request")
+    return hmac.new(key, to_sign.encode(), hashlib.sha256).hexdigest()
+
+
+class Server(ThreadingHTTPServer):
+    request_queue_size = 256  # an uploader opens one connection per job at once
+    daemon_threads = True
+
+
+class Handler(BaseHTTPRequestHandler):
+    protocol_version = "HTTP/1.1"
+    secret = "SECRET"
+    stats = {"parts": 0, "bytes": 0, "bad_hash": 0, "bad_signature": 0, "short_body": 0}
+    lock = threading.Lock()
+
+    def log_message(self, *a):  # quiet
+        pass
+
+    def _reply(self, code, body=b"", etag=None):
+        self.send_response(code)
+        if etag:
+            self.send_header("ETag", f'"{etag}"')
+        self.send_header("Content-Length", str(len(body)))
+        self.end_headers()
+        self.wfile.write(body)
+
+    def do_GET(self):
+        if self.path == "/stats":
+            with self.lock:
+                body = json.dumps(self.stats).encode()
+            return self._reply(200, body)
+        return self._reply(404)
+
+    def do_PUT(self):
+        n = int(self.headers.get("content-length", "0"))
+        body = self.rfile.read(n)
+        if len(body) != n:  # the client went away mid-body
+            with self.lock:
+                self.stats["short_body"] += 1
+            self.close_connection = True
+            return
+        claimed = self.headers.get("x-amz-content-sha256", "")
+        digest = hashlib.sha256(body).hexdigest()
+        if claimed != digest:
+            with self.lock:
+                self.stats["bad_hash"] += 1
+            return self._reply(400, b"XAmzContentSHA256Mismatch")
+        auth = self.headers.get("Authorization", "")
+        try:
+            fields = dict(kv.strip().split("=", 1) for kv in auth.split(" ", 1)[1].split(","))
+            scope = fields["Credential"].split("/", 1)[1]
+            signed = fields["SignedHeaders"].split(";")
+            hdrs = {k.lower(): v for k, v in self.headers.items()}
+            path, _, query = self.path.partition("?")
+            want = expected_signature(self.secret, self.command, path, query, hdrs, signed,
+                                      claimed, hdrs.get("x-amz-date", ""), scope)
+            ok = hmac.compare_digest(want, fields["Signature"])
+        except (KeyError, IndexError, ValueError):
+            ok = False
+        if not ok:
+            with self.lock:
+                self.stats["bad_signature"] += 1
+            return self._reply(403, b"SignatureDoesNotMatch")
+        with self.lock:
+            self.stats["parts"] += 1
+            self.stats["bytes"] += n
+        self._reply(200, etag=hashlib.md5(body).hexdigest())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--port", type=int, default=0)
+    ap.add_argument("--port-file", default="")
+    ap.add_argument("--secret", default="SECRET")
+    a = ap.parse_args()
+    Handler.secret = a.secret
+    srv = Server(("127.0.0.1", a.port), Handler)
+    port = srv.server_address[1]
+    if a.port_file:
+        with open(a.port_file, "w") as f:
+            f.write(str(port))
+    print(port, flush=True)
+    srv.serve_forever()
+
+
+if __name__ == "__main__":
+    main()

@@ -106,3 +106,70 @@ def test_upload_counterpart_memory_multipart(programs, tmp_path, golden, jobs, p
     want = [p for p in mp["parts"] if p["chunks"] == jobs * ppj]
     assert [(int(x[2]), int(x[3]), x[4]) for x in rows] == [(p["offset"], p["size"], p["digest"]) for p in want]
     assert "UNSIGNED-PAYLOAD" not in r.stdout
+
+
+@pytest.fixture
+def s3_mock():
+    """tests/s3_mock_server.py on a free loopback port: checks every PUT body's SHA-256 against
+    x-amz-content-sha256 and verifies its SigV4 signature (config 5's endpoint; MinIO absent)."""
+    import json
+    import sys
+    import time
+    import urllib.request
+    proc = subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "s3_mock_server.py"),
+                             "--port", "0"], stdout=subprocess.PIPE, text=True)
+    try:
+        port = int(proc.stdout.readline())
+        url = f"http://127.0.0.1:{port}"
+
+        def stats():
+            for _ in range(50):
+                try:
+                    with urllib.request.urlopen(url + "/stats", timeout=5) as r:
+                        return json.loads(r.read())
+                except OSError:
+                    time.sleep(0.1)
+            raise RuntimeError("mock S3 server not answering")
+        yield url, stats
+    finally:
+        proc.kill()
+        proc.wait()
+
+
+def _upload(app_args, url, tmp_path, golden):
+    path, t = _xfer_file(tmp_path, golden)
+    app = os.path.join(ROOT, "apps", "build", "s3-upload-hash")
+    r = subprocess.run([app, "-f", path, "-j", "3", "-n", "2", "--send", "--endpoint", url,
+                        *app_args], capture_output=True, text=True, timeout=300)
+    return r, t
+
+
+def test_upload_send_loopback_cpu(programs, tmp_path, golden, s3_mock):
+    """Config 5's path without MinIO: the CPU drop-in hashes the transfer test's 3 jobs x 2 parts
+    and each job PUTs its parts with the digest signed into x-amz-content-sha256; the loopback
+    server accepts all six (body SHA-256 and signature verified), and rejects every part signed
+    with another secret."""
+    url, stats = s3_mock
+    for source in ("file", "memory"):
+        r, t = _upload(["--cpu", "--source", source], url, tmp_path, golden)
+        assert r.returncode == 0, r.stderr
+        assert [x[4] for x in _parse_parts(r.stdout)] == [p["digest"] for p in t["parts"]]
+    s = stats()
+    assert s["parts"] == 12 and s["bytes"] == 2 * t["size"], s
+    assert s["bad_hash"] == 0 and s["bad_signature"] == 0, s
+    r, _ = _upload(["--cpu", "--secret", "WRONG"], url, tmp_path, golden)
+    assert r.returncode != 0 and "6 of 6 PUTs not 200" in r.stderr, r.stderr
+    assert stats()["bad_signature"] == 6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("source,per_job", [("file", False), ("mmap", True), ("memory", True)])
+def test_upload_send_loopback_gpu(programs, tmp_path, golden, s3_mock, source, per_job):
+    """The same upload with the GPU batch path (H2D included): one call, or one concurrent call
+    per job thread before it PUTs its parts; every part accepted by the verifying server."""
+    url, stats = s3_mock
+    r, t = _upload(["--source", source] + (["--per-job"] if per_job else []), url, tmp_path, golden)
+    assert r.returncode == 0, r.stderr
+    assert [x[4] for x in _parse_parts(r.stdout)] == [p["digest"] for p in t["parts"]]
+    s = stats()
+    assert s["parts"] == 6 and s["bad_hash"] == 0 and s["bad_signature"] == 0, s

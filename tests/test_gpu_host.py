@@ -107,6 +107,79 @@ def test_concurrent_host_callers(torch_cuda, oracle, golden):
         assert np.array_equal(results[k], want_r[k - 1]), k
 
 
+def test_sixteen_concurrent_callers_reuse_contexts(torch_cuda, oracle):
+    """16 job threads (the upload.cpp:136-140 shape at -j 16), three rounds each on their own
+    ragged parts: every call takes an idle context of the device or builds one, and returns it;
+    digests vs the oracle every round; s3h_trim then frees all 16 contexts."""
+    torch = torch_cuda
+    s3.trim()
+    free0 = _free(torch)
+    rng = np.random.default_rng(57)
+    sets = [[rng.integers(0, 256, int(L), dtype=np.uint8) for L in rng.integers(0, 120000, 40)]
+            for _ in range(16)]
+    want = [np.stack([oracle.sha256(p.tobytes()) for p in ps]) for ps in sets]
+    errors, bad = [], []
+
+    def job(k):
+        try:
+            for r in range(3):
+                if not np.array_equal(s3.sha256_batch_host(sets[k]), want[k]):
+                    bad.append((k, r))
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=job, args=(k,)) for k in range(16)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors and not bad, (errors, bad)
+    s3.trim()
+    assert free0 - _free(torch) < 64 * MIB
+
+
+def test_concurrent_mixed_sources_and_algorithms(torch_cuda, oracle, tmp_path):
+    """Concurrent calls of different kinds on one device: file ranges and memory parts
+    (SHA-256, merged into one batch of per-part references) beside SHA-256 + MD5 calls (a
+    different algorithm set: their own batches).  Every digest vs the oracle / hashlib."""
+    import hashlib
+    rng = np.random.default_rng(58)
+    data = np.frombuffer(rng.bytes(8 * MIB), dtype=np.uint8)
+    path = tmp_path / "mixed.bin"
+    data.tofile(path)
+    fo = rng.integers(0, 7 * MIB, 50)
+    fl = rng.integers(0, MIB, 50)
+    mem = [[rng.integers(0, 256, int(L), dtype=np.uint8) for L in rng.integers(0, 200000, 30)]
+           for _ in range(3)]
+    want_f = oracle.batch(data, fo, fl)
+    want_m = [np.stack([oracle.sha256(p.tobytes()) for p in ps]) for ps in mem]
+    want_md5 = [[hashlib.md5(p.tobytes()).hexdigest() for p in ps] for ps in mem]
+    errors, bad = [], []
+
+    def job(k):
+        try:
+            for r in range(2):
+                if k == 0:
+                    ok = np.array_equal(s3.sha256_file_parts(str(path), fo, fl), want_f)
+                elif k <= 3:
+                    ok = np.array_equal(s3.sha256_batch_host(mem[k - 1]), want_m[k - 1])
+                else:
+                    sha, md5 = s3.sha256_md5_batch_host(mem[k - 4])
+                    ok = (np.array_equal(sha, want_m[k - 4])
+                          and s3.digests_to_text(md5, 4) == want_md5[k - 4])
+                if not ok:
+                    bad.append((k, r))
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=job, args=(k,)) for k in range(7)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors and not bad, (errors, bad)
+
+
 def test_file_parts_transfer_geometry(torch_cuda, golden, tmp_path):
     """s3h_sha256_file_parts: the transfer test's file, parts as (offset, size) ranges sliced by
     lib/src/upload.cpp geometry (3 jobs x 2 parts), preads straight into pinned staging."""
@@ -172,9 +245,9 @@ def test_two_plans_on_two_streams(torch_cuda, oracle):
 
 
 def test_sharded_host_batch_on_repeated_device(torch_cuda, oracle):
-    """The multi-device host path (one host thread and one context per shard, part i on shard
-    i % N, digests reassembled in part order) exercised on one GPU by listing it 3 times:
-    shards 1 and 2 run on private contexts concurrently with shard 0."""
+    """The multi-device host path (one host thread per shard, part i on shard i % N, digests
+    reassembled in part order) exercised on one GPU by listing it 3 times: the three shards
+    meet in the device's queue and run as one merged batch."""
     rng = np.random.default_rng(55)
     parts = [rng.integers(0, 256, int(L), dtype=np.uint8) for L in rng.integers(0, 300000, 301)]
     want = np.stack([oracle.sha256(p.tobytes()) for p in parts])
