@@ -59,12 +59,12 @@ enum s3h_algo {
 const char *s3h_last_error(void);
 int s3h_api_version(void);
 /* Free the host path's cached per-device contexts.  Between s3h_*_batch_host /
- * s3h_sha256_file_parts / s3h_verify_batch_host calls each device keeps up to 16 idle
- * contexts (one per concurrent caller seen): streams, plans, digest buffers, copy threads, an
- * HBM ring and pinned staging.  The first keeps at most 1 GiB of ring (larger rings are freed
- * when the call returns) and its staging (96 MiB, up to 384 MiB after a file-range call with
- * thousands of parts); the others at most 256 MiB of ring and 96 MiB of staging.  s3h_trim
- * releases every idle context. */
+ * s3h_sha256_file_parts / s3h_verify_batch_host calls each device keeps one context:
+ * streams, plans, digest buffers, copy threads, at most 1 GiB of HBM ring (larger rings are
+ * freed when the call returns) and its pinned staging (96 MiB, up to 384 MiB after a
+ * file-range call with thousands of parts).  Concurrent host calls on one device are merged
+ * into one batch (their digests are the same as from separate calls).  s3h_trim releases the
+ * contexts of idle devices. */
 int s3h_trim(void);
 /* Number of visible HIP devices; S3H_ENODEV (and *count = 0) when there is none. */
 int s3h_device_count(int *count);

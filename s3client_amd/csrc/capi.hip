@@ -447,7 +447,7 @@ int dual_launch(s3h_plan_s* S, s3h_plan_s* M, const void* d_base, uint32_t* d_sh
 class CopyPool {
  public:
   explicit CopyPool(unsigned workers) {
-    for (unsigned i = 0; i < workers; ++i) threads_.emplace_back([this, i] { loop(i); });
+    for (unsigned i = 0; i < workers; ++i) threads_.emplace_back([this] { loop(); });
   }
   ~CopyPool() {
     {
@@ -458,15 +458,13 @@ class CopyPool {
     for (auto& t : threads_) t.join();
   }
   unsigned size() const { return unsigned(threads_.size()); }
-  // fn(i) for every i in [0, n), on the first `active` workers and the calling thread; returns
-  // when done.
-  void run(uint64_t n, const std::function<void(uint64_t)>& fn, unsigned active) {
+  // fn(i) for every i in [0, n), on the workers and the calling thread; returns when done.
+  void run(uint64_t n, const std::function<void(uint64_t)>& fn) {
     {
       std::lock_guard<std::mutex> l(m_);
       fn_ = &fn;
       n_ = n;
       next_ = 0;
-      active_ = active;
       busy_ = threads_.size();
       ++gen_;
     }
@@ -481,18 +479,16 @@ class CopyPool {
   void work() {
     for (uint64_t i; (i = next_.fetch_add(1)) < n_;) (*fn_)(i);
   }
-  void loop(unsigned index) {
+  void loop() {
     uint64_t seen = 0;
     for (;;) {
-      bool mine;
       {
         std::unique_lock<std::mutex> l(m_);
         cv_.wait(l, [&] { return stop_ || gen_ != seen; });
         if (stop_) return;
         seen = gen_;
-        mine = index < active_;
       }
-      if (mine) work();
+      work();
       std::lock_guard<std::mutex> l(m_);
       if (--busy_ == 0) done_.notify_one();
     }
@@ -503,7 +499,6 @@ class CopyPool {
   const std::function<void(uint64_t)>* fn_ = nullptr;
   std::atomic<uint64_t> next_{0};
   uint64_t n_ = 0, gen_ = 0;
-  unsigned active_ = 0;
   size_t busy_ = 0;
   bool stop_ = false;
 };
@@ -515,15 +510,11 @@ class CopyPool {
 // after file; creating and freeing these per call cost ~8 ms of a 27 ms call on a 512 MiB
 // file, profiles/r01_app_upload_hash.txt).  Buffers only grow; an HBM ring above
 // kKeepRingBytes is freed when the call returns, so a cached context holds at most
-// kKeepRingBytes of HBM plus its staging; s3h_trim() frees idle contexts.  Concurrent calls on
-// one device each take a context of their own from the device's idle list (HostCtxCache).
+// kKeepRingBytes of HBM plus its staging; s3h_trim() frees idle contexts.
 constexpr int kHostRing = 3;
 constexpr int kHostMaxAlgo = 2;
 constexpr uint64_t kStageSlot = 32ull << 20;     // pinned staging bytes per ring slot
 constexpr uint64_t kKeepRingBytes = 1ull << 30;  // largest HBM ring kept between calls
-// Further idle contexts of a device (concurrent callers) keep at most these; up to kIdleCtx.
-constexpr uint64_t kKeepRingBytes2 = 256ull << 20, kKeepStageBytes2 = 96ull << 20;
-constexpr size_t kIdleCtx = 16;
 // File ranges stage with one pread per part per slice, whose syscall costs more than it moves
 // below ~32 KiB: their slices are at least 32 KiB up to 4,096 parts per device (slots of up
 // to 128 MiB), 128 MiB / n beyond.
@@ -567,7 +558,6 @@ struct PartSource {
 
 struct HostCtx {
   int device = 0;
-  unsigned share = 1;  // calls on this device when this one started (copy threads are split)
   hipStream_t copy_s = nullptr, hash_s[kHostMaxAlgo] = {};
   hipEvent_t copied[kHostRing] = {}, hashed[kHostRing][kHostMaxAlgo] = {};
   std::unique_ptr<CopyPool> pool;
@@ -642,18 +632,11 @@ struct HostCtx {
     for (hipStream_t st : hash_s)
       if (st) (void)hipStreamSynchronize(st);
   }
-  // After a call: do not keep a large HBM ring; a context kept beside another idle one keeps
-  // at most a small ring and staging.
-  void release_large(bool secondary) {
-    if (ring_bytes > (secondary ? kKeepRingBytes2 : kKeepRingBytes)) {
+  void release_large() {  // after a call: do not keep a large HBM ring
+    if (ring_bytes > kKeepRingBytes) {
       (void)hipFree(ring);
       ring = nullptr;
       ring_bytes = 0;
-    }
-    if (secondary && stage_bytes > kKeepStageBytes2) {
-      (void)hipHostFree(stage);
-      stage = nullptr;
-      stage_bytes = 0;
     }
   }
   ~HostCtx() {
@@ -678,53 +661,43 @@ struct HostCtx {
   }
 };
 
-// Per device: the idle contexts (most recently used first out) and the number of calls
-// running.  Concurrent callers -- upload.cpp:136-140's std::async jobs, each hashing its own
-// parts -- each take an idle context or build one, and return it when done, so the next round
-// of concurrent calls reuses streams, plans, rings and copy threads instead of allocating them
-// (up to kIdleCtx per device).
+// One cached context per device.  Host calls on a device run one batch at a time (the
+// device queue below merges concurrent callers), so the context is normally free; a call that
+// still finds it busy gets a private one.
 struct HostCtxCache {
-  struct Dev {
-    std::vector<HostCtx*> idle;
-    unsigned running = 0;
-  };
   std::mutex m;
-  std::vector<Dev> v;  // indexed by device
+  std::vector<HostCtx*> v;  // indexed by device
+  std::vector<bool> busy;
   HostCtx* acquire(int device) {
     std::lock_guard<std::mutex> l(m);
-    if (v.size() <= size_t(device)) v.resize(device + 1);
-    Dev& d = v[device];
-    HostCtx* c = nullptr;
-    if (!d.idle.empty()) {
-      c = d.idle.back();
-      d.idle.pop_back();
-    } else {
-      c = new HostCtx();
-      c->device = device;
+    if (v.size() <= size_t(device)) {
+      v.resize(device + 1, nullptr);
+      busy.resize(device + 1, false);
     }
-    c->share = ++d.running;
-    return c;
+    if (busy[device]) {
+      auto* p = new HostCtx();
+      p->device = device;
+      return p;
+    }
+    if (!v[device]) {
+      v[device] = new HostCtx();
+      v[device]->device = device;
+    }
+    busy[device] = true;
+    return v[device];
   }
-  // ok: the call succeeded (keep the context); a failed call drops its context.
+  // ok: the call succeeded (keep the cached context); a failed call drops its context.
   void release(HostCtx* c, bool ok) {
-    bool keep, secondary;
+    {
+      DeviceGuard g(c->device);
+      c->release_large();
+    }
     {
       std::lock_guard<std::mutex> l(m);
-      Dev& d = v[c->device];
-      --d.running;
-      keep = ok && d.idle.size() < kIdleCtx;
-      secondary = !d.idle.empty();
-    }
-    if (keep) {
-      {
-        DeviceGuard g(c->device);
-        c->release_large(secondary);
-      }
-      std::lock_guard<std::mutex> l(m);
-      Dev& d = v[c->device];
-      if (d.idle.size() < kIdleCtx) {
-        d.idle.push_back(c);
-        return;
+      if (v[c->device] == c) {
+        busy[c->device] = false;
+        if (ok) return;
+        v[c->device] = nullptr;
       }
     }
     delete c;
@@ -733,10 +706,11 @@ struct HostCtxCache {
     std::vector<HostCtx*> idle;
     {
       std::lock_guard<std::mutex> l(m);
-      for (Dev& d : v) {
-        idle.insert(idle.end(), d.idle.begin(), d.idle.end());
-        d.idle.clear();
-      }
+      for (size_t d = 0; d < v.size(); ++d)
+        if (v[d] && !busy[d]) {
+          idle.push_back(v[d]);
+          v[d] = nullptr;
+        }
     }
     for (HostCtx* c : idle) delete c;
   }
@@ -850,12 +824,9 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
     max_blocks = std::max(max_blocks, C.plan[a]->max_blocks);
   }
   CopyPool* pool = nullptr;
-  unsigned workers = 0;
   if (staged) {
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     pool = C.ensure_pool(std::min(15u, std::max(2u, hw / unsigned(sh.ndevices)) - 1));
-    // concurrent calls on this device split the copy threads (and the caller's thread helps)
-    workers = std::max(1u, (pool->size() + 1) / std::max(1u, C.share)) - 1;
   }
   const uint64_t bps = slice / 64;  // blocks per slice
   s3h_plan_s* P0 = C.plan[0];
@@ -883,7 +854,7 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
         const uint64_t len = lens[j];
         if (byte0 < len && !src.fill(sh.parts[j], byte0, std::min(slice, len - byte0), hslot + j * slice))
           bad.store(true, std::memory_order_relaxed);
-      }, workers);
+      });
       if (bad.load()) { rc = fail(S3H_EINVAL, "reading a part failed (file shorter than a part?)"); break; }
       e = hipMemcpyAsync(slot_base, hslot, slot_bytes, hipMemcpyHostToDevice, C.copy_s);
       if (e != hipSuccess) rc = fail(S3H_EHIP, "H2D staged: %s", hipGetErrorString(e));
@@ -1102,8 +1073,8 @@ namespace {
 // every pending request with the same algorithms and slice size and runs them as ONE shard --
 // parts from memory and file ranges mixed -- then scatters the digests back; calls that arrive
 // meanwhile form the next batch.  Once calls have been seen to overlap (within the last
-// second), a leader first gathers the rest of the burst: it waits until as many calls are
-// pending as the largest recent burst, until none arrived for kGatherQuiet, or kGatherMax.
+// second), a leader first gathers the rest of the burst: it waits until no call has arrived
+// for kGatherQuiet (at most kGatherMax).
 struct HostReq {
   const int* algos;
   int nalgo;
@@ -1123,7 +1094,6 @@ struct DevQueue {
   std::vector<HostReq*> pending;
   bool leader = false;
   double last_overlap = -1e9;  // when a call last found another one on this device
-  size_t burst = 0;            // largest batch of the recent bursts
 };
 
 constexpr double kGatherQuiet = 300e-6, kGatherMax = 3e-3;
@@ -1213,8 +1183,7 @@ void submit(HostReq& r) {
   if (r.done) return;
   q.leader = true;
   const double t0 = wall_s();
-  if (t0 - q.last_overlap >= 1.0) q.burst = 0;
-  for (double t_arr = t0; q.burst > 1 && q.pending.size() < q.burst;) {
+  for (double t_arr = t0; t0 - q.last_overlap < 1.0;) {
     const size_t had = q.pending.size();
     q.cv.wait_for(l, std::chrono::duration<double>(kGatherQuiet / 3));
     const double t = wall_s();
@@ -1222,7 +1191,6 @@ void submit(HostReq& r) {
     if (t - t_arr > kGatherQuiet || t - t0 > kGatherMax) break;
   }
   while (!r.done && !q.pending.empty()) {
-    q.burst = std::max(q.burst, q.pending.size());
     std::vector<HostReq*> batch;
     HostReq* first = q.pending.front();
     for (auto it = q.pending.begin(); it != q.pending.end();) {

@@ -170,8 +170,8 @@ int main(int argc, char** argv) {
     // Concurrent callers in the shape of lib/src/upload.cpp:89-110 + 136-140: the transfer
     // test's object (test/parallel-file-transfer-test.cpp:50-59, bytes i % 128) sliced into
     // 3 jobs x 2 parts; each job is a std::async thread that hashes ITS parts with its own
-    // batch call while the others do (the device's cached host context goes to one of them,
-    // the rest build private ones), plus a fourth job hashing the same parts from a file.
+    // batch call while the others do (the calls meet in the device's queue and run as merged
+    // batches), plus a fourth job hashing the same parts from a file.
     {
       const uint64_t size = 38000007;
       std::vector<uint8_t> obj(size);

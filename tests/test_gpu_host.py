@@ -73,9 +73,9 @@ def test_pageable_parts_beyond_staging_slot_cap(torch_cuda, oracle):
 
 
 def test_concurrent_host_callers(torch_cuda, oracle, golden):
-    """Four threads hash at the same time (ctypes drops the GIL): one uses the device's cached
-    context, the others build private ones -- as upload.cpp:136-140 runs one std::async job per
-    part group.  Each thread's digests vs the transfer-test goldens / the oracle."""
+    """Four threads hash at the same time (ctypes drops the GIL), as upload.cpp:136-140 runs one
+    std::async job per part group: their calls are merged into shared batches.  Each thread's
+    digests vs the transfer-test goldens / the oracle."""
     t = golden["transfer"]
     data = (np.arange(t["size"], dtype=np.uint64) % 128).astype(np.uint8)
     views = [data[p["offset"]:p["offset"] + p["size"]] for p in t["parts"]]
@@ -107,10 +107,11 @@ def test_concurrent_host_callers(torch_cuda, oracle, golden):
         assert np.array_equal(results[k], want_r[k - 1]), k
 
 
-def test_sixteen_concurrent_callers_reuse_contexts(torch_cuda, oracle):
+def test_sixteen_concurrent_callers_merged(torch_cuda, oracle):
     """16 job threads (the upload.cpp:136-140 shape at -j 16), three rounds each on their own
-    ragged parts: every call takes an idle context of the device or builds one, and returns it;
-    digests vs the oracle every round; s3h_trim then frees all 16 contexts."""
+    ragged parts: the calls meet in the device's queue and run as merged batches, each caller
+    getting exactly its own digests back (vs the oracle every round); s3h_trim then frees the
+    device's context."""
     torch = torch_cuda
     s3.trim()
     free0 = _free(torch)
