@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <cerrno>
@@ -1430,6 +1431,20 @@ int s3h_sha256_file_parts(const char* path, const uint64_t* offsets, const uint6
     return fail(S3H_EINVAL, "file_parts: bad arguments");
   const int fd = open(path, O_RDONLY | O_CLOEXEC);
   if (fd < 0) return fail(S3H_EINVAL, "file_parts: cannot open %s: %s", path, std::strerror(errno));
+  // Every range must lie inside the file -- checked before the call can be merged with other
+  // callers' (a batch fails as a whole).
+  struct stat st {};
+  if (fstat(fd, &st) != 0) {
+    close(fd);
+    return fail(S3H_EINVAL, "file_parts: cannot stat %s", path);
+  }
+  for (uint64_t i = 0; i < n; ++i)
+    if (offsets[i] > uint64_t(st.st_size) || lengths[i] > uint64_t(st.st_size) - offsets[i]) {
+      close(fd);
+      return fail(S3H_EINVAL, "file_parts: part %llu [%llu, +%llu) is past the end of %s (%llu B)",
+                  (unsigned long long)i, (unsigned long long)offsets[i],
+                  (unsigned long long)lengths[i], path, (unsigned long long)st.st_size);
+    }
   PartSource src;
   src.fd = fd;
   src.file_off = offsets;

@@ -181,6 +181,36 @@ def test_concurrent_mixed_sources_and_algorithms(torch_cuda, oracle, tmp_path):
     assert not errors and not bad, (errors, bad)
 
 
+def test_concurrent_bad_call_fails_alone(torch_cuda, oracle, tmp_path):
+    """A file-range call with a part past the end of the file fails by itself (checked before
+    it can join a merged batch) while concurrent good calls on the device succeed."""
+    rng = np.random.default_rng(59)
+    data = np.frombuffer(rng.bytes(2 * MIB), dtype=np.uint8)
+    path = tmp_path / "bad.bin"
+    data.tofile(path)
+    parts = [rng.integers(0, 256, int(L), dtype=np.uint8) for L in rng.integers(0, 300000, 40)]
+    want = np.stack([oracle.sha256(p.tobytes()) for p in parts])
+    res = {}
+
+    def good(k):
+        res[k] = all(np.array_equal(s3.sha256_batch_host(parts), want) for _ in range(3))
+
+    def bad():
+        try:
+            s3.sha256_file_parts(str(path), [0, 2 * MIB - 5], [100, 10])
+            res["bad"] = "no error"
+        except s3.S3HashError as e:
+            res["bad"] = str(e)
+
+    th = [threading.Thread(target=good, args=(k,)) for k in range(4)] + [threading.Thread(target=bad)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert all(res[k] for k in range(4)), res
+    assert "past the end" in res["bad"], res
+
+
 def test_file_parts_transfer_geometry(torch_cuda, golden, tmp_path):
     """s3h_sha256_file_parts: the transfer test's file, parts as (offset, size) ranges sliced by
     lib/src/upload.cpp geometry (3 jobs x 2 parts), preads straight into pinned staging."""
