@@ -74,6 +74,8 @@ def parse():
                     help="skip the H2D-inclusive sub-measurement of the default C2 line")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the BASELINE config-4 sub-measurement of multi-GPU runs")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="skip the config-5 loopback upload sub-measurement of the default line")
     return ap.parse_args()
 
 
@@ -374,6 +376,8 @@ def main():
         if (world == 1 and args.config == "c2" and args.algo == "sha256" and not args.parts_per_gpu
                 and not args.part_bytes and not args.no_host_resident):
             line["host_resident"] = host_resident(s3, torch, data, ids, lens, offs, gd)
+            if not args.no_c5:
+                line["c5_loopback"] = c5_loopback(data, offs, lens, gd)
         if world == 1 and not args.no_cpu_baseline:
             n = min(args.cpu_sample_parts, len(lens))
             end = int(offs[n - 1] + lens[n - 1])
@@ -419,6 +423,67 @@ def host_resident(s3, torch, data, ids, lens, offs, gd, reps: int = 3):
            "digests_match_device_run": bool(np.array_equal(out, gd))}
     del host, h, views
     return res
+
+
+def c5_loopback(data, offs, lens, gd, nparts: int = 128, jobs: int = 16, repeat: int = 2):
+    """BASELINE config 5 without MinIO (absent here): C2 parts 0..nparts-1 written to a file,
+    which apps/s3_upload_hash slices as `jobs` x nparts/jobs parts (upload.cpp geometry: the
+    same 8 MiB parts), hashes and PUTs with each digest signed into x-amz-content-sha256 to
+    tests/s3_mock_server.py, which re-hashes every body (hashlib) and verifies every SigV4
+    signature.  Wall-clock of the whole pass (hash + upload; --repeat: the last pass) for the
+    GPU batch (one call, and one call per job: merged on the device), the CPU SHA-NI drop-in
+    and its scalar loop (lib/hash-like cost), plus the GPU hash alone."""
+    import re
+    import subprocess
+    import tempfile
+    import urllib.request
+    app = os.path.join(ROOT, "apps", "build", "s3-upload-hash")
+    end = int(offs[nparts - 1] + lens[nparts - 1])
+    if not os.path.exists(app) or int(offs[nparts - 1]) != (nparts - 1) * int(lens[0]):
+        return {"error": "app not built or parts not contiguous"}
+    res = {"workload": f"{nparts} x 8 MiB (C2 parts 0-{nparts - 1}) in one file, {jobs} jobs x "
+                       f"{nparts // jobs} parts; hash + signed UploadPart PUT per part to a "
+                       "loopback mock S3 endpoint that re-hashes bodies and verifies SigV4",
+           "repeat": repeat, "seconds": {}}
+    srv = None
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        path = os.path.join(td, "object.bin")
+        data[:end].cpu().numpy().tofile(path)
+        try:
+            srv = subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "s3_mock_server.py"),
+                                    "--port", "0"], stdout=subprocess.PIPE,
+                                   stderr=subprocess.DEVNULL, text=True)
+            url = f"http://127.0.0.1:{int(srv.stdout.readline())}"
+            want = [s3_hex(gd[k]) for k in range(nparts)]
+            for name, extra, env in (("gpu", ["--send"], {}),
+                                     ("gpu_per_job", ["--send", "--per-job"], {}),
+                                     ("cpu_shani", ["--send", "--cpu"], {}),
+                                     ("cpu_scalar", ["--send", "--cpu"], {"S3H_CPU_SCALAR": "1"}),
+                                     ("gpu_hash_only", [], {})):
+                r = subprocess.run([app, "-f", path, "-j", str(jobs), "-n", str(nparts // jobs),
+                                    "--endpoint", url, "--repeat", str(repeat), *extra],
+                                   capture_output=True, text=True, timeout=300,
+                                   env={**os.environ, **env})
+                m = re.search(r"in ([\d.]+) s = ", r.stderr)
+                got = [l.split(",")[4] for l in r.stdout.strip().splitlines()[1:]]
+                if r.returncode != 0 or not m or got != want:
+                    res["error"] = f"{name}: rc {r.returncode}, digests match {got == want}"
+                    break
+                res["seconds"][name] = float(m.group(1))
+            with urllib.request.urlopen(url + "/stats", timeout=10) as f:
+                res["server"] = json.loads(f.read())
+        except (OSError, ValueError, subprocess.SubprocessError) as e:
+            res["error"] = repr(e)
+        finally:
+            if srv is not None:
+                srv.kill()
+                srv.wait()
+    res["digests_match_device_run"] = "error" not in res
+    return res
+
+
+def s3_hex(words) -> str:
+    return np.ascontiguousarray(words, dtype=np.uint32).tobytes().hex()
 
 
 def c4_shard(args, s3, torch, dist, dev, rank, world, local, backend, steps: int = 3):
