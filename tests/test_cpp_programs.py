@@ -162,6 +162,17 @@ def test_upload_send_loopback_cpu(programs, tmp_path, golden, s3_mock):
     assert stats()["bad_signature"] == 6
 
 
+def test_upload_send_endpoint_down(programs, tmp_path, golden):
+    """No server listening: every PUT fails, the app reports it and exits non-zero (no hang,
+    no SIGPIPE)."""
+    import socket
+    with socket.socket() as sk:  # a port that was free a moment ago and has no listener
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    r, _ = _upload(["--cpu"], f"http://127.0.0.1:{port}", tmp_path, golden)
+    assert r.returncode == 1 and "6 of 6 PUTs not 200" in r.stderr, r.stderr
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("source,per_job", [("file", False), ("mmap", True), ("memory", True)])
 def test_upload_send_loopback_gpu(programs, tmp_path, golden, s3_mock, source, per_job):
