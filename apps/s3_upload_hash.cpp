@@ -12,7 +12,10 @@
 // each body's SHA-256 against x-amz-content-sha256 and verifies the SigV4 signature): each job
 // thread hashes (per-job mode) and PUTs its own parts in order, as upload.cpp:136-140 runs
 // UploadParts, and the timed pass is then hash + upload.  Only UploadPart requests are sent
-// (no CreateMultipartUpload / CompleteMultipartUpload XML), one connection per part.
+// (no CreateMultipartUpload / CompleteMultipartUpload XML), one connection per part.  As in
+// upload.cpp:94-95 each job sends to an endpoint drawn at random from the --endpoint list, and
+// as DoUploadPart (upload.cpp:55-87) a failed part is sent again while a shared budget of
+// --retries lasts.
 //
 // Part sources (how the bytes reach the hash, mirroring the reference's two upload paths):
 //   --source file    UploadFile (upload.cpp:113-149): parts are (file, offset, size) ranges as
@@ -27,8 +30,9 @@
 //                    upload.cpp:136-140 runs UploadParts), instead of one call for all parts.
 //
 //   s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory] [--per-job]
-//                  [--cpu] [--verify] [--print-headers] [--send] [--devices N] [--repeat R]
-//                  [--endpoint URL --bucket B --key K --access A --secret S --upload-id ID]
+//                  [--cpu] [--verify] [--print-headers] [--send] [--retries N] [--devices N]
+//                  [--repeat R] [--endpoint URL[,URL...] --bucket B --key K --access A
+//                  --secret S --upload-id ID]
 #include <fcntl.h>
 #include <netdb.h>
 #include <sys/mman.h>
@@ -41,6 +45,7 @@
 #include <chrono>
 #include <csignal>
 #include <future>
+#include <random>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -138,8 +143,9 @@ double now() {
 void usage() {
   std::fprintf(stderr,
                "usage: s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory]\n"
-               "       [--per-job] [--cpu] [--verify] [--print-headers] [--send] [--endpoint URL --bucket B\n"
-               "        --key K --access A --secret S --upload-id ID] [--devices N] [--repeat R]\n");
+               "       [--per-job] [--cpu] [--verify] [--print-headers] [--send] [--retries N]\n"
+               "       [--endpoint URL[,URL...] --bucket B --key K --access A --secret S --upload-id ID]\n"
+               "       [--devices N] [--repeat R]\n");
 }
 
 }  // namespace
@@ -148,7 +154,7 @@ int main(int argc, char** argv) {
   std::string file, endpoint = "http://127.0.0.1:9000", bucket = "bucket1", key = "key1";
   std::string access = "ACCESS", secret = "SECRET", upload_id = "UPLOAD-ID";
   std::string source = "file";
-  int jobs = 1, ppj = 1, devices = 0, repeat = 1;
+  int jobs = 1, ppj = 1, devices = 0, repeat = 1, max_retries = 0;
   bool cpu = false, verify = false, print_headers = false, per_job = false, send_parts = false;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
@@ -163,6 +169,7 @@ int main(int argc, char** argv) {
     else if (a == "--verify") verify = true;
     else if (a == "--print-headers") print_headers = true;
     else if (a == "--send") send_parts = true;
+    else if (a == "--retries") max_retries = std::atoi(next().c_str());
     else if (a == "--endpoint") endpoint = next();
     else if (a == "--bucket") bucket = next();
     else if (a == "--key") key = next();
@@ -229,11 +236,18 @@ int main(int argc, char** argv) {
   // Signed UploadPart headers of part i: its digest in x-amz-content-sha256 instead of
   // UNSIGNED-PAYLOAD (aws_sign.cpp:236-237); the memory path forwards it too, where the
   // reference's DoUploadPart drops it (multipart_upload.cpp:131-136).
-  auto part_config = [&](size_t i) {
+  std::vector<std::string> endpoints;  // cfg.endpoints (s3-client.h), comma-separated here
+  for (size_t b = 0, e; b <= endpoint.size(); b = e + 1) {
+    e = endpoint.find(',', b);
+    if (e == std::string::npos) e = endpoint.size();
+    if (e > b) endpoints.push_back(endpoint.substr(b, e - b));
+  }
+  if (endpoints.empty()) { usage(); return 2; }
+  auto part_config = [&](size_t i, const std::string& ep) {
     s3h::sigv4::SignConfig c;
     c.access = access;
     c.secret = secret;
-    c.endpoint = endpoint;
+    c.endpoint = ep;
     c.method = "PUT";
     c.bucket = bucket;
     c.key = key;
@@ -243,24 +257,31 @@ int main(int argc, char** argv) {
     c.headers = {{"content-length", std::to_string(parts[i].size)}};
     return c;
   };
-  std::string host, port;
-  if (send_parts) {  // http://HOST:PORT only (loopback, no TLS)
-    const size_t h0 = endpoint.find("://"), c = endpoint.rfind(':');
-    if (endpoint.rfind("http://", 0) != 0 || c == std::string::npos || c <= h0 + 3) {
-      std::fprintf(stderr, "--send needs --endpoint http://HOST:PORT\n");
+  std::vector<std::pair<std::string, std::string>> hostport;
+  for (const std::string& ep : endpoints) {  // http://HOST:PORT only (loopback, no TLS)
+    const size_t h0 = ep.find("://"), c = ep.rfind(':');
+    if (send_parts && (ep.rfind("http://", 0) != 0 || c == std::string::npos || c <= h0 + 3)) {
+      std::fprintf(stderr, "--send needs --endpoint http://HOST:PORT[,...]\n");
       return 2;
     }
-    host = endpoint.substr(h0 + 3, c - h0 - 3);
-    port = endpoint.substr(c + 1);
+    hostport.emplace_back(send_parts ? ep.substr(h0 + 3, c - h0 - 3) : "", send_parts ? ep.substr(c + 1) : "");
   }
-  std::atomic<int> put_failed{0};
-  auto put = [&](size_t i) {
-    const s3h::sigv4::SignConfig c = part_config(i);
-    const std::string target = "/" + bucket + "/" + key + "?" + s3h::sigv4::UrlEncode(c.parameters);
+  std::atomic<int> put_failed{0}, retries{0};
+  // Part i to endpoint e, signed afresh (new x-amz-date) on every attempt; a failed attempt
+  // is repeated while the shared retry budget lasts (retriesG, upload.cpp:55-69).
+  auto put = [&](size_t i, size_t e) {
     const uint8_t* mem = source == "file" ? nullptr : ptrs[i];
-    if (put_part(host, port, target, s3h::sigv4::SignHeaders(c), mem, fd, offs[i], lens[i]) != 200)
-      ++put_failed;
+    for (;;) {
+      const s3h::sigv4::SignConfig c = part_config(i, endpoints[e]);
+      const std::string target = "/" + bucket + "/" + key + "?" + s3h::sigv4::UrlEncode(c.parameters);
+      if (put_part(hostport[e].first, hostport[e].second, target, s3h::sigv4::SignHeaders(c), mem,
+                   fd, offs[i], lens[i]) == 200)
+        return;
+      if (retries++ >= max_retries) break;
+    }
+    ++put_failed;
   };
+  std::mt19937 rng{std::random_device{}()};
   std::vector<std::vector<size_t>> job_parts(jobs);
   for (size_t i = 0; i < parts.size(); ++i) job_parts[parts[i].job].push_back(i);
   auto cpu_hash = [&](size_t i) {
@@ -299,11 +320,13 @@ int main(int argc, char** argv) {
       std::vector<std::future<void>> fut;
       for (int j = 0; j < jobs; ++j) {
         if (job_parts[j].empty()) continue;
-        fut.push_back(std::async(std::launch::async, [&, j] {
+        // RandomIndex(0, cfg.endpoints.size() - 1) per job (upload.cpp:94-95)
+        const size_t ep = std::uniform_int_distribution<size_t>(0, endpoints.size() - 1)(rng);
+        fut.push_back(std::async(std::launch::async, [&, j, ep] {
           if (!cpu && per_job) gpu(job_parts[j]);
           for (size_t i : job_parts[j]) {
             if (cpu) cpu_hash(i);
-            if (send_parts) put(i);
+            if (send_parts) put(i, ep);
           }
         }));
       }
@@ -341,7 +364,7 @@ int main(int argc, char** argv) {
                 hex[i].c_str());
   if (print_headers)
     for (size_t i = 0; i < parts.size(); ++i)
-      for (const auto& kv : s3h::sigv4::SignHeaders(part_config(i)))
+      for (const auto& kv : s3h::sigv4::SignHeaders(part_config(i, endpoints[0])))
         std::printf("# part %d %s: %s\n", parts[i].number, kv.first.c_str(), kv.second.c_str());
   std::string what = cpu ? std::string("cpu lib/hash drop-in")
                          : "gpu batch (H2D included, source " + source +
@@ -351,7 +374,8 @@ int main(int argc, char** argv) {
                double(size) / (1 << 30), dt, double(size) / (1 << 30) / dt,
                verify ? (mismatches ? ", VERIFY FAILED" : ", verified vs CPU") : "");
   if (send_parts)
-    std::fprintf(stderr, " (%d of %zu PUTs not 200)", put_failed.load(), parts.size() * size_t(repeat));
+    std::fprintf(stderr, " (%d of %zu PUTs not 200, %d retries)", put_failed.load(),
+                 parts.size() * size_t(repeat), retries.load());
   if (repeat > 1) std::fprintf(stderr, " (pass %d of %d; first pass %.3f s)", repeat, repeat, first);
   if (!cpu) std::fprintf(stderr, " (GPU runtime start-up before it: %.3f s)", init_s);
   std::fprintf(stderr, "\n");

@@ -14,7 +14,8 @@ and checks each one the way an S3 server would:
   lib/src/aws_sign.cpp:226-308 builds it (403 SignatureDoesNotMatch otherwise).
 
 A verified part gets 200 with `ETag: "<md5 of body>"` (what S3 returns for UploadPart).
-`GET /stats` returns JSON counts.  Run: `s3_mock_server.py --port 0 --port-file F` (prints
+`--fail-every K` answers every K-th PUT with 503 SlowDown after reading it (to exercise the
+uploader's retries, upload.cpp:55-87).  `GET /stats` returns JSON counts.  Run: `s3_mock_server.py --port 0 --port-file F` (prints
 the bound port).  Nothing is stored."""
 import argparse
 import hashlib
@@ -57,7 +58,9 @@ class Server(ThreadingHTTPServer):
 class Handler(BaseHTTPRequestHandler):
     protocol_version = "HTTP/1.1"
     secret = "SECRET"
-    stats = {"parts": 0, "bytes": 0, "bad_hash": 0, "bad_signature": 0, "short_body": 0}
+    stats = {"parts": 0, "bytes": 0, "bad_hash": 0, "bad_signature": 0, "short_body": 0,
+             "injected_503": 0, "puts": 0}
+    fail_every = 0
     lock = threading.Lock()
 
     def log_message(self, *a):  # quiet
@@ -86,6 +89,13 @@ class Handler(BaseHTTPRequestHandler):
                 self.stats["short_body"] += 1
             self.close_connection = True
             return
+        with self.lock:
+            self.stats["puts"] += 1
+            inject = self.fail_every > 0 and self.stats["puts"] % self.fail_every == 0
+            if inject:
+                self.stats["injected_503"] += 1
+        if inject:
+            return self._reply(503, b"SlowDown")
         claimed = self.headers.get("x-amz-content-sha256", "")
         digest = hashlib.sha256(body).hexdigest()
         if claimed != digest:
@@ -119,8 +129,10 @@ def main():
     ap.add_argument("--port", type=int, default=0)
     ap.add_argument("--port-file", default="")
     ap.add_argument("--secret", default="SECRET")
+    ap.add_argument("--fail-every", type=int, default=0)
     a = ap.parse_args()
     Handler.secret = a.secret
+    Handler.fail_every = a.fail_every
     srv = Server(("127.0.0.1", a.port), Handler)
     port = srv.server_address[1]
     if a.port_file:

@@ -108,28 +108,33 @@ def test_upload_counterpart_memory_multipart(programs, tmp_path, golden, jobs, p
     assert "UNSIGNED-PAYLOAD" not in r.stdout
 
 
-@pytest.fixture
-def s3_mock():
+def _start_mock(*args):
     """tests/s3_mock_server.py on a free loopback port: checks every PUT body's SHA-256 against
-    x-amz-content-sha256 and verifies its SigV4 signature (config 5's endpoint; MinIO absent)."""
+    x-amz-content-sha256 and verifies its SigV4 signature (config 5's endpoint; MinIO absent).
+    Returns (process, url, stats())."""
     import json
     import sys
     import time
     import urllib.request
     proc = subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "s3_mock_server.py"),
-                             "--port", "0"], stdout=subprocess.PIPE, text=True)
-    try:
-        port = int(proc.stdout.readline())
-        url = f"http://127.0.0.1:{port}"
+                             "--port", "0", *args], stdout=subprocess.PIPE, text=True)
+    url = f"http://127.0.0.1:{int(proc.stdout.readline())}"
 
-        def stats():
-            for _ in range(50):
-                try:
-                    with urllib.request.urlopen(url + "/stats", timeout=5) as r:
-                        return json.loads(r.read())
-                except OSError:
-                    time.sleep(0.1)
-            raise RuntimeError("mock S3 server not answering")
+    def stats():
+        for _ in range(50):
+            try:
+                with urllib.request.urlopen(url + "/stats", timeout=5) as r:
+                    return json.loads(r.read())
+            except OSError:
+                time.sleep(0.1)
+        raise RuntimeError("mock S3 server not answering")
+    return proc, url, stats
+
+
+@pytest.fixture
+def s3_mock():
+    proc, url, stats = _start_mock()
+    try:
         yield url, stats
     finally:
         proc.kill()
@@ -184,3 +189,25 @@ def test_upload_send_loopback_gpu(programs, tmp_path, golden, s3_mock, source, p
     assert [x[4] for x in _parse_parts(r.stdout)] == [p["digest"] for p in t["parts"]]
     s = stats()
     assert s["parts"] == 6 and s["bad_hash"] == 0 and s["bad_signature"] == 0, s
+
+
+def test_upload_send_retries_and_endpoints(programs, tmp_path, golden):
+    """upload.cpp's endpoint list and retries: jobs draw their endpoint at random from two
+    servers (upload.cpp:94-95); one server answers every 3rd PUT with 503, and a failed part is
+    signed and sent again while the shared --retries budget lasts (upload.cpp:55-87).  With no
+    budget the failures surface."""
+    servers = [_start_mock("--fail-every", "3"), _start_mock()]
+    try:
+        urls = ",".join(u for _, u, _ in servers)
+        for _ in range(2):
+            r, t = _upload(["--cpu", "--retries", "20"], urls, tmp_path, golden)
+            assert r.returncode == 0, r.stderr
+        st = [f() for _, _, f in servers]
+        assert sum(x["parts"] for x in st) == 12, st
+        assert all(x["bad_hash"] == 0 and x["bad_signature"] == 0 for x in st), st
+        r, _ = _upload(["--cpu", "--retries", "0"], servers[0][1], tmp_path, golden)
+        assert r.returncode == 1 and "2 of 6 PUTs not 200" in r.stderr, r.stderr
+    finally:
+        for p, _, _ in servers:
+            p.kill()
+            p.wait()
