@@ -19,6 +19,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -1116,9 +1117,8 @@ bool same_work(const HostReq& a, const HostReq& b) {
 }
 
 // One context, one shard: a single request as it is, several merged into one part list.
-void run_batch(const std::vector<HostReq*>& batch) {
+int run_merged(HostCtx* C, const std::vector<HostReq*>& batch) {
   const HostReq& f = *batch[0];
-  HostCtx* C = host_ctx_cache().acquire(f.sh->device);
   int rc;
   if (batch.size() == 1) {
     rc = run_host_shard(*C, *f.sh, f.algos, f.nalgo, *f.src, f.lengths, f.digests, f.slice);
@@ -1165,8 +1165,24 @@ void run_batch(const std::vector<HostReq*>& batch) {
       }
     }
   }
+  return rc;
+}
+
+// Runs a batch and hands every request its status; nothing escapes, so the device queue's
+// leader always gets to mark the batch done.
+void run_batch(const std::vector<HostReq*>& batch) {
+  HostCtx* C = nullptr;
+  int rc;
+  try {
+    C = host_ctx_cache().acquire(batch[0]->sh->device);
+    rc = run_merged(C, batch);
+  } catch (const std::bad_alloc&) {
+    rc = fail(S3H_ENOMEM, "host batch: out of host memory");
+  } catch (...) {
+    rc = fail(S3H_EHIP, "host batch: unexpected exception");
+  }
   const std::string err = rc ? g_err : std::string();
-  host_ctx_cache().release(C, rc == S3H_OK);
+  if (C) host_ctx_cache().release(C, rc == S3H_OK);
   for (HostReq* r : batch) {
     r->rc = rc;
     r->err = err;
