@@ -136,3 +136,36 @@ def test_two_group_solo_grid(torch_cuda, oracle):
         assert torch.equal(one, many), n
         del data
         _release(torch)
+
+
+def test_64bit_lengths_and_offsets(torch_cuda):
+    """Sizes past 32 bits: a part of 512 MiB + 7 B (its bit length, 2^32 + 56, has a non-zero
+    high word in the padding, alloc_padded utility.cpp:42-56) and small parts placed beyond
+    the 4 GiB byte offset of the device buffer, hashed by resumable launches of ~2 s each over
+    block ranges (sha256_stream semantics).  Bit-exact vs hashlib."""
+    import hashlib
+    torch = torch_cuda
+    big = 512 * MIB + 7
+    lens = np.array([big, 0, 55, 64, 1000, 8 * MIB + 1], dtype=np.uint64)
+    offs = np.array([0, (4 << 30) + 3, (4 << 30) + 256, (4 << 30) + 4096 + 1, (4 << 30) + 9000,
+                     (4 << 30) + 16 * MIB], dtype=np.uint64)
+    data = torch.empty(int(offs[-1] + lens[-1]) + 256, dtype=torch.uint8, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(61)
+    for o, L in zip(offs, lens):
+        if L:
+            data[int(o):int(o) + int(L)] = torch.randint(0, 256, (int(L),), dtype=torch.uint8,
+                                                         device="cuda", generator=g)
+    want = [hashlib.sha256(data[int(o):int(o) + int(L)].cpu().numpy().tobytes()).hexdigest()
+            for o, L in zip(offs, lens)]
+    plan = s3.Plan(offs, lens)
+    info = plan.info()
+    assert info["max_blocks"] == (big + 9 + 63) // 64
+    out = torch.zeros((len(lens), 8), dtype=torch.int32, device="cuda")
+    step = 2 << 20  # blocks per launch: ~2 s of one chain
+    for b in range(0, info["max_blocks"], step):
+        plan.launch_range(data.data_ptr(), out, b, min(b + step, info["max_blocks"]), 0)
+        torch.cuda.synchronize()
+    assert s3.digests_to_text(out.cpu().numpy().view(np.uint32)) == want
+    plan.close()
+    del data, out
+    _release(torch)
