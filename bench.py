@@ -76,6 +76,8 @@ def parse():
                     help="skip the BASELINE config-4 sub-measurement of multi-GPU runs")
     ap.add_argument("--no-c5", action="store_true",
                     help="skip the config-5 loopback upload sub-measurement of the default line")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the C3 / C4-shard sub-measurements of the default N=1 line")
     return ap.parse_args()
 
 
@@ -383,6 +385,13 @@ def main():
             end = int(offs[n - 1] + lens[n - 1])
             host = data[:end].cpu().numpy()
             line["cpu_baseline"] = cpu_baseline(host, offs, lens, gd, n, args.algo)
+            del host
+        if (world == 1 and args.config == "c2" and args.algo == "sha256" and not args.parts_per_gpu
+                and not args.part_bytes and not args.no_configs):
+            del data, digests
+            plan.close()
+            torch.cuda.empty_cache()
+            line["configs"] = {c: single_gpu_config(s3, torch, dev, c) for c in ("c3", "c4")}
     c4 = None
     if world > 1 and args.config == "c2" and args.algo == "sha256" and not args.no_c4:
         del data, digests
@@ -423,6 +432,55 @@ def host_resident(s3, torch, data, ids, lens, offs, gd, reps: int = 3):
            "digests_match_device_run": bool(np.array_equal(out, gd))}
     del host, h, views
     return res
+
+
+def single_gpu_config(s3, torch, dev, cfg: str, steps: int = 2) -> dict:
+    """BASELINE configs 3 and 4 beside the C2 headline of the default N=1 line, so every
+    single-GPU configuration has a driver-run number: C3 = 4,096 x U[5,64] MiB (~138 GiB
+    resident), C4 = rank 0's shard of 65,536 x 8 MiB over 8 GPUs (parts 8k, 64 GiB).  HIP-event
+    kernel time on the launch stream, AUTO kernel, fixture parity."""
+    from s3client_amd.shard import pack_offsets, shard_ids
+    if cfg == "c3":
+        ids, lens, offs, name = workload("c3", 0, 1, 0)
+    else:
+        ids = shard_ids(65536, 0, 8)
+        lens = np.full(8192, 8 * MIB, dtype=np.uint64)
+        offs = pack_offsets(lens)
+        name = "C4: rank 0 of 8 -- 8192 x 8 MiB (global parts 8k)"
+    data = torch.empty(int(offs[-1] + lens[-1]) + 256, dtype=torch.uint8, device=dev)
+    s3.generate_parts(data, offs, lens, ids, SEED)
+    stream = torch.cuda.current_stream(dev)
+    plan = s3.Plan(offs, lens, device=dev.index)
+    out = torch.zeros((len(lens), 8), dtype=torch.int32, device=dev)
+    plan.launch(data, out, stream)
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        plan.launch(data, out, stream)
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = (time.perf_counter() - t0) / steps
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    gd = out.cpu().numpy().view(np.uint32)
+    fx = golden_fixtures(cfg, "sha256")
+    checked = [k for k, p in enumerate(ids) if int(p) in fx]
+    bad = sum(s3_hex(gd[k]) != fx[int(ids[k])] for k in checked)
+    info = plan.info()
+    plan.close()
+    del data, out
+    torch.cuda.empty_cache()
+    part_bytes = float(lens.sum())
+    algo = part_bytes + 32 * len(lens)
+    return {"workload": name, "kernel": info["kernel"], "grid": info["grid"],
+            "solo_workgroups": info["solo"], "steps": steps,
+            "GiBps": round(part_bytes / 2**30 / wall, 3), "ms_per_step": round(1e3 * wall, 3),
+            "kernel_ms": round(kern_ms, 3),
+            "hbm_roofline_frac": round(algo / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5),
+            "bound": "the longest part's chain" if cfg == "c3" else "per-wave issue of 8,192 chains",
+            "parity": {"fixtures_checked": len(checked), "mismatches": int(bad)}}
 
 
 def c5_loopback(data, offs, lens, gd, nparts: int = 128, jobs: int = 16, repeat: int = 2):
