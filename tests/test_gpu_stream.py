@@ -136,3 +136,25 @@ def test_stream_two_group_grid_ragged_updates(torch_cuda, oracle):
     """3,000 messages (AUTO = the two-group skew kernel): every update re-sorts the plans and
     re-plans the solo workgroups for that update's ragged chunk lengths (plan_refill)."""
     _check_stream(oracle, "sha256", "auto", n=3000, rounds=3, maxlen=20000, seed=13, finals=1)
+
+
+def test_concurrent_stream_objects(torch_cuda, oracle):
+    """Four threads each drive their own stream object (objects uploaded as their chunks
+    arrive, one per upload job) at the same time: SHA-256 on three, MD5 on one; every digest
+    vs the oracle over the concatenated chunks."""
+    import threading
+    errors = []
+
+    def job(k):
+        try:
+            _check_stream(oracle, "md5" if k == 3 else "sha256", "auto", 40 + 7 * k, 6, 20000,
+                          seed=70 + k, finals=2)
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(f"{k}: {e!r}")
+
+    th = [threading.Thread(target=job, args=(k,)) for k in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
