@@ -166,6 +166,12 @@ int s3h_sha256_file_parts(const char *path, const uint64_t *offsets, const uint6
 int s3h_sha256_md5_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                               uint32_t *sha256_digests, uint32_t *md5_digests, int ndevices,
                               uint64_t slice_bytes);
+/* Both digests of (file, offset, size) parts, each slice read once (pread into pinned
+ * staging) and crossing PCIe once: s3h_sha256_file_parts for uploads that also send
+ * Content-MD5.  Same arguments and errors as s3h_sha256_file_parts. */
+int s3h_sha256_md5_file_parts(const char *path, const uint64_t *offsets, const uint64_t *lengths,
+                              uint64_t n, uint32_t *sha256_digests, uint32_t *md5_digests,
+                              int ndevices, uint64_t slice_bytes);
 int s3h_sha256_md5_batch_device(int device, const void *d_base, const uint64_t *offsets,
                                 const uint64_t *lengths, uint64_t n, uint32_t *d_sha256,
                                 uint32_t *d_md5, void *stream);

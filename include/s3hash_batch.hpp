@@ -100,6 +100,17 @@ inline DualDigests sha256_md5_batch(const std::vector<const uint8_t*>& parts,
   return d;
 }
 
+// The same for (file, offset, size) parts (s3h_sha256_md5_file_parts): each slice is read once.
+inline DualDigests file_part_sha256_md5(const std::string& path, const std::vector<uint64_t>& offsets,
+                                        const std::vector<uint64_t>& lengths, int ndevices = 0) {
+  if (offsets.size() != lengths.size()) throw std::invalid_argument("offsets/lengths size mismatch");
+  DualDigests d{std::vector<uint32_t>(8 * offsets.size()), std::vector<uint32_t>(4 * offsets.size())};
+  if (!offsets.empty())
+    batch_check(s3h_sha256_md5_file_parts(path.c_str(), offsets.data(), lengths.data(),
+                                          offsets.size(), d.sha256.data(), d.md5.data(), ndevices, 0));
+  return d;
+}
+
 // n objects hashed as their bodies arrive (s3h_stream_*): append() one chunk per object
 // (any length, 0 allowed), finish() -> n digests of everything appended since the last
 // finish(), after which the object restarts with n empty messages.  The batched, on-device

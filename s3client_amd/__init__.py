@@ -7,6 +7,7 @@ from .hashing import (Plan, device_count, digests_to_text, generate_parts, hash_
                       cpu_backend, md5, md5_batch_device, md5_batch_host, multipart_etag,
                       verify_batch_device, verify_batch_host, Stream,
                       sha256_md5_batch_device, sha256_md5_batch_host, sha256_file_parts,
+                      sha256_md5_file_parts,
                       trim, sha256_batch_host_on)
 from .upload import upload_parts_geometry, UploadPart
 from ._native import S3HashError, LIB_PATH
@@ -15,5 +16,6 @@ __all__ = ["Plan", "device_count", "digests_to_text", "generate_parts", "hash_to
            "hmac256", "nblocks", "sha256", "sha256_batch_device", "sha256_batch_host",
            "cpu_backend", "md5", "md5_batch_device", "md5_batch_host", "multipart_etag",
            "verify_batch_device", "verify_batch_host", "Stream",
-           "sha256_md5_batch_device", "sha256_md5_batch_host", "sha256_file_parts", "trim", "sha256_batch_host_on",
+           "sha256_md5_batch_device", "sha256_md5_batch_host", "sha256_file_parts",
+           "sha256_md5_file_parts", "trim", "sha256_batch_host_on",
            "upload_parts_geometry", "UploadPart", "S3HashError", "LIB_PATH"]

@@ -1441,34 +1441,62 @@ int s3h_sha256_batch_host_on(const uint8_t* const* parts, const uint64_t* length
                        slice_bytes);
 }
 
-int s3h_sha256_file_parts(const char* path, const uint64_t* offsets, const uint64_t* lengths,
-                          uint64_t n, uint32_t* digests, int ndevices, uint64_t slice_bytes) {
-  if (!path || !offsets || !lengths || !digests || n == 0)
-    return fail(S3H_EINVAL, "file_parts: bad arguments");
+// Open `path` and check that every range lies inside it -- before the call can be merged
+// with other callers' (a batch fails as a whole).  Returns the descriptor or -1 (error set).
+static int open_file_parts(const char* path, const uint64_t* offsets, const uint64_t* lengths,
+                           uint64_t n) {
   const int fd = open(path, O_RDONLY | O_CLOEXEC);
-  if (fd < 0) return fail(S3H_EINVAL, "file_parts: cannot open %s: %s", path, std::strerror(errno));
-  // Every range must lie inside the file -- checked before the call can be merged with other
-  // callers' (a batch fails as a whole).
+  if (fd < 0) {
+    fail(S3H_EINVAL, "file_parts: cannot open %s: %s", path, std::strerror(errno));
+    return -1;
+  }
   struct stat st {};
   if (fstat(fd, &st) != 0) {
     close(fd);
-    return fail(S3H_EINVAL, "file_parts: cannot stat %s", path);
+    fail(S3H_EINVAL, "file_parts: cannot stat %s", path);
+    return -1;
   }
   for (uint64_t i = 0; i < n; ++i)
     if (offsets[i] > uint64_t(st.st_size) || lengths[i] > uint64_t(st.st_size) - offsets[i]) {
       close(fd);
-      return fail(S3H_EINVAL, "file_parts: part %llu [%llu, +%llu) is past the end of %s (%llu B)",
-                  (unsigned long long)i, (unsigned long long)offsets[i],
-                  (unsigned long long)lengths[i], path, (unsigned long long)st.st_size);
+      fail(S3H_EINVAL, "file_parts: part %llu [%llu, +%llu) is past the end of %s (%llu B)",
+           (unsigned long long)i, (unsigned long long)offsets[i],
+           (unsigned long long)lengths[i], path, (unsigned long long)st.st_size);
+      return -1;
     }
+  return fd;
+}
+
+static int file_parts(const int* algos, int nalgo, const char* path, const uint64_t* offsets,
+                      const uint64_t* lengths, uint64_t n, uint32_t* const* digests,
+                      int ndevices, uint64_t slice_bytes) {
+  if (!path || !offsets || !lengths || n == 0)
+    return fail(S3H_EINVAL, "file_parts: bad arguments");
+  for (int a = 0; a < nalgo; ++a)
+    if (!digests[a]) return fail(S3H_EINVAL, "file_parts: null digest array");
+  const int fd = open_file_parts(path, offsets, lengths, n);
+  if (fd < 0) return S3H_EINVAL;
   PartSource src;
   src.fd = fd;
   src.file_off = offsets;
-  static const int algo = S3H_ALGO_SHA256;
-  uint32_t* const out[1] = {digests};
-  const int rc = batch_host(&algo, 1, src, lengths, n, out, ndevices, slice_bytes);
+  const int rc = batch_host(algos, nalgo, src, lengths, n, digests, ndevices, slice_bytes);
   close(fd);
   return rc;
+}
+
+int s3h_sha256_file_parts(const char* path, const uint64_t* offsets, const uint64_t* lengths,
+                          uint64_t n, uint32_t* digests, int ndevices, uint64_t slice_bytes) {
+  static const int algo = S3H_ALGO_SHA256;
+  uint32_t* const out[1] = {digests};
+  return file_parts(&algo, 1, path, offsets, lengths, n, out, ndevices, slice_bytes);
+}
+
+int s3h_sha256_md5_file_parts(const char* path, const uint64_t* offsets, const uint64_t* lengths,
+                              uint64_t n, uint32_t* sha256_digests, uint32_t* md5_digests,
+                              int ndevices, uint64_t slice_bytes) {
+  static const int algos[2] = {S3H_ALGO_SHA256, S3H_ALGO_MD5};
+  uint32_t* const out[2] = {sha256_digests, md5_digests};
+  return file_parts(algos, 2, path, offsets, lengths, n, out, ndevices, slice_bytes);
 }
 
 int s3h_sha256_md5_batch_device(int device, const void* d_base, const uint64_t* offsets,

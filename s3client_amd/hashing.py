@@ -362,6 +362,20 @@ def sha256_file_parts(path: str, offsets, lengths, ndevices: int = 0,
     return out
 
 
+def sha256_md5_file_parts(path: str, offsets, lengths, ndevices: int = 0,
+                          slice_bytes: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """SHA-256 (n, 8) and MD5 (n, 4) uint32 digests of file ranges, each slice read once
+    (s3h_sha256_md5_file_parts): x-amz-content-sha256 and Content-MD5 of UploadFilePart parts."""
+    offs, lens = _u64(offsets), _u64(lengths)
+    if offs.shape != lens.shape or offs.ndim != 1 or offs.size == 0:
+        raise ValueError("offsets and lengths must be 1-D, equal length and non-empty")
+    sha = np.zeros((offs.size, DIGEST_WORDS), dtype=np.uint32)
+    m5 = np.zeros((offs.size, 4), dtype=np.uint32)
+    check(lib().s3h_sha256_md5_file_parts(os.fsencode(path), _p64(offs), _p64(lens), offs.size,
+                                          sha.ctypes.data, m5.ctypes.data, ndevices, slice_bytes))
+    return sha, m5
+
+
 def trim() -> None:
     """Free the host path's cached per-device buffers (HBM ring, pinned staging, plans):
     s3h_trim.  A process that shares the GPU with other work calls this when it is done."""

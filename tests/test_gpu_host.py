@@ -252,6 +252,34 @@ def test_file_parts_many_parts(torch_cuda, oracle, tmp_path):
         s3.sha256_file_parts(str(path), bad_offs, bad_lens)
 
 
+def test_dual_digest_file_parts(torch_cuda, golden, tmp_path):
+    """s3h_sha256_md5_file_parts: the transfer test's file as its six (offset, size) parts --
+    SHA-256 vs the lib/hash goldens, MD5s vs md5_file's and the multipart ETag -- and 2,500
+    ragged ranges of a random file vs hashlib (both digests, each slice read once)."""
+    import hashlib
+    t = golden["transfer"]
+    path = tmp_path / "xfer.bin"
+    (np.arange(t["size"], dtype=np.uint64) % 128).astype(np.uint8).tofile(path)
+    sha, m5 = s3.sha256_md5_file_parts(str(path), [p["offset"] for p in t["parts"]],
+                                       [p["size"] for p in t["parts"]])
+    assert s3.digests_to_text(sha) == [p["digest"] for p in t["parts"]]
+    assert s3.digests_to_text(m5, 4) == [p["digest"] for p in golden["md5"]["transfer"]]
+    assert s3.multipart_etag(m5) == golden["md5"]["transfer_etag"]
+    rng = np.random.default_rng(60)
+    size = 24 * MIB + 5
+    data = np.frombuffer(rng.bytes(size), dtype=np.uint8)
+    path2 = tmp_path / "dual.bin"
+    data.tofile(path2)
+    n = 2500
+    lens = rng.integers(0, 20000, n)
+    offs = rng.integers(0, size - 20000, n)
+    lens[:4] = [0, 55, 56, 64]
+    sha, m5 = s3.sha256_md5_file_parts(str(path2), offs, lens)
+    views = [data[o:o + L].tobytes() for o, L in zip(offs, lens)]
+    assert s3.digests_to_text(sha) == [hashlib.sha256(v).hexdigest() for v in views]
+    assert s3.digests_to_text(m5, 4) == [hashlib.md5(v).hexdigest() for v in views]
+
+
 def test_two_plans_on_two_streams(torch_cuda, oracle):
     """Two device-resident plans launched concurrently on two torch streams."""
     torch = torch_cuda
