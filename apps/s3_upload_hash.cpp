@@ -30,7 +30,8 @@
 //                    upload.cpp:136-140 runs UploadParts), instead of one call for all parts.
 //
 //   s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory] [--per-job]
-//                  [--cpu] [--verify] [--print-headers] [--send] [--retries N] [--devices N]
+//                  [--cpu] [--verify] [--print-headers] [--send] [--retries N] [--content-md5]
+//                  [--devices N]
 //                  [--repeat R] [--endpoint URL[,URL...] --bucket B --key K --access A
 //                  --secret S --upload-id ID]
 #include <fcntl.h>
@@ -54,6 +55,7 @@
 #include <vector>
 
 #include "aws_sign.h"
+#include "md5.h"
 #include "s3hash_batch.hpp"
 #include "sha256.h"
 
@@ -136,6 +138,21 @@ int put_part(const std::string& host, const std::string& port, const std::string
   return code;
 }
 
+// Content-MD5 header value: base64 of the 16 digest bytes (RFC 1864).
+std::string base64(const uint8_t* p, size_t n) {
+  static const char k[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  std::string o;
+  for (size_t i = 0; i < n; i += 3) {
+    const uint32_t v = uint32_t(p[i]) << 16 | (i + 1 < n ? uint32_t(p[i + 1]) << 8 : 0) |
+                       (i + 2 < n ? p[i + 2] : 0);
+    o += k[v >> 18];
+    o += k[(v >> 12) & 63];
+    o += i + 1 < n ? k[(v >> 6) & 63] : '=';
+    o += i + 2 < n ? k[v & 63] : '=';
+  }
+  return o;
+}
+
 double now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -143,7 +160,7 @@ double now() {
 void usage() {
   std::fprintf(stderr,
                "usage: s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory]\n"
-               "       [--per-job] [--cpu] [--verify] [--print-headers] [--send] [--retries N]\n"
+               "       [--per-job] [--cpu] [--verify] [--print-headers] [--send] [--retries N] [--content-md5]\n"
                "       [--endpoint URL[,URL...] --bucket B --key K --access A --secret S --upload-id ID]\n"
                "       [--devices N] [--repeat R]\n");
 }
@@ -156,6 +173,7 @@ int main(int argc, char** argv) {
   std::string source = "file";
   int jobs = 1, ppj = 1, devices = 0, repeat = 1, max_retries = 0;
   bool cpu = false, verify = false, print_headers = false, per_job = false, send_parts = false;
+  bool content_md5 = false;  // also send Content-MD5: both digests from one pass
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -170,6 +188,7 @@ int main(int argc, char** argv) {
     else if (a == "--print-headers") print_headers = true;
     else if (a == "--send") send_parts = true;
     else if (a == "--retries") max_retries = std::atoi(next().c_str());
+    else if (a == "--content-md5") content_md5 = true;
     else if (a == "--endpoint") endpoint = next();
     else if (a == "--bucket") bucket = next();
     else if (a == "--key") key = next();
@@ -218,7 +237,7 @@ int main(int argc, char** argv) {
     offs.push_back(p.offset);
   }
 
-  std::vector<std::string> hex(parts.size());
+  std::vector<std::string> hex(parts.size()), md5b64(content_md5 ? parts.size() : 0);
   // GPU runtime start-up (device discovery, code-object load) happens once per process in a
   // real uploader: do it before the timed hash stage with a one-part warm-up batch.
   double init_s = 0;
@@ -255,6 +274,7 @@ int main(int argc, char** argv) {
     // partNumber = i + 1 (multipart_upload.cpp:79, :126)
     c.parameters = {{"partNumber", std::to_string(parts[i].number + 1)}, {"uploadId", upload_id}};
     c.headers = {{"content-length", std::to_string(parts[i].size)}};
+    if (content_md5) c.headers["Content-MD5"] = md5b64[i];  // sent, not signed (aws_sign.cpp:266-271)
     return c;
   };
   std::vector<std::pair<std::string, std::string>> hostport;
@@ -290,6 +310,11 @@ int main(int argc, char** argv) {
     char t[65];
     sha256::hash_to_text(h, t);
     hex[i] = t;
+    if (content_md5) {
+      uint32_t m[4];
+      md5::md5(ptrs[i], lens[i], m);
+      md5b64[i] = base64(reinterpret_cast<const uint8_t*>(m), 16);
+    }
   };
   // GPU: the parts of `idx` through the chosen source, hex digests into hex[idx[k]]
   auto gpu = [&](const std::vector<size_t>& idx) {
@@ -299,6 +324,18 @@ int main(int argc, char** argv) {
       p.push_back(ptrs[i]);
       l.push_back(lens[i]);
       o.push_back(offs[i]);
+    }
+    if (content_md5) {  // both digests, each slice read and copied once
+      const sha256::DualDigests d = source == "file"
+                                        ? sha256::file_part_sha256_md5(file, o, l, devices)
+                                        : sha256::sha256_md5_batch(p, l, devices);
+      for (size_t k = 0; k < idx.size(); ++k) {
+        char t[65];
+        sha256::hash_to_text(const_cast<uint32_t*>(&d.sha256[8 * k]), t);
+        hex[idx[k]] = t;
+        md5b64[idx[k]] = base64(reinterpret_cast<const uint8_t*>(&d.md5[4 * k]), 16);
+      }
+      return;
     }
     const std::vector<std::string> h = source == "file"
                                            ? sha256::file_part_hashes(file, o, l, devices)

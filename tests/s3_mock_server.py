@@ -11,13 +11,15 @@ and checks each one the way an S3 server would:
   `x-amz-content-sha256` header (400 XAmzContentSHA256Mismatch otherwise), and
 * the SigV4 `Authorization` header verifies: the canonical request is rebuilt from the
   received method, path, query and the headers named in SignedHeaders, as
-  lib/src/aws_sign.cpp:226-308 builds it (403 SignatureDoesNotMatch otherwise).
+  lib/src/aws_sign.cpp:226-308 builds it (403 SignatureDoesNotMatch otherwise), and
+* a `Content-MD5` header, when sent, is the base64 MD5 of the body (400 BadDigest otherwise).
 
 A verified part gets 200 with `ETag: "<md5 of body>"` (what S3 returns for UploadPart).
 `--fail-every K` answers every K-th PUT with 503 SlowDown after reading it (to exercise the
 uploader's retries, upload.cpp:55-87).  `GET /stats` returns JSON counts.  Run: `s3_mock_server.py --port 0 --port-file F` (prints
 the bound port).  Nothing is stored."""
 import argparse
+import base64
 import hashlib
 import hmac
 import json
@@ -59,7 +61,7 @@ class Handler(BaseHTTPRequestHandler):
     protocol_version = "HTTP/1.1"
     secret = "SECRET"
     stats = {"parts": 0, "bytes": 0, "bad_hash": 0, "bad_signature": 0, "short_body": 0,
-             "injected_503": 0, "puts": 0}
+             "injected_503": 0, "puts": 0, "md5_checked": 0, "bad_md5": 0}
     fail_every = 0
     lock = threading.Lock()
 
@@ -102,6 +104,13 @@ class Handler(BaseHTTPRequestHandler):
             with self.lock:
                 self.stats["bad_hash"] += 1
             return self._reply(400, b"XAmzContentSHA256Mismatch")
+        cmd5 = self.headers.get("Content-MD5")
+        if cmd5 is not None:
+            ok = cmd5 == base64.b64encode(hashlib.md5(body).digest()).decode()
+            with self.lock:
+                self.stats["md5_checked" if ok else "bad_md5"] += 1
+            if not ok:
+                return self._reply(400, b"BadDigest")
         auth = self.headers.get("Authorization", "")
         try:
             fields = dict(kv.strip().split("=", 1) for kv in auth.split(" ", 1)[1].split(","))

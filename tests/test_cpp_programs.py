@@ -211,3 +211,28 @@ def test_upload_send_retries_and_endpoints(programs, tmp_path, golden):
         for p, _, _ in servers:
             p.kill()
             p.wait()
+
+
+def test_upload_send_content_md5_cpu(programs, tmp_path, golden, s3_mock):
+    """--content-md5: each part also carries Content-MD5 (base64 of md5::md5 of the part); the
+    endpoint checks it against the body (400 BadDigest otherwise) besides the SHA-256 and the
+    signature."""
+    url, stats = s3_mock
+    r, t = _upload(["--cpu", "--content-md5"], url, tmp_path, golden)
+    assert r.returncode == 0, r.stderr
+    s = stats()
+    assert s["parts"] == 6 and s["md5_checked"] == 6 and s["bad_md5"] == 0, s
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("source,per_job", [("file", True), ("memory", False)])
+def test_upload_send_content_md5_gpu(programs, tmp_path, golden, s3_mock, source, per_job):
+    """The same with both digests from the GPU's dual pass (file ranges: one pread per slice
+    for both; memory parts: one copy per slice for both)."""
+    url, stats = s3_mock
+    r, t = _upload(["--source", source, "--content-md5"] + (["--per-job"] if per_job else []),
+                   url, tmp_path, golden)
+    assert r.returncode == 0, r.stderr
+    assert [x[4] for x in _parse_parts(r.stdout)] == [p["digest"] for p in t["parts"]]
+    s = stats()
+    assert s["parts"] == 6 and s["md5_checked"] == 6 and s["bad_md5"] == 0, s
