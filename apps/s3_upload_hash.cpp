@@ -30,7 +30,8 @@
 //                    upload.cpp:136-140 runs UploadParts), instead of one call for all parts.
 //
 //   s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory] [--per-job]
-//                  [--cpu] [--verify] [--print-headers] [--send] [--retries N] [--content-md5]
+//                  [--cpu] [--verify] [--print-headers] [--send] [--get-verify] [--retries N]
+//                  [--content-md5]
 //                  [--devices N]
 //                  [--repeat R] [--endpoint URL[,URL...] --bucket B --key K --access A
 //                  --secret S --upload-id ID]
@@ -138,6 +139,50 @@ int put_part(const std::string& host, const std::string& port, const std::string
   return code;
 }
 
+// One ranged GetObject over plain HTTP/1.1 (Connection: close) into dst[0, size): the ranged
+// GETs of DownloadPart (lib/src/download.cpp:72-85).  Returns the HTTP status, or -1 on a
+// socket error or a body of another length.
+int get_range(const std::string& host, const std::string& port, const std::string& target,
+              const s3h::sigv4::Map& headers, uint8_t* dst, uint64_t size) {
+  addrinfo hints{}, *ai = nullptr;
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  if (getaddrinfo(host.c_str(), port.c_str(), &hints, &ai) != 0 || !ai) return -1;
+  const int sock = socket(ai->ai_family, ai->ai_socktype, ai->ai_protocol);
+  const bool connected = sock >= 0 && connect(sock, ai->ai_addr, ai->ai_addrlen) == 0;
+  freeaddrinfo(ai);
+  if (!connected) {
+    if (sock >= 0) close(sock);
+    return -1;
+  }
+  std::string req = "GET " + target + " HTTP/1.1\r\n";
+  for (const auto& kv : headers) req += kv.first + ": " + kv.second + "\r\n";
+  req += "Connection: close\r\n\r\n";
+  bool ok = send(sock, req.data(), req.size(), MSG_NOSIGNAL) == ssize_t(req.size());
+  std::string head;
+  char buf[65536];
+  size_t hdr_end = std::string::npos;
+  uint64_t got = 0;
+  for (ssize_t r; ok && (r = recv(sock, buf, sizeof buf, 0)) > 0;) {
+    if (hdr_end == std::string::npos) {
+      head.append(buf, size_t(r));
+      hdr_end = head.find("\r\n\r\n");
+      if (hdr_end == std::string::npos) continue;
+      const size_t body0 = hdr_end + 4, n = std::min<uint64_t>(head.size() - body0, size);
+      std::memcpy(dst, head.data() + body0, n);
+      got = head.size() - body0;
+    } else {
+      const uint64_t n = got < size ? std::min<uint64_t>(uint64_t(r), size - got) : 0;
+      std::memcpy(dst + got, buf, n);
+      got += uint64_t(r);
+    }
+  }
+  close(sock);
+  int code = -1;
+  if (!ok || std::sscanf(head.c_str(), "HTTP/%*d.%*d %d", &code) != 1) return -1;
+  return got == size ? code : -1;
+}
+
 // Content-MD5 header value: base64 of the 16 digest bytes (RFC 1864).
 std::string base64(const uint8_t* p, size_t n) {
   static const char k[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
@@ -160,7 +205,8 @@ double now() {
 void usage() {
   std::fprintf(stderr,
                "usage: s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory]\n"
-               "       [--per-job] [--cpu] [--verify] [--print-headers] [--send] [--retries N] [--content-md5]\n"
+               "       [--per-job] [--cpu] [--verify] [--print-headers] [--send] [--get-verify]\n"
+               "       [--retries N] [--content-md5]\n"
                "       [--endpoint URL[,URL...] --bucket B --key K --access A --secret S --upload-id ID]\n"
                "       [--devices N] [--repeat R]\n");
 }
@@ -174,6 +220,7 @@ int main(int argc, char** argv) {
   int jobs = 1, ppj = 1, devices = 0, repeat = 1, max_retries = 0;
   bool cpu = false, verify = false, print_headers = false, per_job = false, send_parts = false;
   bool content_md5 = false;  // also send Content-MD5: both digests from one pass
+  bool get_verify = false;   // after the upload, GET every part back and verify it
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -189,6 +236,7 @@ int main(int argc, char** argv) {
     else if (a == "--send") send_parts = true;
     else if (a == "--retries") max_retries = std::atoi(next().c_str());
     else if (a == "--content-md5") content_md5 = true;
+    else if (a == "--get-verify") get_verify = true;
     else if (a == "--endpoint") endpoint = next();
     else if (a == "--bucket") bucket = next();
     else if (a == "--key") key = next();
@@ -394,6 +442,66 @@ int main(int argc, char** argv) {
       mismatches += hex[i] != t;
     }
 
+  // --get-verify: the download side (DownloadFile / DownloadParts, download.cpp:88-130): each
+  // job GETs its parts by byte range into one buffer, then every part is checked against the
+  // digest it was uploaded with -- on the GPU in one s3h_verify_batch_host call (the CPU
+  // drop-in with --cpu).
+  int get_failed = 0;
+  uint64_t down_bad = 0;
+  double t_get = 0, t_check = 0;
+  if (send_parts && get_verify) {
+    std::vector<uint8_t> down(size);
+    std::atomic<int> failed{0};
+    const double g0 = now();
+    std::vector<std::future<void>> fut;
+    for (int j = 0; j < jobs; ++j) {
+      if (job_parts[j].empty()) continue;
+      const size_t e = std::uniform_int_distribution<size_t>(0, endpoints.size() - 1)(rng);
+      fut.push_back(std::async(std::launch::async, [&, j, e] {
+        for (size_t i : job_parts[j]) {
+          s3h::sigv4::SignConfig c;
+          c.access = access;
+          c.secret = secret;
+          c.endpoint = endpoints[e];
+          c.method = "GET";
+          c.bucket = bucket;
+          c.key = key;
+          c.headers = {{"Range", "bytes=" + std::to_string(offs[i]) + "-" +
+                                     std::to_string(offs[i] + lens[i] - 1)}};
+          if (get_range(hostport[e].first, hostport[e].second, "/" + bucket + "/" + key,
+                        s3h::sigv4::SignHeaders(c), down.data() + offs[i], lens[i]) != 206)
+            ++failed;
+        }
+      }));
+    }
+    for (auto& f : fut) f.get();
+    get_failed = failed.load();
+    const double g1 = now();
+    std::vector<uint32_t> want(8 * parts.size());
+    for (size_t i = 0; i < parts.size(); ++i)
+      for (int b = 0; b < 32; ++b)
+        reinterpret_cast<uint8_t*>(&want[8 * i])[b] =
+            uint8_t(std::stoi(hex[i].substr(2 * b, 2), nullptr, 16));
+    std::vector<const uint8_t*> dp(parts.size());
+    for (size_t i = 0; i < parts.size(); ++i) dp[i] = down.data() + offs[i];
+    if (cpu) {
+      for (size_t i = 0; i < parts.size(); ++i) {
+        uint32_t h[8];
+        sha256::sha256(dp[i], lens[i], h);
+        down_bad += std::memcmp(h, &want[8 * i], 32) != 0;
+      }
+    } else {
+      std::vector<uint8_t> bad(parts.size());
+      if (s3h_verify_batch_host(S3H_ALGO_SHA256, dp.data(), lens.data(), parts.size(), want.data(),
+                                bad.data(), &down_bad, devices) != S3H_OK) {
+        std::fprintf(stderr, "verify: %s\n", s3h_last_error());
+        return 1;
+      }
+    }
+    t_get = g1 - g0;
+    t_check = now() - g1;
+  }
+
   std::printf("part,job,offset,size,sha256\n");
   for (size_t i = 0; i < parts.size(); ++i)
     std::printf("%d,%d,%llu,%llu,%s\n", parts[i].number, parts[i].job,
@@ -416,7 +524,11 @@ int main(int argc, char** argv) {
   if (repeat > 1) std::fprintf(stderr, " (pass %d of %d; first pass %.3f s)", repeat, repeat, first);
   if (!cpu) std::fprintf(stderr, " (GPU runtime start-up before it: %.3f s)", init_s);
   std::fprintf(stderr, "\n");
+  if (send_parts && get_verify)
+    std::fprintf(stderr, "download verify: %zu parts, %d GETs failed, %llu mismatches (GET %.3f s, %s check %.3f s)\n",
+                 parts.size(), get_failed, (unsigned long long)down_bad, t_get, cpu ? "CPU" : "GPU",
+                 t_check);
   munmap(const_cast<uint8_t*>(data), size);
   close(fd);
-  return mismatches || put_failed.load() ? 1 : 0;
+  return mismatches || put_failed.load() || get_failed || down_bad ? 1 : 0;
 }

@@ -15,6 +15,9 @@ and checks each one the way an S3 server would:
 * a `Content-MD5` header, when sent, is the base64 MD5 of the body (400 BadDigest otherwise).
 
 A verified part gets 200 with `ETag: "<md5 of body>"` (what S3 returns for UploadPart).
+With `--store` the parts are kept and a signed `GET /{bucket}/{key}` with `Range: bytes=a-b`
+returns that range of the parts concatenated in part-number order (the ranged GETs of
+lib/src/download.cpp:72-103); `--corrupt-get K` flips one byte of the K-th GET's body.
 `--fail-every K` answers every K-th PUT with 503 SlowDown after reading it (to exercise the
 uploader's retries, upload.cpp:55-87).  `GET /stats` returns JSON counts.  Run: `s3_mock_server.py --port 0 --port-file F` (prints
 the bound port).  Nothing is stored."""
@@ -63,6 +66,10 @@ class Handler(BaseHTTPRequestHandler):
     stats = {"parts": 0, "bytes": 0, "bad_hash": 0, "bad_signature": 0, "short_body": 0,
              "injected_503": 0, "puts": 0, "md5_checked": 0, "bad_md5": 0}
     fail_every = 0
+    store = False
+    corrupt_get = 0
+    objects = {}  # "/bucket/key" -> {part number: bytes}
+    gets = 0
     lock = threading.Lock()
 
     def log_message(self, *a):  # quiet
@@ -76,12 +83,48 @@ class Handler(BaseHTTPRequestHandler):
         self.end_headers()
         self.wfile.write(body)
 
+    def _signature_ok(self, payload: str) -> bool:
+        auth = self.headers.get("Authorization", "")
+        try:
+            fields = dict(kv.strip().split("=", 1) for kv in auth.split(" ", 1)[1].split(","))
+            scope = fields["Credential"].split("/", 1)[1]
+            signed = fields["SignedHeaders"].split(";")
+            hdrs = {k.lower(): v for k, v in self.headers.items()}
+            path, _, query = self.path.partition("?")
+            want = expected_signature(self.secret, self.command, path, query, hdrs, signed,
+                                      payload, hdrs.get("x-amz-date", ""), scope)
+            return hmac.compare_digest(want, fields["Signature"])
+        except (KeyError, IndexError, ValueError):
+            return False
+
     def do_GET(self):
         if self.path == "/stats":
             with self.lock:
                 body = json.dumps(self.stats).encode()
             return self._reply(200, body)
-        return self._reply(404)
+        if not self._signature_ok(self.headers.get("x-amz-content-sha256", "")):
+            with self.lock:
+                self.stats["bad_signature"] += 1
+            return self._reply(403, b"SignatureDoesNotMatch")
+        path = self.path.partition("?")[0]
+        with self.lock:
+            parts = self.objects.get(path)
+            obj = b"".join(parts[k] for k in sorted(parts)) if parts else None
+            Handler.gets += 1
+            nth = Handler.gets
+        if obj is None:
+            return self._reply(404, b"NoSuchKey")
+        rng = self.headers.get("Range", "")
+        a, b = 0, len(obj) - 1
+        if rng.startswith("bytes="):
+            lo, _, hi = rng[6:].partition("-")
+            a, b = int(lo), min(int(hi), len(obj) - 1) if hi else len(obj) - 1
+        body = bytearray(obj[a:b + 1])
+        if self.corrupt_get and nth == self.corrupt_get and body:
+            body[len(body) // 2] ^= 0x01
+        with self.lock:
+            self.stats["gets"] = self.stats.get("gets", 0) + 1
+        self._reply(206 if rng else 200, bytes(body))
 
     def do_PUT(self):
         n = int(self.headers.get("content-length", "0"))
@@ -111,25 +154,17 @@ class Handler(BaseHTTPRequestHandler):
                 self.stats["md5_checked" if ok else "bad_md5"] += 1
             if not ok:
                 return self._reply(400, b"BadDigest")
-        auth = self.headers.get("Authorization", "")
-        try:
-            fields = dict(kv.strip().split("=", 1) for kv in auth.split(" ", 1)[1].split(","))
-            scope = fields["Credential"].split("/", 1)[1]
-            signed = fields["SignedHeaders"].split(";")
-            hdrs = {k.lower(): v for k, v in self.headers.items()}
-            path, _, query = self.path.partition("?")
-            want = expected_signature(self.secret, self.command, path, query, hdrs, signed,
-                                      claimed, hdrs.get("x-amz-date", ""), scope)
-            ok = hmac.compare_digest(want, fields["Signature"])
-        except (KeyError, IndexError, ValueError):
-            ok = False
-        if not ok:
+        if not self._signature_ok(claimed):
             with self.lock:
                 self.stats["bad_signature"] += 1
             return self._reply(403, b"SignatureDoesNotMatch")
         with self.lock:
             self.stats["parts"] += 1
             self.stats["bytes"] += n
+            if self.store:
+                path, _, query = self.path.partition("?")
+                pn = int(dict(urllib.parse.parse_qsl(query)).get("partNumber", "0"))
+                self.objects.setdefault(path, {})[pn] = body
         self._reply(200, etag=hashlib.md5(body).hexdigest())
 
 
@@ -139,9 +174,13 @@ def main():
     ap.add_argument("--port-file", default="")
     ap.add_argument("--secret", default="SECRET")
     ap.add_argument("--fail-every", type=int, default=0)
+    ap.add_argument("--store", action="store_true")
+    ap.add_argument("--corrupt-get", type=int, default=0)
     a = ap.parse_args()
     Handler.secret = a.secret
     Handler.fail_every = a.fail_every
+    Handler.store = a.store
+    Handler.corrupt_get = a.corrupt_get
     srv = Server(("127.0.0.1", a.port), Handler)
     port = srv.server_address[1]
     if a.port_file:

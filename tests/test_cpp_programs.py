@@ -236,3 +236,38 @@ def test_upload_send_content_md5_gpu(programs, tmp_path, golden, s3_mock, source
     assert [x[4] for x in _parse_parts(r.stdout)] == [p["digest"] for p in t["parts"]]
     s = stats()
     assert s["parts"] == 6 and s["md5_checked"] == 6 and s["bad_md5"] == 0, s
+
+
+def test_upload_then_download_verify_cpu(programs, tmp_path, golden):
+    """--get-verify: after the upload each job GETs its parts back by byte range (download.cpp
+    geometry) from the storing endpoint and every part is checked against the digest it was
+    uploaded with; a byte flipped in one GET response is caught."""
+    proc, url, stats = _start_mock("--store")
+    try:
+        r, _ = _upload(["--cpu", "--get-verify"], url, tmp_path, golden)
+        assert r.returncode == 0 and "0 GETs failed, 0 mismatches" in r.stderr, r.stderr
+        assert stats()["gets"] == 6
+    finally:
+        proc.kill()
+        proc.wait()
+    proc, url, stats = _start_mock("--store", "--corrupt-get", "4")
+    try:
+        r, _ = _upload(["--cpu", "--get-verify"], url, tmp_path, golden)
+        assert r.returncode == 1 and "0 GETs failed, 1 mismatches" in r.stderr, r.stderr
+    finally:
+        proc.kill()
+        proc.wait()
+
+
+@pytest.mark.gpu
+def test_upload_then_download_verify_gpu(programs, tmp_path, golden):
+    """The same round trip with the GPU: hash + PUT, ranged GETs, one s3h_verify_batch_host
+    call over the downloaded parts (download verification)."""
+    proc, url, stats = _start_mock("--store", "--corrupt-get", "2")
+    try:
+        r, _ = _upload(["--source", "memory", "--get-verify"], url, tmp_path, golden)
+        assert r.returncode == 1 and "0 GETs failed, 1 mismatches" in r.stderr, r.stderr
+        assert "GPU check" in r.stderr
+    finally:
+        proc.kill()
+        proc.wait()
