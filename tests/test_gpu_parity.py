@@ -440,3 +440,33 @@ def test_flag_synchronised_kernels_resumable(torch_cuda, oracle, n, kernel):
     assert torch_cuda.equal(one, many)
     assert np.array_equal(one.cpu().numpy().view(np.uint32), oracle.batch(host, offs, lens))
     plan.close()
+
+
+AUTO_EDGES = [(1, "skew"), (2048, "skew"), (2049, "skew"), (4096, "skew"), (4097, "skews"),
+              (8192, "skews"), (8193, "skewp"), (28672, "skewp"), (28673, "pair"),
+              (32768, "pair"), (32769, "pc"), (65536, "pc"), (65537, "lane")]
+
+
+def test_auto_kernel_edges(torch_cuda, oracle):
+    """Every AUTO switch point of capi.hip resolve_kernel, one part below and above: the plan
+    picks the documented kernel and every digest of ragged small parts (0-300 B,
+    all byte alignments) matches the oracle; SHA-256 + MD5 from the dual path at the dual
+    kernel's switch points (split grid / skew group / skewp group / two streams) vs the oracle
+    as well."""
+    rng = np.random.default_rng(62)
+    host = rng.integers(0, 256, (1 << 20) + 512, dtype=np.uint8)
+    data = _dev_buffer(torch_cuda, host)
+    for n, kernel in AUTO_EDGES:
+        lens = rng.integers(0, 300, n)
+        offs = rng.integers(0, 1 << 20, n)
+        assert s3.Plan(offs, lens).info()["kernel"] == kernel, n
+        got = s3.sha256_batch_device(data, offs, lens).cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, oracle.batch(host, offs, lens, threads=16)), n
+    for n in (1820, 1821, 2048, 2049, 4096, 4097, 8192, 8193):
+        lens = rng.integers(0, 300, n)
+        offs = rng.integers(0, 1 << 20, n)
+        sha, m5 = s3.sha256_md5_batch_device(data, offs, lens)
+        assert np.array_equal(sha.cpu().numpy().view(np.uint32),
+                              oracle.batch(host, offs, lens, threads=16)), n
+        assert np.array_equal(m5.cpu().numpy().view(np.uint32),
+                              oracle.md5_batch(host, offs, lens, threads=16)), n
