@@ -335,3 +335,51 @@ def test_host_batch_shared_simd_kernel_range(torch_cuda, oracle):
     offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
     views = [buf[o:o + L] for o, L in zip(offs, lens)]
     assert np.array_equal(s3.sha256_batch_host(views), oracle.batch(buf, offs, lens, threads=16))
+
+
+def test_device_queue_soak_mixed_calls(torch_cuda, tmp_path):
+    """Eight threads, 12 random host calls each -- SHA-256 from memory or file ranges,
+    SHA-256 + MD5, download verification with a planted mismatch -- all meeting in the
+    device's queue in random combinations; every result vs hashlib."""
+    import hashlib
+    rng0 = np.random.default_rng(63)
+    data = np.frombuffer(rng0.bytes(6 * MIB), dtype=np.uint8)
+    path = tmp_path / "soak.bin"
+    data.tofile(path)
+    errors = []
+
+    def job(k):
+        rng = np.random.default_rng(100 + k)
+        try:
+            for r in range(12):
+                n = int(rng.integers(1, 400))
+                lens = rng.integers(0, 40000, n)
+                offs = rng.integers(0, data.size - 40000, n)
+                views = [data[o:o + L] for o, L in zip(offs, lens)]
+                sha = [hashlib.sha256(v.tobytes()).hexdigest() for v in views]
+                kind = int(rng.integers(0, 4))
+                if kind == 0:
+                    ok = s3.digests_to_text(s3.sha256_batch_host(views)) == sha
+                elif kind == 1:
+                    ok = s3.digests_to_text(s3.sha256_file_parts(str(path), offs, lens)) == sha
+                elif kind == 2:
+                    a, b = s3.sha256_md5_batch_host(views)
+                    ok = (s3.digests_to_text(a) == sha and s3.digests_to_text(b, 4) ==
+                          [hashlib.md5(v.tobytes()).hexdigest() for v in views])
+                else:
+                    want = np.stack([np.frombuffer(bytes.fromhex(h), dtype=np.uint32) for h in sha])
+                    bad = int(rng.integers(0, n))
+                    want[bad, 0] ^= 1
+                    mism = s3.verify_batch_host(views, want)
+                    ok = list(np.flatnonzero(mism)) == [bad]
+                if not ok:
+                    errors.append(f"thread {k} call {r} kind {kind} n {n}")
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(f"thread {k}: {e!r}")
+
+    th = [threading.Thread(target=job, args=(k,)) for k in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
