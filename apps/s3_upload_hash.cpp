@@ -477,24 +477,21 @@ int main(int argc, char** argv) {
     for (auto& f : fut) f.get();
     get_failed = failed.load();
     const double g1 = now();
-    std::vector<uint32_t> want(8 * parts.size());
-    for (size_t i = 0; i < parts.size(); ++i)
-      for (int b = 0; b < 32; ++b)
-        reinterpret_cast<uint8_t*>(&want[8 * i])[b] =
-            uint8_t(std::stoi(hex[i].substr(2 * b, 2), nullptr, 16));
     std::vector<const uint8_t*> dp(parts.size());
     for (size_t i = 0; i < parts.size(); ++i) dp[i] = down.data() + offs[i];
     if (cpu) {
       for (size_t i = 0; i < parts.size(); ++i) {
         uint32_t h[8];
         sha256::sha256(dp[i], lens[i], h);
-        down_bad += std::memcmp(h, &want[8 * i], 32) != 0;
+        char t[65];
+        sha256::hash_to_text(h, t);
+        down_bad += hex[i] != t;
       }
     } else {
-      std::vector<uint8_t> bad(parts.size());
-      if (s3h_verify_batch_host(S3H_ALGO_SHA256, dp.data(), lens.data(), parts.size(), want.data(),
-                                bad.data(), &down_bad, devices) != S3H_OK) {
-        std::fprintf(stderr, "verify: %s\n", s3h_last_error());
+      try {
+        for (bool b : sha256::verify_payloads(dp, lens, hex, devices)) down_bad += b;
+      } catch (const std::exception& e) {
+        std::fprintf(stderr, "verify: %s\n", e.what());
         return 1;
       }
     }

@@ -111,6 +111,29 @@ inline DualDigests file_part_sha256_md5(const std::string& path, const std::vect
   return d;
 }
 
+// Download-side check (s3h_verify_batch_host): true for every part whose SHA-256 differs from
+// the expected hex digest (the x-amz-content-sha256 it was uploaded with).
+inline std::vector<bool> verify_payloads(const std::vector<const uint8_t*>& parts,
+                                         const std::vector<uint64_t>& lengths,
+                                         const std::vector<std::string>& expected_hex,
+                                         int ndevices = 0) {
+  if (parts.size() != lengths.size() || parts.size() != expected_hex.size())
+    throw std::invalid_argument("parts/lengths/expected size mismatch");
+  std::vector<uint32_t> want(8 * parts.size());
+  for (size_t i = 0; i < parts.size(); ++i) {
+    if (expected_hex[i].size() != 64) throw std::invalid_argument("expected digest is not 64 hex");
+    for (int b = 0; b < 32; ++b)
+      reinterpret_cast<uint8_t*>(&want[8 * i])[b] =
+          uint8_t(std::stoi(expected_hex[i].substr(2 * b, 2), nullptr, 16));
+  }
+  std::vector<uint8_t> bad(parts.size());
+  uint64_t count = 0;
+  if (!parts.empty())
+    batch_check(s3h_verify_batch_host(S3H_ALGO_SHA256, parts.data(), lengths.data(), parts.size(),
+                                      want.data(), bad.data(), &count, ndevices));
+  return std::vector<bool>(bad.begin(), bad.end());
+}
+
 // n objects hashed as their bodies arrive (s3h_stream_*): append() one chunk per object
 // (any length, 0 allowed), finish() -> n digests of everything appended since the last
 // finish(), after which the object restarts with n empty messages.  The batched, on-device
