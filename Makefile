@@ -15,16 +15,14 @@ LIB := $(LIBDIR)/libs3hash.so
 
 all: $(LIB) oracle cpptests
 
-# The device code object is kept (build/isa, -save-temps) and the chain-loop instruction counts
-# bench.py reports are derived from its disassembly (tools/isa_counts.py ->
-# s3client_amd/kernel_isa_counts.json).
-OBJDUMP ?= /opt/rocm/lib/llvm/bin/llvm-objdump
-ISA_DIS := build/isa/capi_gfx950.dis
-$(LIBDIR)/capi.o: $(CSRC)/capi.hip $(CSRC)/sha256_kernels.hip $(CSRC)/sha256_device.hpp $(CSRC)/sha256_skew_rounds.inc $(CSRC)/sha256_producer_simple.inc include/s3hash.h tools/isa_counts.py
+# The chain-loop instruction counts bench.py reports, the kernels' code hashes and the
+# error-word check are read from the gfx950 code object the linked library ships
+# (tools/isa_counts.py -> s3client_amd/kernel_isa_counts.json; disassembly in build/isa).
+ISA_DIS := build/isa/libs3hash_gfx950.dis
+KSRC := $(CSRC)/capi.hip $(CSRC)/sha256_kernels.hip $(CSRC)/sha256_device.hpp $(CSRC)/sha256_skew_rounds.inc $(CSRC)/sha256_producer_simple.inc include/s3hash.h
+$(LIBDIR)/capi.o: $(KSRC)
 	@mkdir -p $(LIBDIR) build/isa
 	cd build/isa && $(HIPCC) $(HIPFLAGS) -save-temps -c -o ../../$@ ../../$<
-	$(OBJDUMP) -d --symbolize-operands build/isa/capi-hip-amdgcn-amd-amdhsa-gfx950.o > $(ISA_DIS)
-	python3 tools/isa_counts.py $(ISA_DIS) s3client_amd/kernel_isa_counts.json
 
 $(LIBDIR)/lib_hash.o: $(CSRC)/cpu/lib_hash.cpp include/sha256.h include/utility.h include/s3hash.h
 	@mkdir -p $(LIBDIR)
@@ -34,13 +32,24 @@ $(LIBDIR)/lib_md5.o: $(CSRC)/cpu/lib_md5.cpp include/md5.h include/utility.h inc
 	@mkdir -p $(LIBDIR)
 	$(CXX) $(CXXFLAGS) -c -o $@ $<
 
-$(LIB): $(LIBDIR)/capi.o $(LIBDIR)/lib_hash.o $(LIBDIR)/lib_md5.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
+$(LIB): $(LIBDIR)/capi.o $(LIBDIR)/lib_hash.o $(LIBDIR)/lib_md5.o tools/isa_counts.py tools/code_object.py
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(filter %.o,$^) -lpthread
+	python3 tools/isa_counts.py $@ s3client_amd/kernel_isa_counts.json $(ISA_DIS)
+
+# Forced-fault build for tests/test_gpu_errors.py: every flag-synchronised producer stops
+# publishing after its first step and waits give up after 4,096 polls, so each consumer
+# wave's wait times out -- the device error word must fail the call.  Test-only (never the
+# product library; loaded through S3H_LIBRARY in a child process).
+STALL := tests/cpp/build/libs3hash_stall.so
+$(STALL): $(KSRC) $(LIBDIR)/lib_hash.o $(LIBDIR)/lib_md5.o
+	@mkdir -p tests/cpp/build
+	$(HIPCC) $(HIPFLAGS) -DS3H_EXP_STALL_PRODUCER=1 -DS3H_EXP_SPIN_LIMIT=4096 -c -o tests/cpp/build/capi_stall.o $(CSRC)/capi.hip
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ tests/cpp/build/capi_stall.o $(LIBDIR)/lib_hash.o $(LIBDIR)/lib_md5.o -lpthread
 
 oracle: $(LIB)
 	$(MAKE) -C oracle
 
-CPPTESTS := tests/cpp/build/dropin_test tests/cpp/build/sign_test
+CPPTESTS := tests/cpp/build/dropin_test tests/cpp/build/sign_test $(STALL)
 cpptests: $(CPPTESTS) apps/build/s3-upload-hash
 
 apps/build/s3-upload-hash: apps/s3_upload_hash.cpp s3client_amd/host/aws_sign.cpp s3client_amd/host/aws_sign.h include/s3hash_batch.hpp $(LIB)

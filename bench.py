@@ -108,17 +108,77 @@ def workload(cfg: str, rank: int, world: int, ppg: int, part_bytes: int = 0):
     return ids, lens, pack_offsets(lens), name
 
 
-def pmc_traffic(cfg: str, kernel: str, algo_bytes: float):
-    """HBM bytes per launch from the committed rocprofv3 --pmc summary of this config+kernel
-    (profiles/rNN_<cfg>_<kernel>_pmc.json, FETCH_SIZE x2 + WRITE_SIZE), scaled per launch."""
+def isa_key(kname: str, nparts: int) -> str:
+    """tools/isa_counts.py key of the kernel a plan runs (the two-group skew grid above 2,048)."""
+    return "skew_nc2" if kname == "skew" and nparts > 2048 else kname
+
+
+def library_info(keys=()) -> dict:
+    """Which libs3hash.so this run loaded (S3H_LIBRARY may name an experiment build), its
+    sha256, and the code hashes of the kernels measured (tools/code_object.py: the key that
+    profiles/*_pmc.json records, so a counter profile is only used for the code it measured)."""
+    from s3client_amd import _native
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import code_object
+    import isa_counts
+    path = _native.LIB_PATH
+    info = {"path": os.path.relpath(path, ROOT), "sha256": code_object.file_sha256(path),
+            "product_build": os.path.realpath(path) == os.path.realpath(
+                os.path.join(ROOT, "s3client_amd", "lib", "libs3hash.so"))}
+    try:
+        lines = code_object.disassemble(path)
+        info["kernel_code_hash"] = {k: code_object.code_hash(lines, isa_counts.ALL_KERNELS[k])
+                                    for k in keys if k in isa_counts.ALL_KERNELS}
+    except Exception as e:  # no llvm-objdump: the profile link is then unverifiable
+        info["kernel_code_hash"] = {}
+        info["kernel_code_hash_error"] = repr(e)
+    return info
+
+
+def pmc_traffic(cfg: str, kname: str, key: str, code_hash, algo_bytes: float):
+    """HBM bytes per launch from the newest committed rocprofv3 --pmc summary of this config
+    and kernel (profiles/rNN_<cfg>_<kernel>_pmc.json: FETCH_SIZE x2 + WRITE_SIZE, separate
+    passes, tools/pmc_summary.py), scaled to this launch -- ONLY if that profile measured the
+    same kernel machine code as this run loaded (its kernel_code_hash); otherwise null with
+    the reason.  Returns (traffic, source, note)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{cfg}_{kernel}_pmc.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{cfg}_{kname}_pmc.json")))
     if not files:
-        return None, None
+        return None, None, "no PMC profile of this config and kernel"
+    rel = os.path.relpath(files[-1], ROOT)
     with open(files[-1]) as f:
         s = json.load(f)
+    if not code_hash:
+        return None, rel, "kernel code hash of this build unavailable: profile link unverifiable"
+    if s.get("kernel_key") != key or s.get("kernel_code_hash") != code_hash:
+        return None, rel, (f"{rel} measured kernel {s.get('kernel_key')} code "
+                           f"{s.get('kernel_code_hash')}; this build runs {key} code {code_hash}")
     ratio = s["traffic_bytes_per_launch"] / s["algorithmic_bytes_per_launch"]
-    return int(round(ratio * algo_bytes)), os.path.relpath(files[-1], ROOT)
+    return int(round(ratio * algo_bytes)), rel, (
+        f"same kernel code {code_hash} (profile: library {str(s.get('library_sha256'))[:12]}, "
+        f"commit {str(s.get('git_head'))[:12]})")
+
+
+def clock_probe(torch, plan, info, data, digests, stream, dev):
+    """One extra launch (outside any timed region) on which every consumer wave of a skew /
+    skewp / skews plan records s_memtime and s_memrealtime around its chain loop -> the live
+    shader clock and cycles per block; None for kernels without the probe."""
+    if info["kernel"] not in ("skew", "skewp", "skews"):
+        return None
+    clocks = torch.zeros(4 * 4 * max(info["grid"], info["groups"]), dtype=torch.int64, device=dev)
+    waves = plan.set_clock_probe(clocks)
+    plan.launch(data, digests, stream)
+    torch.cuda.synchronize(dev)
+    plan.set_clock_probe(None)
+    plan.status(stream)
+    c = clocks.view(-1, 4)[:waves].cpu().numpy().astype(np.float64)
+    cyc, rt = c[:, 1] - c[:, 0], c[:, 3] - c[:, 2]
+    ok = rt > 0
+    if not ok.any():
+        return None
+    return {"clock_GHz": round(float(np.median(cyc[ok] / rt[ok] * 0.1)), 3),  # rt: 100 MHz ticks
+            "cycles_per_block": round(float(np.max(cyc[ok])) / info["max_blocks"], 1),
+            "waves": int(ok.sum())}
 
 
 def _cgroup_cpu_quota():
@@ -230,16 +290,15 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     # One process per GPU.  S3H_BENCH_SHARE_GPU=1 (rehearsal on a 1-GPU box only) maps ranks
-    # onto the visible devices modulo their count and uses gloo for the timing collectives.
+    # onto the visible devices modulo their count.  The timing collectives (barrier, max over
+    # ranks, per-rank parity) use gloo on the host in every multi-process run: the data path
+    # has no collective at all, so RCCL would buy nothing, and the one-GPU rehearsal then runs
+    # exactly the code of a real N-GPU run.
     share = os.environ.get("S3H_BENCH_SHARE_GPU") == "1"
     gpu = local % torch.cuda.device_count() if share else local
     torch.cuda.set_device(gpu)
-    backend = "gloo" if share else "nccl"
     if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
-        else:
-            dist.init_process_group("gloo")
+        dist.init_process_group("gloo")
     dev = torch.device("cuda", gpu)
     local = gpu
 
@@ -264,6 +323,7 @@ def main():
     for _ in range(args.warmup):
         plan.launch(data, digests, stream)
     torch.cuda.synchronize(dev)
+    plan.status(stream)
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
@@ -279,33 +339,18 @@ def main():
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
+    # every timed launch's device error word (a timed-out producer/consumer wait): raises
+    plan.status(stream)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    t = torch.tensor([wall, kern_ms], dtype=torch.float64,
-                     device=dev if backend == "nccl" else "cpu")
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)  # max over ranks: the slowest GPU sets the time
     wall, kern_ms_max = float(t[0]), float(t[1])
 
-    # Clock probe (outside the timed region): one more launch on which every consumer wave
-    # records s_memtime / s_memrealtime around its chain loop -> live shader clock and cycles
-    # per block (skew kernel only).
-    probe = None
-    if kname in ("skew", "skewp", "skews"):
-        clocks = torch.zeros(4 * 4 * info["grid"], dtype=torch.int64, device=dev)
-        waves = plan.set_clock_probe(clocks)
-        plan.launch(data, digests, stream)
-        torch.cuda.synchronize(dev)
-        plan.set_clock_probe(None)
-        c = clocks.view(-1, 4)[:waves].cpu().numpy().astype(np.float64)
-        cyc, rt = c[:, 1] - c[:, 0], c[:, 3] - c[:, 2]
-        ok = rt > 0
-        if ok.any():
-            ghz = float(np.median(cyc[ok] / rt[ok] * 0.1))  # rt ticks at 100 MHz
-            probe = {"clock_GHz": round(ghz, 3),
-                     "cycles_per_block": round(float(np.max(cyc[ok])) / info["max_blocks"], 1),
-                     "waves": int(ok.sum())}
+    probe = clock_probe(torch, plan, info, data, digests, stream, dev)
 
-    # parity spot-check of the last timed step's digests against the reference fixtures
+    # parity of the last timed step's digests against the reference fixtures, on EVERY rank
+    # (tests/golden: C2/C4 parts and four parts of each rank's shard at N = 2, 4, 8)
     gd = digests.cpu().numpy().view(np.uint32)
     fixtures = golden_fixtures(args.config, args.algo, args.part_bytes)
     checked = bad = 0
@@ -314,14 +359,19 @@ def main():
         if want is not None:
             checked += 1
             bad += s3.hash_to_text(gd[slot]) != want
+    par = per_rank(dist, world, [checked, int(bad)])
 
+    key = isa_key(kname, len(lens))
+    lib_info = library_info([key])
     part_bytes = float(lens.sum())
     total_bytes = part_bytes * world * args.steps
     value = total_bytes / 2**30 / wall
     algo_bytes = part_bytes + 4 * plan.words * len(lens)  # read once + digests written
     achieved = algo_bytes / (kern_ms / 1e3) / 1e9      # GB/s, this rank's kernel
     compressions = info["total_blocks"]
-    traffic, traffic_src = pmc_traffic(args.config, kname, algo_bytes)
+    traffic, traffic_src, traffic_note = pmc_traffic(args.config, kname, key,
+                                                     lib_info["kernel_code_hash"].get(key),
+                                                     algo_bytes)
     # one part = one sequential chain on one lane: report what one chain sustains and how
     # many of the chip's 256 CU x 4 SIMD x 64 = 65,536 lanes the batch can occupy
     chain_gbps = float(lens.max()) / (kern_ms / 1e3) / 1e9
@@ -348,6 +398,7 @@ def main():
                                      * 64 / 1e9, 1),
              "parallelism_ceiling": round(min(len(lens), 65536) / 65536, 5)}
 
+    line = None
     if rank == 0:
         line = {
             "metric": ("device-resident SHA-256 GiB/s over 8 MiB parts; bit-exact digests vs lib/hash"
@@ -362,10 +413,16 @@ def main():
                        "kernel": kname, "grid": info["grid"], "groups": info["groups"],
                        "solo_workgroups": info["solo"],
                        "parallelism": f"parts sharded round-robin over {world} GPU(s), no collective"},
-            "parity": {"fixtures_checked": checked, "mismatches": int(bad)},
+            "parity": {"fixtures_checked": sum(r[0] for r in par),
+                       "mismatches": sum(r[1] for r in par),
+                       "per_rank": [{"rank": k, "fixtures_checked": r[0], "mismatches": r[1]}
+                                    for k, r in enumerate(par)]},
+            "status": "ok: device error word clear after every launch (s3h_plan_status)",
+            "library": lib_info,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_source": traffic_src,
+                         "traffic_note": traffic_note,
                          "kernel_ms": round(kern_ms, 3),
                          "kernel_ms_max_rank": round(kern_ms_max, 3),
                          "bytes_per_launch": int(algo_bytes),
@@ -392,19 +449,35 @@ def main():
             plan.close()
             torch.cuda.empty_cache()
             line["configs"] = {c: single_gpu_config(s3, torch, dev, c) for c in ("c3", "c4")}
-    c4 = None
-    if world > 1 and args.config == "c2" and args.algo == "sha256" and not args.no_c4:
+    if world > 1 and args.config == "c2" and args.algo == "sha256":
         del data, digests
         plan.close()
         torch.cuda.empty_cache()
-        c4 = c4_shard(args, s3, torch, dist, dev, rank, world, local, backend)
+        if not args.no_c4:
+            c4 = c4_shard(args, s3, torch, dist, dev, rank, world, local)
+            if rank == 0:
+                line["c4"] = c4
+        if not args.no_host_resident:
+            dist.barrier()  # the other ranks wait while rank 0 drives every GPU from the host
+            if rank == 0:
+                line["host_resident"] = host_resident_multi(s3, torch, dev, world)
+            dist.barrier()
     if rank == 0:
-        if c4 is not None:
-            line["c4"] = c4
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def per_rank(dist, world: int, vals):
+    """[vals of rank 0, vals of rank 1, ...] (int64) -- gloo all_gather; [vals] at N = 1."""
+    import torch
+    t = torch.tensor(vals, dtype=torch.int64)
+    if world == 1:
+        return [[int(x) for x in t]]
+    allt = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(allt, t)
+    return [[int(x) for x in a] for a in allt]
 
 
 def host_resident(s3, torch, data, ids, lens, offs, gd, reps: int = 3):
@@ -463,6 +536,7 @@ def single_gpu_config(s3, torch, dev, cfg: str, steps: int = 2) -> dict:
         b.record(stream)
     torch.cuda.synchronize(dev)
     wall = (time.perf_counter() - t0) / steps
+    plan.status(stream)  # device error word clear (raises otherwise)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     gd = out.cpu().numpy().view(np.uint32)
     fx = golden_fixtures(cfg, "sha256")
@@ -544,10 +618,13 @@ def s3_hex(words) -> str:
     return np.ascontiguousarray(words, dtype=np.uint32).tobytes().hex()
 
 
-def c4_shard(args, s3, torch, dist, dev, rank, world, local, backend, steps: int = 3):
+def c4_shard(args, s3, torch, dist, dev, rank, world, local, steps: int = 3):
     """BASELINE config 4 beside the C2 headline of a multi-GPU run: 8,192 x 8 MiB per GPU,
     global part p on rank p % N (65,536 parts = 512 GiB at N = 8), no collective on the data
-    path; per-GPU and aggregate GiB/s with the max-over-ranks time."""
+    path.  The AUTO kernel (skews: producers on their consumers' SIMDs, ~1.4 kW per board) and
+    skewp (~0.7 kW) are timed on the same parts, each with the clock probe, so the node's power
+    envelope decides between them on measured numbers; per-GPU and aggregate GiB/s over the
+    max-over-ranks time, fixture parity on every rank (four own-shard fixtures per rank)."""
     from s3client_amd.shard import shard_ids
     per, L = 8192, 8 * MIB
     ids = shard_ids(per * world, rank, world)
@@ -556,47 +633,106 @@ def c4_shard(args, s3, torch, dist, dev, rank, world, local, backend, steps: int
     data = torch.empty(per * L, dtype=torch.uint8, device=dev)
     s3.generate_parts(data, offs, lens, ids, SEED)
     stream = torch.cuda.current_stream(dev)
-    plan = s3.Plan(offs, lens, device=local)
-    out = torch.zeros((per, 8), dtype=torch.int32, device=dev)
-    plan.launch(data, out, stream)
-    torch.cuda.synchronize(dev)
-    dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        plan.launch(data, out, stream)
-    torch.cuda.synchronize(dev)
-    mine = time.perf_counter() - t0
-    dist.barrier()
-    wall = time.perf_counter() - t0
-    tt = torch.tensor([mine], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-    allt = [torch.zeros_like(tt) for _ in range(world)]
-    dist.all_gather(allt, tt)
-    per_rank = [float(x[0]) for x in allt]
-    gd = out.cpu().numpy().view(np.uint32)
-    with open(os.path.join(ROOT, "tests", "golden", "sha256_golden.json")) as f:
-        gold = json.load(f)
-    fx = {e["p"]: e["digest"] for e in gold["c2_parts"] + gold["c4_parts"]}
-    bad = sum(s3.hash_to_text(gd[k]) != fx[int(p)] for k, p in enumerate(ids) if int(p) in fx)
-    badt = torch.tensor([bad, sum(int(p) in fx for p in ids)], dtype=torch.int64,
-                        device=dev if backend == "nccl" else "cpu")
-    dist.all_reduce(badt)
-    kernel = plan.info()["kernel"]
-    plan.close()
-    del data, out
-    torch.cuda.empty_cache()
+    fx = golden_fixtures("c4", "sha256")
     gib_gpu = per * L * steps / 2**30
     algo = per * (L + 32)  # bytes read once + digests written, per GPU per launch
-    return {"workload": f"C4: {per} x 8 MiB per GPU, {per * world} parts over {world} GPUs "
-                        "(part p on rank p % N)",
-            "kernel": kernel, "steps": steps,
-            "per_gpu_GiBps": [round(gib_gpu / t, 3) for t in per_rank],
-            "aggregate_GiBps": round(gib_gpu * world / max(max(per_rank), wall), 3),
-            "ms_per_step_max_rank": round(1e3 * max(per_rank) / steps, 3),
-            # per GPU: algorithmic HBM bytes per launch / launch time vs the 8 TB/s HBM roof
+    res = {"workload": f"C4: {per} x 8 MiB per GPU, {per * world} parts over {world} GPUs "
+                       "(part p on rank p % N)", "steps": steps, "kernels": {}}
+    for kern in ("auto", "skewp"):
+        plan = s3.Plan(offs, lens, device=local, kernel=kern)
+        info = plan.info()
+        out = torch.zeros((per, 8), dtype=torch.int32, device=dev)
+        plan.launch(data, out, stream)
+        plan.status(stream)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            plan.launch(data, out, stream)
+        torch.cuda.synchronize(dev)
+        mine = time.perf_counter() - t0
+        dist.barrier()
+        wall = time.perf_counter() - t0
+        plan.status(stream)
+        probe = clock_probe(torch, plan, info, data, out, stream, dev) or {}
+        gd = out.cpu().numpy().view(np.uint32)
+        chk = [k for k, p in enumerate(ids) if int(p) in fx]
+        bad = sum(s3.hash_to_text(gd[k]) != fx[int(ids[k])] for k in chk)
+        plan.close()
+        # per rank: time (us), wall (us), fixtures checked, mismatches, clock (MHz), cycles/block
+        r = per_rank(dist, world, [int(mine * 1e6), int(wall * 1e6), len(chk), int(bad),
+                                   int(probe.get("clock_GHz", 0) * 1e3),
+                                   int(probe.get("cycles_per_block", 0))])
+        t_rank = [x[0] / 1e6 for x in r]
+        res["kernels"][info["kernel"]] = {
+            "per_gpu_GiBps": [round(gib_gpu / t, 3) for t in t_rank],
+            "aggregate_GiBps": round(gib_gpu * world / max(max(t_rank), max(x[1] for x in r) / 1e6), 3),
+            "ms_per_step_max_rank": round(1e3 * max(t_rank) / steps, 3),
             "hbm_roofline_frac_per_gpu": [round(algo * steps / t / 1e9 / HBM_PEAK_GBS, 5)
-                                          for t in per_rank],
-            "parity": {"fixtures_checked": int(badt[1]), "mismatches": int(badt[0])}}
+                                          for t in t_rank],
+            "clock_GHz_per_gpu": [x[4] / 1e3 for x in r],
+            "cycles_per_block_per_gpu": [x[5] for x in r],
+            "parity": {"fixtures_checked": sum(x[2] for x in r), "mismatches": sum(x[3] for x in r),
+                       "fixtures_checked_per_rank": [x[2] for x in r]}}
+        if kern == "auto":
+            res["kernel"] = info["kernel"]
+    del data
+    torch.cuda.empty_cache()
+    auto = res["kernels"][res["kernel"]]
+    res.update({k: auto[k] for k in ("per_gpu_GiBps", "aggregate_GiBps", "ms_per_step_max_rank",
+                                     "hbm_roofline_frac_per_gpu", "parity")})
+    res["faster_kernel"] = max(res["kernels"], key=lambda k: res["kernels"][k]["aggregate_GiBps"])
+    return res
+
+
+def host_resident_multi(s3, torch, dev, world: int, per: int = 1024, reps: int = 3):
+    """Rank 0 of an N-GPU run: the C2 weak-scaling job's parts (1,024 x 8 MiB per GPU, global
+    ids 0..1024N-1) starting and ending in HOST memory, through
+    s3h_sha256_batch_host(..., ndevices=N) -- part i on device i % N, the device-resident
+    line's split -- with every H2D copy inside the timed region.  The parts are generated on
+    this GPU and copied into one pinned buffer beforehand (setup_s, untimed)."""
+    L = 8 * MIB
+    n = per * world
+    t_setup = time.perf_counter()
+    try:
+        host = torch.empty(n * L, dtype=torch.uint8, pin_memory=True)
+    except RuntimeError as e:
+        return {"error": f"pinned host buffer of {n * L / 2**30:.0f} GiB: {e}"}
+    buf = torch.empty(per * L, dtype=torch.uint8, device=dev)
+    lens = np.full(per, L, dtype=np.uint64)
+    offs = np.arange(per, dtype=np.uint64) * np.uint64(L)
+    for c in range(world):
+        s3.generate_parts(buf, offs, lens, np.arange(c * per, (c + 1) * per), SEED)
+        host[c * per * L:(c + 1) * per * L].copy_(buf)
+    del buf
+    torch.cuda.empty_cache()
+    h = host.numpy()
+    views = [h[i * L:(i + 1) * L] for i in range(n)]
+    setup = time.perf_counter() - t_setup
+    ndev = min(world, torch.cuda.device_count())
+    out = s3.sha256_batch_host(views, ndevices=ndev)  # warm: a cached context per device
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = s3.sha256_batch_host(views, ndevices=ndev)
+        times.append(time.perf_counter() - t0)
+    fx = golden_fixtures("c2", "sha256")
+    chk = [p for p in range(n) if p in fx]
+    bad = sum(s3.hash_to_text(out[p]) != fx[p] for p in chk)
+    threads, cpus = s3.host_threads(ndev)
+    gib = n * L / 2**30
+    del host, h, views
+    s3.trim()
+    return {"metric": f"host-resident (H2D-inclusive) SHA-256 GiB/s over {ndev} GPU(s)",
+            "value": round(gib / float(np.mean(times)), 3), "best": round(gib / min(times), 3),
+            "per_gpu": round(gib / float(np.mean(times)) / ndev, 3), "unit": "GiB/s",
+            "devices": ndev, "parts": n, "reps": reps,
+            "ms_per_batch": round(1e3 * float(np.mean(times)), 2), "setup_s": round(setup, 2),
+            "path": "pinned host parts -> per-device 3-slot HBM ring (one 2-D H2D copy per "
+                    "256 KiB slice) -> skew kernel per slice -> digests D2H "
+                    "(s3h_sha256_batch_host, one host thread per device)",
+            "host_cpus": cpus, "staging_threads_per_device": threads,
+            "fixtures_checked": len(chk), "fixture_mismatches": int(bad)}
 
 
 def host_mode(args, s3, torch, dist, data, ids, lens, offs, world, rank, name):
@@ -635,8 +771,9 @@ def host_mode(args, s3, torch, dist, data, ids, lens, offs, world, rank, name):
 
 def golden_fixtures(cfg: str, algo: str, part_bytes: int = 0) -> dict:
     """{global part id: hex digest} of the committed lib/hash fixtures that apply to this
-    workload's parts: generator-G 8 MiB parts (C2 / C4 ids; MD5: the C2 ids) or the C3 parts
-    (SHA-256 only); none for a --part-bytes override."""
+    workload's parts: generator-G 8 MiB parts (C2 / C4 ids and four parts of every rank's
+    shard at N = 2, 4, 8; MD5: the C2 ids) or the C3 parts (SHA-256 only); none for a
+    --part-bytes override."""
     if part_bytes:
         return {}
     with open(os.path.join(ROOT, "tests", "golden", "sha256_golden.json")) as f:
@@ -644,7 +781,8 @@ def golden_fixtures(cfg: str, algo: str, part_bytes: int = 0) -> dict:
     if algo == "md5":
         src = [] if cfg == "c3" else gold["md5"]["c2_parts"]
     else:
-        src = gold["c3_parts"] if cfg == "c3" else gold["c2_parts"] + gold["c4_parts"]
+        src = (gold["c3_parts"] if cfg == "c3"
+               else gold["c2_parts"] + gold["c4_parts"] + gold["shard_parts"])
     return {e["p"]: e["digest"] for e in src}
 
 

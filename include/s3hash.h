@@ -66,6 +66,13 @@ int s3h_api_version(void);
  * into one batch (their digests are the same as from separate calls).  s3h_trim releases the
  * contexts of idle devices. */
 int s3h_trim(void);
+/* Host threads (the calling thread included) the host path uses per device to stage
+ * pageable parts and file ranges when `ndevices` device shards run at once: the CPUs this
+ * process may use -- its sched_getaffinity mask, capped by the cgroup CPU quota (cpu.max, or
+ * cfs_quota_us / cfs_period_us) -- split evenly over the devices, at least 1 and at most 16.
+ * *cpus (if non-null) receives that CPU count.  Needs no GPU.  The reference's jobs run on
+ * the cores the host grants (lib/src/upload.cpp:136-140, std::async). */
+int s3h_host_threads(int ndevices, int *cpus);
 /* Number of visible HIP devices; S3H_ENODEV (and *count = 0) when there is none. */
 int s3h_device_count(int *count);
 
@@ -83,8 +90,19 @@ int s3h_plan_create_ex(int device, int algo, const uint64_t *offsets, const uint
                        uint64_t n, int kernel, s3h_plan_t *plan);
 int s3h_plan_algo(s3h_plan_t plan);
 int s3h_plan_destroy(s3h_plan_t plan);
-/* Asynchronous on `stream`: d_base and d_digests (n*8 uint32) are device pointers. */
+/* Asynchronous on `stream`: d_base and d_digests (n*8 uint32) are device pointers.  The
+ * launch's success is known only after it has run: call s3h_plan_status before using the
+ * digests. */
 int s3h_plan_launch(s3h_plan_t plan, const void *d_base, uint32_t *d_digests, void *stream);
+/* Waits for `stream`, then reads and clears the plan's device error word, which every launch
+ * of the plan (s3h_plan_launch / _range) ORs its faults into.  S3H_OK: the digests of every
+ * launch since the last status call are valid.  S3H_EHIP ("synchronisation timeout"): a
+ * flag-synchronised kernel (the two-group skew, shared-SIMD skew and dual-digest group
+ * kernels pair a producer and a consumer wave through LDS step counters) gave up a bounded
+ * wait, so the grid drained instead of hanging and those digests are NOT the parts' digests.
+ * The one-shot, host, dual, verification and stream entry points check this word themselves
+ * and fail the call; lib/hash's sha256() (sha256.cpp:147-160) never returns a wrong digest. */
+int s3h_plan_status(s3h_plan_t plan, void *stream);
 /* Resumable form: process blocks [blk_begin, blk_end) of every part, where part p's block b
  * lives at d_base + offsets[p] + 64*(b - blk_origin).  Chaining state is kept in the plan
  * between launches (same stream order required); a part's digest is written by the launch
@@ -129,7 +147,8 @@ int s3h_md5_batch_device(int device, const void *d_base, const uint64_t *offsets
  * slot: slices of 32 MiB / n bytes, down to 64 B) and DMA'd from there; beyond 524,288
  * pageable parts, or when pinned memory is unavailable, each part is DMA'd from pageable memory.
  * Everything is cached per device between calls (s3h_trim).  Safe to call from concurrent
- * threads (a call that finds the device busy builds private resources).  Blocking. */
+ * threads (concurrent calls on a device are merged into one batch, see
+ * s3h_sha256_batch_host_on).  Blocking. */
 int s3h_sha256_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                           uint32_t *digests, int ndevices, uint64_t slice_bytes);
 
@@ -137,8 +156,13 @@ int s3h_md5_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uin
                        uint32_t *digests, int ndevices, uint64_t slice_bytes);
 
 /* The same over an explicit device list: shard k = parts i with i % ndevices == k, hashed on
- * devices[k].  A device may be listed more than once (its shards run concurrently, e.g. one
- * per NUMA node's copy threads, or to exercise sharding on a one-GPU host). */
+ * devices[k].  A device may be listed more than once: its shards then meet in that device's
+ * queue like concurrent callers (below) and run merged into one batch, or one after another
+ * when they arrive apart -- the digests are the same either way (this is how the sharding is
+ * exercised on a one-GPU host).  Concurrent host calls on one device are merged in its queue:
+ * the first caller runs every pending request with the same algorithms and slice size as one
+ * batch; if that batch fails, each request is re-run on its own, so each caller gets its own
+ * status.  Staging threads per device: s3h_host_threads(number of shards). */
 int s3h_sha256_batch_host_on(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                              uint32_t *digests, const int *devices, int ndevices,
                              uint64_t slice_bytes);
@@ -208,9 +232,13 @@ int s3h_stream_create(int device, int algo, uint64_t n, int kernel, s3h_stream_t
 int s3h_stream_update_device(s3h_stream_t s, const void *d_base, const uint64_t *offsets,
                              const uint64_t *lengths, void *stream);
 int s3h_stream_final_device(s3h_stream_t s, uint32_t *d_digests, void *stream);
-/* Host-memory forms (blocking): chunks[i] may be null when lengths[i] == 0. */
+/* Host-memory forms (blocking; they check the launches' device error word like
+ * s3h_plan_status): chunks[i] may be null when lengths[i] == 0. */
 int s3h_stream_update_host(s3h_stream_t s, const uint8_t *const *chunks, const uint64_t *lengths);
 int s3h_stream_final_host(s3h_stream_t s, uint32_t *digests);
+/* Device forms: waits for `stream` and reports (and clears) a fault of any update / final
+ * launch since the last check, as s3h_plan_status does for a plan. */
+int s3h_stream_status(s3h_stream_t s, void *stream);
 /* Bytes appended so far to message i (host bookkeeping; no device sync). */
 int s3h_stream_total(s3h_stream_t s, uint64_t i, uint64_t *total);
 int s3h_stream_destroy(s3h_stream_t s);

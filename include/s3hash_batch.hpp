@@ -120,11 +120,20 @@ inline std::vector<bool> verify_payloads(const std::vector<const uint8_t*>& part
   if (parts.size() != lengths.size() || parts.size() != expected_hex.size())
     throw std::invalid_argument("parts/lengths/expected size mismatch");
   std::vector<uint32_t> want(8 * parts.size());
+  auto nibble = [](char c) -> int {
+    return c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10
+           : c >= 'A' && c <= 'F' ? c - 'A' + 10 : -1;
+  };
   for (size_t i = 0; i < parts.size(); ++i) {
-    if (expected_hex[i].size() != 64) throw std::invalid_argument("expected digest is not 64 hex");
-    for (int b = 0; b < 32; ++b)
-      reinterpret_cast<uint8_t*>(&want[8 * i])[b] =
-          uint8_t(std::stoi(expected_hex[i].substr(2 * b, 2), nullptr, 16));
+    const std::string& h = expected_hex[i];
+    // exactly 64 hex digits: no sign, whitespace or prefix is accepted
+    bool ok = h.size() == 64;
+    for (size_t k = 0; ok && k < 64; ++k) ok = nibble(h[k]) >= 0;
+    if (!ok)
+      throw std::invalid_argument("verify_payloads: expected digest of part " + std::to_string(i) +
+                                  " is not 64 hex digits: \"" + h + "\"");
+    uint8_t* w = reinterpret_cast<uint8_t*>(&want[8 * i]);
+    for (int b = 0; b < 32; ++b) w[b] = uint8_t(nibble(h[2 * b]) << 4 | nibble(h[2 * b + 1]));
   }
   std::vector<uint8_t> bad(parts.size());
   uint64_t count = 0;

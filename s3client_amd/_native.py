@@ -36,7 +36,7 @@ C_ABI_SYMBOLS = (
     "s3h_stream_total", "s3h_stream_destroy", "s3h_plan_set_clock_probe",
     "s3h_sha256_md5_batch_host", "s3h_sha256_md5_batch_device", "s3h_trim",
     "s3h_sha256_file_parts", "s3h_sha256_batch_host_on", "s3h_plan_groups",
-    "s3h_sha256_md5_file_parts",
+    "s3h_sha256_md5_file_parts", "s3h_plan_status", "s3h_stream_status", "s3h_host_threads",
 )
 ALGO_SHA256, ALGO_MD5 = 0, 1
 ALGO_IDS = {"sha256": ALGO_SHA256, "md5": ALGO_MD5}
@@ -93,6 +93,9 @@ def lib() -> ctypes.CDLL:
             L.s3h_plan_launch_range.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                 ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                 ctypes.c_void_p]
+            L.s3h_plan_status.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            L.s3h_stream_status.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            L.s3h_host_threads.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
             L.s3h_plan_set_clock_probe.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
                                                    ctypes.POINTER(ctypes.c_uint32)]
             L.s3h_plan_info.argtypes = [ctypes.c_void_p, u64p, u64p, u64p,

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
+#include <sched.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -15,6 +16,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
 #include <functional>
 #include <memory>
@@ -91,6 +93,7 @@ struct s3h_plan_s {
   int quad_waves = 1;           // skew / quad kernels: consumer waves per workgroup (1-2)
   uint32_t solo = 0;            // two-group skew grid: leading one-group workgroups (plan_solo)
   uint64_t* d_clocks = nullptr; // clock probe buffer (caller-owned), see s3h_plan_set_clock_probe
+  uint32_t* d_err = nullptr;    // device error word (s3h::kErr* bits), read by plan_check
 };
 
 namespace {
@@ -234,10 +237,13 @@ int plan_alloc(int device, int algo, uint64_t cap, s3h_plan_s** out) {
   if (e == hipSuccess) e = hipMalloc(&P->d_out_idx, cap * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&P->d_zero, 256);
   if (e == hipSuccess) e = hipMemset(P->d_zero, 0, 256);
+  if (e == hipSuccess) e = hipMalloc(&P->d_err, sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemset(P->d_err, 0, sizeof(uint32_t));
   if (e != hipSuccess) {
     (void)hipFree(P->d_slots);
     (void)hipFree(P->d_out_idx);
     (void)hipFree(P->d_zero);
+    (void)hipFree(P->d_err);
     delete P;
     *out = nullptr;
     return fail(e == hipErrorOutOfMemory ? S3H_ENOMEM : S3H_EHIP, "plan alloc: %s", hipGetErrorString(e));
@@ -319,7 +325,29 @@ s3h::LaunchArgs make_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests
   A.flags = flags;
   A.clocks = P->d_clocks;
   A.solo = P->solo;
+  A.err = P->d_err;
   return A;
+}
+
+const char* kernel_name(const s3h_plan_s* P) {
+  static const char* const names[] = {"auto", "lane", "pc", "pair", "quad", "skew", "skewp", "skews"};
+  if (P->algo == S3H_ALGO_MD5) return "md5";
+  return P->kernel >= 0 && P->kernel <= S3H_KERNEL_SKEWS ? names[P->kernel] : "?";
+}
+
+// Reads, and clears, plan P's device error word once `s` has run everything launched on it
+// before.  S3H_EHIP when a launch reported a fault (a producer/consumer wait that timed out,
+// sha256_kernels.hip flag_wait_ge): that launch's digests are not the parts' digests, so the
+// call must not succeed -- lib/hash's sha256() never returns a wrong digest.
+int plan_check(s3h_plan_s* P, hipStream_t s) {
+  uint32_t h = 0;
+  HIP_TRY(hipMemcpyAsync(&h, P->d_err, sizeof h, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (h == 0) return S3H_OK;
+  HIP_TRY(hipMemsetAsync(P->d_err, 0, sizeof h, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return fail(S3H_EHIP, "%s kernel: synchronisation timeout (device error word 0x%x): a producer/"
+              "consumer wait timed out, the launch's digests are invalid", kernel_name(P), h);
 }
 
 // Dynamic LDS added to a grid with solo workgroups: 72 KiB of groups + 12 KiB > half of the
@@ -443,6 +471,52 @@ int dual_launch(s3h_plan_s* S, s3h_plan_s* M, const void* d_base, uint32_t* d_sh
 }
 
 // ------------------------------------------------------------------ host streaming path
+// CPUs this process may use: its affinity mask, capped by a cgroup CPU quota (v2 cpu.max, v1
+// cfs_quota_us / cfs_period_us), at least 1.  The reference's jobs run as std::async threads
+// on whatever the host grants (lib/src/upload.cpp:136-140); hardware_concurrency() counts the
+// machine's CPUs instead -- 256 on the GPU box, whose container quota is 16, where
+// over-subscribed copy threads halved the staging rate (BENCH_r02 cpu_baseline.GiBps_by_threads).
+double cgroup_cpu_quota() {
+  double q = 0, per = 0;
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char a[32] = {0};
+    const int got = std::fscanf(f, "%31s %lf", a, &per);
+    std::fclose(f);
+    if (got == 2 && std::strcmp(a, "max") != 0 && per > 0) return std::atof(a) / per;
+    if (got >= 1) return 0;  // "max": unlimited
+  }
+  FILE* fq = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r");
+  FILE* fp = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r");
+  if (fq && fp && std::fscanf(fq, "%lf", &q) == 1 && std::fscanf(fp, "%lf", &per) == 1 && q > 0 &&
+      per > 0) {
+    std::fclose(fq);
+    std::fclose(fp);
+    return q / per;
+  }
+  if (fq) std::fclose(fq);
+  if (fp) std::fclose(fp);
+  return 0;
+}
+
+unsigned host_cpus() {
+  static const unsigned cpus = [] {
+    unsigned n = std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) == 0 && CPU_COUNT(&set) > 0) n = unsigned(CPU_COUNT(&set));
+    const double quota = cgroup_cpu_quota();
+    if (quota > 0) n = std::min(n, std::max(1u, unsigned(std::ceil(quota))));
+    return n;
+  }();
+  return cpus;
+}
+
+// Host threads (the calling thread included) each of `ndevices` concurrent device shards may
+// use to stage its parts: the process's CPUs split evenly, at least 1, at most 16.
+unsigned host_threads_per_device(int ndevices) {
+  return std::min(16u, std::max(1u, host_cpus() / unsigned(std::max(1, ndevices))));
+}
+
 // Host threads that fill a pinned staging slot from pageable part memory (one task per part
 // slice).  DMA straight from pageable memory goes through the runtime's bounce buffer and
 // serialises with the host; staging keeps the copy engine fed from pinned memory.
@@ -606,8 +680,8 @@ struct HostCtx {
   hipError_t ensure_digests(int a, uint64_t bytes) {
     return grow_dev(reinterpret_cast<uint8_t**>(&d_dig[a]), &dig_bytes[a], bytes);
   }
-  CopyPool* ensure_pool(unsigned workers) {  // grows only; run() chooses how many take part
-    if (!pool || pool->size() < workers) pool.reset(new CopyPool(workers));
+  CopyPool* ensure_pool(unsigned workers) {  // exactly `workers` threads beside the caller
+    if (!pool || pool->size() != workers) pool.reset(new CopyPool(workers));
     return pool.get();
   }
   // plan[a] for algorithm `algo` with room for n parts (reallocated only to grow)
@@ -634,11 +708,16 @@ struct HostCtx {
     for (hipStream_t st : hash_s)
       if (st) (void)hipStreamSynchronize(st);
   }
-  void release_large() {  // after a call: do not keep a large HBM ring
+  void release_large() {  // after a call: do not keep a large HBM ring or staging ring
     if (ring_bytes > kKeepRingBytes) {
       (void)hipFree(ring);
       ring = nullptr;
       ring_bytes = 0;
+    }
+    if (stage_bytes > kHostRing * kFileStageSlot) {
+      (void)hipHostFree(stage);
+      stage = nullptr;
+      stage_bytes = 0;
     }
   }
   ~HostCtx() {
@@ -818,6 +897,7 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
   uint64_t max_blocks = 0;
   for (int a = 0; a < nalgo; ++a) {
     if (int rc = C.ensure_plan(a, algos[a], n)) return rc;
+    HIP_TRY(hipMemsetAsync(C.plan[a]->d_err, 0, sizeof(uint32_t), C.copy_s));  // before any launch
     HIP_TRY(C.ensure_digests(a, n * digest_words(algos[a]) * sizeof(uint32_t)));
     // geometry upload on the copy stream: every launch waits for a later copy on it
     if (int rc = plan_geometry(C.plan[a], offs.data(), lens.data(), n, S3H_KERNEL_AUTO,
@@ -826,10 +906,8 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
     max_blocks = std::max(max_blocks, C.plan[a]->max_blocks);
   }
   CopyPool* pool = nullptr;
-  if (staged) {
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    pool = C.ensure_pool(std::min(15u, std::max(2u, hw / unsigned(sh.ndevices)) - 1));
-  }
+  const unsigned threads = host_threads_per_device(sh.ndevices);  // the caller + workers
+  if (staged) pool = C.ensure_pool(threads - 1);
   const uint64_t bps = slice / 64;  // blocks per slice
   s3h_plan_s* P0 = C.plan[0];
   s3h_plan_s* P1 = nalgo == 2 ? C.plan[1] : nullptr;
@@ -904,6 +982,7 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
     hipError_t e = hipMemcpyAsync(local.data(), C.d_dig[a], n * dw * 4, hipMemcpyDeviceToHost, hs);
     if (e == hipSuccess) e = hipStreamSynchronize(hs);
     if (e != hipSuccess) { rc = fail(S3H_EHIP, "D2H digests: %s", hipGetErrorString(e)); break; }
+    if ((rc = plan_check(C.plan[a], hs)) != S3H_OK) break;  // every slice's launch reported in
     for (uint64_t j = 0; j < n; ++j)
       std::memcpy(digests[a] + dw * sh.parts[j], &local[dw * j], dw * 4);
   }
@@ -911,13 +990,33 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
   if (trace_host())
     std::fprintf(stderr,
                  "[s3h host] dev %d: %llu parts, slice %llu B, %s, %llu slices: setup %.2f ms, "
-                 "issue %.2f ms, drain %.2f ms\n",
+                 "issue %.2f ms, drain %.2f ms; copy threads %u (%u CPUs over %d devices)\n",
                  sh.device, (unsigned long long)n, (unsigned long long)slice,
                  !parts ? "staged (file pread)" : staged ? "staged (pageable)"
                  : direct_pageable ? "pageable per-part" : uniform ? "pinned 2-D" : "pinned per-part",
                  (unsigned long long)k, 1e3 * (t_setup - t_start), 1e3 * (t_issue - t_setup),
-                 1e3 * (wall_s() - t_issue));
+                 1e3 * (wall_s() - t_issue), staged ? threads : 0u, host_cpus(), sh.ndevices);
   return rc;
+}
+
+// File ranges and merged part references have no pageable-DMA fallback, and their staging
+// slot is n x slice bytes with slices of at least 64 B: a shard of more than
+// kMaxStagedRefs such parts runs in passes of that many, so the pinned staging ring never
+// exceeds kHostRing x kFileStageSlot (384 MiB).
+constexpr uint64_t kMaxStagedRefs = kFileStageSlot / 64;  // 2,097,152 parts
+
+int run_host_shard_passes(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
+                          const PartSource& src, const uint64_t* lengths, uint32_t* const* digests,
+                          uint64_t slice) {
+  if (src.parts || sh.parts.size() <= kMaxStagedRefs)
+    return run_host_shard(C, sh, algos, nalgo, src, lengths, digests, slice);
+  for (uint64_t s = 0; s < sh.parts.size(); s += kMaxStagedRefs) {
+    const uint64_t e = std::min<uint64_t>(sh.parts.size(), s + kMaxStagedRefs);
+    HostShard sub{sh.device, sh.ndevices,
+                  std::vector<uint64_t>(sh.parts.begin() + s, sh.parts.begin() + e)};
+    if (int rc = run_host_shard(C, sub, algos, nalgo, src, lengths, digests, slice)) return rc;
+  }
+  return S3H_OK;
 }
 
 // Re-sort a plan's slots for new lengths (same n) and upload them asynchronously from
@@ -1045,6 +1144,14 @@ int stream_update(s3h_stream_s* S, const uint8_t* base, const uint64_t* offsets,
   return S3H_OK;
 }
 
+// The error words of the stream's three plans (head / body / final launches), once `s` has
+// run everything before: plan_check.
+int stream_check(s3h_stream_s* S, hipStream_t s) {
+  for (s3h_plan_s* P : {S->head, S->body, S->fin})
+    if (int rc = plan_check(P, s)) return rc;
+  return S3H_OK;
+}
+
 int stream_final(s3h_stream_s* S, uint32_t* d_digests, hipStream_t s) {
   const uint64_t n = S->n;
   HIP_TRY(hipEventSynchronize(S->staged));
@@ -1121,7 +1228,7 @@ int run_merged(HostCtx* C, const std::vector<HostReq*>& batch) {
   const HostReq& f = *batch[0];
   int rc;
   if (batch.size() == 1) {
-    rc = run_host_shard(*C, *f.sh, f.algos, f.nalgo, *f.src, f.lengths, f.digests, f.slice);
+    rc = run_host_shard_passes(*C, *f.sh, f.algos, f.nalgo, *f.src, f.lengths, f.digests, f.slice);
   } else {
     uint64_t m = 0;
     bool mem = true;
@@ -1153,7 +1260,7 @@ int run_merged(HostCtx* C, const std::vector<HostReq*>& batch) {
       out[a].resize(m * digest_words(f.algos[a]));
       outp[a] = out[a].data();
     }
-    rc = run_host_shard(*C, sh, f.algos, f.nalgo, src, lens.data(), outp, f.slice);
+    rc = run_host_shard_passes(*C, sh, f.algos, f.nalgo, src, lens.data(), outp, f.slice);
     k = 0;
     for (const HostReq* r : batch) {
       for (uint64_t g : r->sh->parts) {
@@ -1168,9 +1275,8 @@ int run_merged(HostCtx* C, const std::vector<HostReq*>& batch) {
   return rc;
 }
 
-// Runs a batch and hands every request its status; nothing escapes, so the device queue's
-// leader always gets to mark the batch done.
-void run_batch(const std::vector<HostReq*>& batch) {
+// Runs a batch on the device's context; nothing escapes.
+int run_guarded(const std::vector<HostReq*>& batch, std::string* err) {
   HostCtx* C = nullptr;
   int rc;
   try {
@@ -1181,8 +1287,22 @@ void run_batch(const std::vector<HostReq*>& batch) {
   } catch (...) {
     rc = fail(S3H_EHIP, "host batch: unexpected exception");
   }
-  const std::string err = rc ? g_err : std::string();
+  *err = rc ? g_err : std::string();
   if (C) host_ctx_cache().release(C, rc == S3H_OK);
+  return rc;
+}
+
+// Runs a batch and hands every request its status, so the device queue's leader always gets
+// to mark the batch done.  A merged batch that fails is re-run one request at a time: one
+// caller's unreadable file range or allocation failure must not fail the other callers,
+// and each caller gets its own status and message.
+void run_batch(const std::vector<HostReq*>& batch) {
+  std::string err;
+  const int rc = run_guarded(batch, &err);
+  if (rc != S3H_OK && batch.size() > 1) {
+    for (HostReq* r : batch) r->rc = run_guarded({r}, &r->err);
+    return;
+  }
   for (HostReq* r : batch) {
     r->rc = rc;
     r->err = err;
@@ -1240,6 +1360,11 @@ int s3h_trim(void) {
   return S3H_OK;
 }
 
+int s3h_host_threads(int ndevices, int* cpus) {
+  if (cpus) *cpus = int(host_cpus());
+  return int(host_threads_per_device(ndevices));
+}
+
 int s3h_device_count(int* count) {
   if (!count) return fail(S3H_EINVAL, "null count");
   *count = 0;
@@ -1270,8 +1395,15 @@ int s3h_plan_destroy(s3h_plan_t P) {
   (void)hipFree(P->d_out_idx);
   (void)hipFree(P->d_state);
   (void)hipFree(P->d_zero);
+  (void)hipFree(P->d_err);
   delete P;
   return S3H_OK;
+}
+
+int s3h_plan_status(s3h_plan_t P, void* stream) {
+  if (!P) return fail(S3H_EINVAL, "null plan");
+  DeviceGuard g(P->device);
+  return plan_check(P, static_cast<hipStream_t>(stream));
 }
 
 int s3h_plan_launch(s3h_plan_t P, const void* d_base, uint32_t* d_digests, void* stream) {
@@ -1329,6 +1461,7 @@ static int batch_device(int device, int algo, const void* d_base, const uint64_t
     DeviceGuard g(device);
     hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
     if (e != hipSuccess) rc = fail(S3H_EHIP, "batch_device sync: %s", hipGetErrorString(e));
+    else rc = plan_check(P, static_cast<hipStream_t>(stream));
   }
   s3h_plan_destroy(P);
   return rc;
@@ -1526,7 +1659,7 @@ int s3h_sha256_md5_batch_device(int device, const void* d_base, const uint64_t* 
                              main_s))
       return rc;
     HIP_TRY(hipStreamSynchronize(main_s));
-    return S3H_OK;
+    return plan_check(P[0], main_s);  // the one grid reports into S's word
   }
   // Otherwise MD5 runs on a side stream forked from and joined back into the caller's: the two
   // kernels occupy different CUs, so both digests take about the SHA-256 time.
@@ -1540,7 +1673,8 @@ int s3h_sha256_md5_batch_device(int device, const void* d_base, const uint64_t* 
   HIP_TRY(hipEventRecord(C.ev[1], C.side));
   HIP_TRY(hipStreamWaitEvent(main_s, C.ev[1], 0));
   HIP_TRY(hipStreamSynchronize(main_s));
-  return S3H_OK;
+  if (int rc = plan_check(P[0], main_s)) return rc;
+  return plan_check(P[1], main_s);
 }
 
 int s3h_verify_batch_device(int device, int algo, const void* d_base, const uint64_t* offsets,
@@ -1570,6 +1704,7 @@ int s3h_verify_batch_device(int device, int algo, const void* d_base, const uint
     if (e == hipSuccess) e = hipMemcpyAsync(&c, d_count, 8, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) rc = fail(S3H_EHIP, "verify: %s", hipGetErrorString(e));
+    else rc = plan_check(P, s);  // a faulted launch verifies nothing
     *mismatches = c;
   }
   (void)hipFreeAsync(d_dig, s);
@@ -1720,6 +1855,7 @@ int s3h_stream_update_host(s3h_stream_t S, const uint8_t* const* chunks, const u
   int rc = stream_update(S, S->d_stage, offs.data(), lengths, S->own);
   hipError_t e = hipStreamSynchronize(S->own);  // chunks may be released on return
   if (!rc && e != hipSuccess) rc = fail(S3H_EHIP, "stream update: %s", hipGetErrorString(e));
+  if (!rc) rc = stream_check(S, S->own);
   return rc;
 }
 
@@ -1732,7 +1868,13 @@ int s3h_stream_final_host(s3h_stream_t S, uint32_t* digests) {
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(digests, S->d_dig, bytes, hipMemcpyDeviceToHost, S->own));
   HIP_TRY(hipStreamSynchronize(S->own));
-  return S3H_OK;
+  return stream_check(S, S->own);
+}
+
+int s3h_stream_status(s3h_stream_t S, void* stream) {
+  if (!S) return fail(S3H_EINVAL, "stream status: null stream");
+  DeviceGuard g(S->device);
+  return stream_check(S, static_cast<hipStream_t>(stream));
 }
 
 int s3h_stream_total(s3h_stream_t S, uint64_t i, uint64_t* total) {

@@ -44,6 +44,17 @@
 #ifndef S3H_EXP_MD5_SELF_DEPTH
 #define S3H_EXP_MD5_SELF_DEPTH 4  // self-fed MD5: blocks fetched ahead
 #endif
+#ifndef S3H_EXP_MD5_C_STEPS
+#define S3H_EXP_MD5_C_STEPS 0  // 1: the MD5 consumer's steps as compiled C (round-2 form)
+#endif
+#ifndef S3H_EXP_SPIN_LIMIT
+#define S3H_EXP_SPIN_LIMIT (1u << 24)  // flag waits: s_sleep 1 polls before a wait times out
+#endif
+#ifndef S3H_EXP_STALL_PRODUCER
+// 1: flag-synchronised producers stop publishing after their first step, so every consumer
+// wait times out (the forced-fault build `make stall`, tests/test_gpu_errors.py)
+#define S3H_EXP_STALL_PRODUCER 0
+#endif
 #if S3H_EXP_PRODUCER_ROLLED
 #define S3H_PROD_UNROLL _Pragma("unroll 1")
 #else
@@ -55,6 +66,11 @@ namespace s3h {
 // LaunchArgs::flags
 constexpr uint32_t kNoPad = 1;   // hash only the slot's whole 64-B blocks; never pad or emit
 constexpr uint32_t kResume = 2;  // load the chaining state even at blk_begin == 0
+
+// Bits of the device error word (LaunchArgs::err).  Every host entry point reads the word
+// after its launches complete and fails the call when it is non-zero (capi.hip plan_check):
+// a launch whose digests may be wrong never returns S3H_OK.
+constexpr uint32_t kErrSyncTimeout = 1;  // a producer/consumer flag wait timed out
 
 struct LaunchArgs {
   const uint8_t* base;       // part p's block b is at base + slots[p].off + 64*(b - blk_origin)
@@ -73,6 +89,8 @@ struct LaunchArgs {
   // sha256_skew_pairs_kernel: the first `solo` workgroups run one group each (the longest
   // parts, on a CU of their own), the rest two.  0 elsewhere.
   uint32_t solo;
+  // Device error word of the plan (kErr* bits OR-ed in by global atomics; cleared by the host).
+  uint32_t* err;
 };
 
 // Compressions the launch sequence runs for a slot of `len` bytes.
@@ -684,7 +702,8 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_quad_kernel(LaunchArgs A
 //                  workgroup scope), so several independent groups -- or a SHA-256 group and
 //                  an MD5 group -- share one workgroup without stalling on each other's
 //                  barriers (NC = 1 in this mode).  Every wait is bounded (kFlagSpinLimit), so
-//                  a wave can never hang on a counter.
+//                  a wave can never hang on a counter, and a wait that times out sets the
+//                  launch's error word, which fails the host call (flag_wait_ge).
 // `group` numbers the group's parts (slots group*kParts...), `role` is the wave's job in it:
 // consumer index 0..NC-1, or NC for the producer.
 template <int NC, bool PAIR>
@@ -709,19 +728,22 @@ struct SkewLds {
   uint4 wk[2][SkewGeom<NC, PAIR>::kBps][SkewGeom<NC, PAIR>::kBlkStride];
 };
 
-constexpr uint32_t kFlagSpinLimit = 1u << 24;  // x s_sleep 1 (64 clocks): ~0.45 s
+constexpr uint32_t kFlagSpinLimit = S3H_EXP_SPIN_LIMIT;  // x s_sleep 1 (64 clocks): ~0.45 s
 __device__ __forceinline__ void flag_publish(uint32_t* f, uint32_t v) {
   __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// Wait for *f >= v.  `alive` (wave-uniform) turns false after one timed-out wait and every
-// later wait of the wave returns at once: a synchronisation fault costs one timeout per wave
-// (wrong digests, caught by every parity test) instead of a hung GPU.
-__device__ __forceinline__ void flag_wait_ge(uint32_t* f, uint32_t v, bool& alive) {
+// Wait for *f >= v.  A wait that times out ORs kErrSyncTimeout into the launch's device error
+// word (a global vector atomic), and `alive` (wave-uniform) turns false so every later wait of
+// the wave returns at once: the grid always drains -- one timeout per wave, never a hung GPU
+// -- and the host entry point that reads the word fails the call (S3H_EHIP) instead of
+// returning the launch's now meaningless digests.
+__device__ __forceinline__ void flag_wait_ge(uint32_t* f, uint32_t v, bool& alive, uint32_t* err) {
   if (!alive) return;
   uint32_t spin = 0;
   while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) {
     if (++spin >= kFlagSpinLimit) {
       alive = false;
+      __hip_atomic_fetch_or(err, kErrSyncTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -813,10 +835,13 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
   auto rows = [&](uint32_t b, uint32_t h) { return reinterpret_cast<uint4 (*)[kCols]>(lds_wk[b][h]); };
   bool alive = true;  // FLAGS: false after a timed-out wait (flag_wait_ge)
   // FLAGS: flags[0] = producer steps published, flags[1] = consumer steps released
-#define S3H_SYNC_PRODUCED(m)                 \
-  do {                                       \
-    if constexpr (FLAGS) flag_publish(&flags[0], (m)); \
-    else __syncthreads();                    \
+#define S3H_SYNC_PRODUCED(m)                                                  \
+  do {                                                                        \
+    if constexpr (FLAGS) {                                                    \
+      if (!S3H_EXP_STALL_PRODUCER || (m) <= 1u) flag_publish(&flags[0], (m)); \
+    } else {                                                                  \
+      __syncthreads();                                                        \
+    }                                                                         \
   } while (0)
 
   const uint32_t lane = threadIdx.x & 63u;
@@ -877,7 +902,7 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
     for (uint64_t k = 1; k <= steps; k += 2) {
       if (k < steps) {
         if constexpr (FLAGS) {
-          if (k >= 2) flag_wait_ge(&flags[1], uint32_t(k - 1), alive);
+          if (k >= 2) flag_wait_ge(&flags[1], uint32_t(k - 1), alive, A.err);
         }
         S3H_PROD_UNROLL
         for (uint32_t r = 0; r < kItems; ++r) {
@@ -888,7 +913,7 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
       S3H_SYNC_PRODUCED(uint32_t(k + 1));
       if (k + 1 > steps) break;
       if (k + 1 < steps) {
-        if constexpr (FLAGS) flag_wait_ge(&flags[1], uint32_t(k), alive);
+        if constexpr (FLAGS) flag_wait_ge(&flags[1], uint32_t(k), alive, A.err);
         S3H_PROD_UNROLL
         for (uint32_t r = 0; r < kItems; ++r) {
           fetch_full(p[r] + kStride * (k + 2), bh[r] + kBps * (k + 2) < fend[r], A.zero, rb[r]);
@@ -976,7 +1001,7 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
   do {                                                         \
     if constexpr (FLAGS) {                                     \
       flag_publish(&flags[1], (released));                     \
-      if ((needed) != 0u) flag_wait_ge(&flags[0], (needed), alive);   \
+      if ((needed) != 0u) flag_wait_ge(&flags[0], (needed), alive, A.err); \
     } else {                                                   \
       __syncthreads();                                         \
     }                                                          \
@@ -1257,6 +1282,45 @@ __device__ __forceinline__ void md5_steps(uint32_t& a, uint32_t& b, uint32_t& c,
   }
 }
 
+// The same 64 steps as four asm statements of 16 steps, every instruction 8 bytes (v_add_u32
+// in its VOP3 encoding) and each statement 8-byte aligned.  Compiled C mixes the 4-byte VOP2
+// add into the 8-byte bitop3 / add3 / alignbit stream, so half the 8-byte instructions sit at
+// an address = 4 (mod 8), where a lone wave issues them in ~5 instead of ~4 cycles
+// (profiles/r01_ubench_alignment.txt) -- the standalone MD5 consumer ran 1,370 cycles per
+// block for ~280 instructions.  Step: f = F(b,c,d) (one bitop3), t = a + f + (M+K),
+// t = rotl(t, s) (alignbit by 32 - s), a = b + t; the names rotate (a,b,c,d) -> (d,a,b,c).
+#define S3H_MD5_ST(TT, A, B, C, D, K, R)                                                 \
+  "v_bitop3_b32 %[f], %[" #B "], %[" #C "], %[" #D "] bitop3:" #TT "\n\t"               \
+  "v_add3_u32 %[t], %[" #A "], %[f], %[" #K "]\n\t"                                     \
+  "v_alignbit_b32 %[t], %[t], %[t], " #R "\n\t"                                         \
+  "v_add_u32_e64 %[" #A "], %[" #B "], %[t]\n\t"
+#define S3H_MD5_4(TT, K0, K1, K2, K3, R0, R1, R2, R3)                                    \
+  S3H_MD5_ST(TT, a, b, c, d, K0, R0) S3H_MD5_ST(TT, d, a, b, c, K1, R1)                   \
+  S3H_MD5_ST(TT, c, d, a, b, K2, R2) S3H_MD5_ST(TT, b, c, d, a, K3, R3)
+// 16 steps of one round: truth table TT, rotations (as alignbit amounts 32 - s) R0..R3
+#define S3H_MD5_16(TT, R0, R1, R2, R3)                                                   \
+  S3H_MD5_4(TT, k0, k1, k2, k3, R0, R1, R2, R3) S3H_MD5_4(TT, k4, k5, k6, k7, R0, R1, R2, R3) \
+  S3H_MD5_4(TT, k8, k9, k10, k11, R0, R1, R2, R3) S3H_MD5_4(TT, k12, k13, k14, k15, R0, R1, R2, R3)
+#define S3H_MD5_ROUND(Q, TT, R0, R1, R2, R3)                                              \
+  asm volatile(S3H_ALIGN8 S3H_MD5_16(TT, R0, R1, R2, R3)                                  \
+               : [a] "+v"(a), [b] "+v"(b), [c] "+v"(c), [d] "+v"(d), [f] "=&v"(f), [t] "=&v"(t) \
+               : [k0] "v"(km[16 * Q]), [k1] "v"(km[16 * Q + 1]), [k2] "v"(km[16 * Q + 2]),   \
+                 [k3] "v"(km[16 * Q + 3]), [k4] "v"(km[16 * Q + 4]), [k5] "v"(km[16 * Q + 5]), \
+                 [k6] "v"(km[16 * Q + 6]), [k7] "v"(km[16 * Q + 7]), [k8] "v"(km[16 * Q + 8]), \
+                 [k9] "v"(km[16 * Q + 9]), [k10] "v"(km[16 * Q + 10]),                       \
+                 [k11] "v"(km[16 * Q + 11]), [k12] "v"(km[16 * Q + 12]),                     \
+                 [k13] "v"(km[16 * Q + 13]), [k14] "v"(km[16 * Q + 14]),                     \
+                 [k15] "v"(km[16 * Q + 15]))
+
+__device__ __forceinline__ void md5_steps_asm(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d,
+                                              const uint32_t km[64]) {
+  uint32_t f, t;
+  S3H_MD5_ROUND(0, 0xca, 25, 20, 15, 10);  // F = b ? c : d;       s = 7, 12, 17, 22
+  S3H_MD5_ROUND(1, 0xe4, 27, 23, 18, 12);  // G = d ? b : c;       s = 5, 9, 14, 20
+  S3H_MD5_ROUND(2, 0x96, 28, 21, 16, 9);   // H = b ^ c ^ d;       s = 4, 11, 16, 23
+  S3H_MD5_ROUND(3, 0x39, 26, 22, 17, 11);  // I = c ^ (b | ~d);    s = 6, 10, 15, 21
+}
+
 // Decoded message words of MD5 block `blk` (zeros past the launch's range, padding at the end).
 __device__ __forceinline__ void md5_decode(const RawBlock& r, uint32_t sel, const uint8_t* bp,
                                            uint64_t len, uint64_t bits, uint64_t blk,
@@ -1437,7 +1501,11 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
         km[4 * q] = v.x; km[4 * q + 1] = v.y; km[4 * q + 2] = v.z; km[4 * q + 3] = v.w;
       }
       uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+#if S3H_EXP_MD5_C_STEPS
       md5_steps<0>(a, b, c, d, km);
+#else
+      md5_steps_asm(a, b, c, d, km);
+#endif
       const bool live = (A.blk_begin + i) < nb;
       st[0] = live ? st[0] + a : st[0];
       st[1] = live ? st[1] + b : st[1];

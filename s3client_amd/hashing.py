@@ -115,6 +115,12 @@ class Plan:
                                     ctypes.c_void_p(digests.data_ptr()),
                                     ctypes.c_void_p(_stream_handle(stream))))
 
+    def status(self, stream=None) -> None:
+        """Wait for ``stream`` and raise S3HashError (S3H_EHIP, "synchronisation timeout") if a
+        launch since the last check reported a fault through the plan's device error word --
+        its digests are then invalid (s3h_plan_status).  Clears the word."""
+        check(lib().s3h_plan_status(self._h, ctypes.c_void_p(_stream_handle(stream))))
+
     def launch_range(self, data_ptr: int, digests, blk_begin: int, blk_end: int,
                      blk_origin: int, stream=None) -> None:
         check(lib().s3h_plan_launch_range(self._h, ctypes.c_void_p(data_ptr),
@@ -151,7 +157,7 @@ def sha256_batch_device(data, offsets, lengths, device: int | None = None, kerne
     with Plan(offsets, lengths, device=dev, kernel=kernel, algo=algo) as plan:
         out = torch.empty((plan.n, plan.words), dtype=torch.int32, device=data.device)
         plan.launch(data, out, stream)
-        torch.cuda.current_stream(data.device).synchronize() if stream is None else stream.synchronize()
+        plan.status(stream)  # waits for the launch; raises if it reported a fault
     return out
 
 
@@ -308,6 +314,11 @@ class Stream:
         check(lib().s3h_stream_final_device(self._h, ctypes.c_void_p(digests.data_ptr()),
                                             ctypes.c_void_p(_stream_handle(stream))))
 
+    def status(self, stream=None) -> None:
+        """Wait for ``stream``; raise if an update/final launch reported a fault
+        (s3h_stream_status).  The host forms check by themselves."""
+        check(lib().s3h_stream_status(self._h, ctypes.c_void_p(_stream_handle(stream))))
+
     def total(self, i: int) -> int:
         t = ctypes.c_uint64()
         check(lib().s3h_stream_total(self._h, i, ctypes.byref(t)))
@@ -374,6 +385,14 @@ def sha256_md5_file_parts(path: str, offsets, lengths, ndevices: int = 0,
     check(lib().s3h_sha256_md5_file_parts(os.fsencode(path), _p64(offs), _p64(lens), offs.size,
                                           sha.ctypes.data, m5.ctypes.data, ndevices, slice_bytes))
     return sha, m5
+
+
+def host_threads(ndevices: int = 1) -> tuple[int, int]:
+    """(staging threads per device when ``ndevices`` device shards run at once, CPUs this
+    process may use: affinity capped by the cgroup quota) -- s3h_host_threads."""
+    cpus = ctypes.c_int(0)
+    per = lib().s3h_host_threads(ndevices, ctypes.byref(cpus))
+    return per, cpus.value
 
 
 def trim() -> None:

@@ -127,6 +127,24 @@ def main():
     out["c4_parts"] = [{"p": p, "L": 8 << 20, "digest": ref_digest(ref, gen(orc, p, 8 << 20))}
                        for p in (8, 16, 4096, 32768, 65520, 65528)]
 
+    # 4c. Every rank's shard at N = 2, 4, 8 GPUs (global part p -> rank p % N, slot p // N;
+    #     s3client_amd/shard.py): the C2 weak-scaling job (1,024 parts per GPU, ids < 1024 N)
+    #     and C4 (8,192 per GPU, ids < 8192 N; N = 8 is BASELINE configs[3]).  Four slots per
+    #     rank -- first, an odd one, the middle and the last -- so every rank of a multi-GPU run
+    #     checks its own digests against lib/hash, not only the fixtures that happen to fall in
+    #     its residue class.
+    shards, seen = [], {}
+    for cfg, per in (("c2", 1024), ("c4", 8192)):
+        for N in (2, 4, 8):
+            for r in range(N):
+                for slot in (0, per // 4 + 1, per // 2, per - 1):
+                    p = slot * N + r
+                    if p not in seen:
+                        seen[p] = ref_digest(ref, gen(orc, p, L8))
+                    shards.append({"cfg": cfg, "N": N, "rank": r, "slot": slot, "p": p, "L": L8,
+                                   "digest": seen[p]})
+    out["shard_parts"] = shards
+
     # 5. test/parallel-file-transfer-test.cpp:50-59 data (i % 128, 38000007 B), parts sliced
     #    with lib/src/upload.cpp:98-107 geometry (3 jobs x 2 parts)
     size = 38000007

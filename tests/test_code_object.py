@@ -1,0 +1,100 @@
+"""The gfx950 code object libs3hash.so ships (CPU only: read from the library file).
+
+* Every flag-synchronised kernel (two-group skew, shared-SIMD skew, both dual-digest group
+  kernels) contains the global atomic OR with which a timed-out producer/consumer wait reports
+  into the device error word (sha256_kernels.hip flag_wait_ge) -- so the host entry points
+  that read the word can fail the call instead of returning wrong digests.  The forced-fault
+  library (tests/cpp/build/libs3hash_stall.so) is exercised on the GPU by test_gpu_errors.py.
+* s3client_amd/kernel_isa_counts.json (bench.py's instruction counts and the code hashes that
+  key profiles/*_pmc.json) describes THIS library's code object.
+* Host staging threads follow the CPUs the process may use (s3h_host_threads).
+"""
+import json
+import math
+import os
+import sys
+
+import pytest
+
+from s3client_amd import _native
+import s3client_amd as s3
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import code_object  # noqa: E402
+import isa_counts  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def shipped():
+    return code_object.disassemble(_native.LIB_PATH)
+
+
+def _atomics(lines, sym):
+    return sum(bool(isa_counts.ERR_STORE.match(l)) for l in code_object.function_body(lines, sym))
+
+
+@pytest.mark.parametrize("kernel", isa_counts.FLAG_KERNELS)
+def test_flag_kernels_store_the_error_word(shipped, kernel):
+    assert _atomics(shipped, isa_counts.ALL_KERNELS[kernel]) >= 1, kernel
+
+
+def test_barrier_kernels_have_no_error_store(shipped):
+    # kernels synchronised by s_barrier cannot time out: nothing to report
+    for k in ("skew", "skewp", "pc", "lane", "md5-pc"):
+        assert _atomics(shipped, isa_counts.ALL_KERNELS[k]) == 0, k
+
+
+def test_isa_counts_describe_the_shipped_library(shipped):
+    with open(os.path.join(ROOT, "s3client_amd", "kernel_isa_counts.json")) as f:
+        counts = json.load(f)
+    for k, sym in isa_counts.ALL_KERNELS.items():
+        assert counts["code_hash"][k] == code_object.code_hash(shipped, sym), k
+    for k in isa_counts.FLAG_KERNELS:
+        assert counts["error_word_atomics"][k] >= 1
+    # the skew consumer's fast loop: the round stream plus LDS reads, nothing of the cold
+    # error-report span (tools/isa_counts.py loops())
+    assert 540 < counts["kernels"]["skew"]["instr_per_block"] < 550
+    assert 540 < counts["kernels"]["skews"]["instr_per_block"] < 550
+
+
+def test_code_hash_ignores_label_numbering():
+    a = ["\ts_branch L7   // 0: 00", "0000000000000010 <L7>:", "\tv_add_u32_e32 v1, v2, v3   // 10: 00"]
+    b = ["\ts_branch L9   // 8: 11", "0000000000000018 <L9>:", "\tv_add_u32_e32 v1, v2, v3   // 18: 11"]
+    assert code_object.instructions(a) == code_object.instructions(b)
+
+
+def _expected_cpus():
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            quota = q / per if q > 0 else None
+        except (OSError, ValueError):
+            pass
+    return min(n, max(1, math.ceil(quota))) if quota else n
+
+
+def test_host_threads_follow_affinity_and_quota():
+    cpus = _expected_cpus()
+    for nd in (1, 2, 3, 8, 64):
+        per, got = s3.host_threads(nd)
+        assert got == cpus
+        assert per == min(16, max(1, cpus // nd))
+        assert per * nd <= max(cpus, nd)  # never more threads than CPUs (1 per device minimum)
+
+
+def test_host_threads_respect_a_narrowed_affinity():
+    # a child process pinned to 2 CPUs must see 2 (or fewer under a smaller quota)
+    import subprocess
+    code = ("import os,sys;os.sched_setaffinity(0,sorted(os.sched_getaffinity(0))[:2]);"
+            "sys.path.insert(0,'.');import s3client_amd as s;print(*s.host_threads(1))")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=ROOT)
+    assert r.returncode == 0, r.stderr
+    per, cpus = map(int, r.stdout.split())
+    assert cpus == min(2, _expected_cpus()) and per == cpus

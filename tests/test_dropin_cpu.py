@@ -105,12 +105,9 @@ def test_kernel_isa_counts_match_the_built_code_object(tmp_path):
     must be what tools/isa_counts.py derives from the code object `make` just built."""
     import json
     import subprocess
-    dis = os.path.join(ROOT, "build", "isa", "capi_gfx950.dis")
-    if not os.path.exists(dis):
-        pytest.skip("build/isa not present (run make)")
     out = tmp_path / "counts.json"
-    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_counts.py"), dis, str(out)],
-                   check=True, capture_output=True)
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_counts.py"), _native.LIB_PATH,
+                    str(out)], check=True, capture_output=True)
     with open(out) as f:
         fresh = json.load(f)
     with open(os.path.join(ROOT, "s3client_amd", "kernel_isa_counts.json")) as f:

@@ -98,6 +98,48 @@ def test_c4_rank0_shard(torch_cuda, oracle, golden):
         _release(torch)
 
 
+@pytest.mark.parametrize("cfg,world,rank", [("c4", 8, 7), ("c2", 4, 3), ("c4", 2, 1), ("c2", 8, 6)])
+def test_other_rank_shards(torch_cuda, oracle, golden, cfg, world, rank):
+    """The shard a rank other than 0 hashes in a multi-GPU run (bench.py, one process per GPU,
+    global part p on rank p % N): BASELINE configs[3]'s rank 7 of 8, the C2 weak-scaling job's
+    rank 3 of 4, and two more -- run here on the one GPU, checked against that rank's own
+    lib/hash fixtures (gen_golden.py 4c: four slots per rank, plus any other fixture whose id
+    falls in the shard) and the oracle on 64 random parts."""
+    torch = torch_cuda
+    from s3client_amd.shard import shard_ids
+    per = 8192 if cfg == "c4" else 1024
+    ids = shard_ids(per * world, rank, world)
+    L = 8 * MIB
+    lens = np.full(per, L, dtype=np.uint64)
+    offs = np.arange(per, dtype=np.uint64) * np.uint64(L)
+    data = torch.empty(per * L, dtype=torch.uint8, device="cuda")
+    try:
+        s3.generate_parts(data, offs, lens, ids, SEED)
+        with s3.Plan(offs, lens) as plan:
+            assert plan.info()["kernel"] == ("skews" if cfg == "c4" else "skew")
+            out = torch.empty((per, 8), dtype=torch.int32, device="cuda")
+            plan.launch(data, out)
+            plan.status()  # device error word clear
+        got = out.cpu().numpy().view(np.uint32)
+        txt = s3.digests_to_text(got)
+        own = [e for e in golden["shard_parts"]
+               if e["cfg"] == cfg and e["N"] == world and e["rank"] == rank]
+        assert len(own) == 4
+        for e in own:
+            assert int(ids[e["slot"]]) == e["p"] and txt[e["slot"]] == e["digest"], e
+        slot_of = {int(p): k for k, p in enumerate(ids)}
+        extra = [e for e in golden["c2_parts"] + golden["c4_parts"] + golden["shard_parts"]
+                 if e["p"] in slot_of]
+        for e in extra:
+            assert txt[slot_of[e["p"]]] == e["digest"], e["p"]
+        rng = np.random.default_rng(1000 * world + rank)
+        slots = np.sort(rng.choice(per, 64, replace=False))
+        assert np.array_equal(got[slots], _oracle_sample(torch, oracle, data, offs, lens, slots))
+    finally:
+        del data
+        _release(torch)
+
+
 def _ragged_top(rng, n, top, top_len, rest_len):
     lens = rng.integers(*rest_len, n)
     lens[:top] = rng.integers(*top_len, top)

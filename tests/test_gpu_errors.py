@@ -1,0 +1,54 @@
+"""A launch that faults must fail its call, never return wrong digests (the reference's
+sha256::sha256, lib/hash/sha256.cpp:147-160, always returns the message's digest).
+
+The flag-synchronised kernels (two-group skew, shared-SIMD skew, dual-digest group kernels)
+bound every producer/consumer wait; a wait that times out ORs kErrSyncTimeout into the plan's
+device error word (sha256_kernels.hip flag_wait_ge) and every host entry point reads the word
+(capi.hip plan_check).  tests/cpp/build/libs3hash_stall.so (Makefile `STALL`) is the product
+source built with producers that stop publishing after their first step: every consumer wait
+times out, and every entry point must report S3H_EHIP.  The same probe against the product
+library must succeed with the oracle's digests.  Each library runs in its own child process
+(S3H_LIBRARY is read when s3client_amd is imported)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STALL = os.path.join(ROOT, "tests", "cpp", "build", "libs3hash_stall.so")
+PROBE = os.path.join(ROOT, "tests", "gpu_stall_probe.py")
+S3H_EHIP = -3
+
+
+def _probe(lib=None):
+    env = dict(os.environ)
+    env.pop("S3H_LIBRARY", None)
+    if lib:
+        env["S3H_LIBRARY"] = lib
+    r = subprocess.run([sys.executable, PROBE], capture_output=True, text=True, env=env,
+                       cwd=ROOT, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.gpu
+def test_forced_stall_fails_every_entry_point():
+    assert os.path.exists(STALL), "build the forced-fault library first: make"
+    res = _probe(STALL)
+    assert res.pop("library").endswith("libs3hash_stall.so")
+    assert res.pop("control_1000_parts") == 0  # barrier kernels are unaffected
+    assert len(res) == 16, sorted(res)
+    for name, out in res.items():
+        assert out != 0, f"{name}: succeeded although every consumer wait timed out"
+        assert isinstance(out, list), f"{name}: {out}"
+        code, msg = out
+        assert code == S3H_EHIP and "synchronisation timeout" in msg, (name, msg)
+
+
+@pytest.mark.gpu
+def test_product_library_passes_the_same_probe():
+    res = _probe()
+    assert res.pop("library").endswith(os.path.join("lib", "libs3hash.so"))
+    assert all(v == 0 for v in res.values()), {k: v for k, v in res.items() if v != 0}

@@ -36,6 +36,29 @@ def test_generator_matches_c2_fixtures(oracle, golden):
         assert oracle.hex(oracle.generate(e["p"], e["L"])) == e["digest"], e["p"]
 
 
+def test_shard_fixtures(oracle, golden):
+    """Every rank's shard fixtures at N = 2, 4, 8 (gen_golden.py 4c): p = slot * N + rank, four
+    slots per rank, both the C2 weak-scaling job and C4; the oracle agrees on all of them."""
+    from s3client_amd.shard import shard_ids
+    sh = golden["shard_parts"]
+    for cfg, per in (("c2", 1024), ("c4", 8192)):
+        for N in (2, 4, 8):
+            for r in range(N):
+                mine = [e for e in sh if e["cfg"] == cfg and e["N"] == N and e["rank"] == r]
+                assert len(mine) == 4, (cfg, N, r)
+                ids = shard_ids(per * N, r, N)
+                for e in mine:
+                    assert int(ids[e["slot"]]) == e["p"] and e["p"] % N == r
+    distinct = {e["p"]: e["digest"] for e in sh}
+    blob = np.zeros((len(distinct), 8 << 20), dtype=np.uint8)
+    for k, p in enumerate(distinct):
+        blob[k] = np.frombuffer(oracle.generate(p, 8 << 20), dtype=np.uint8)
+    got = oracle.batch(blob.reshape(-1), np.arange(len(distinct)) * (8 << 20),
+                       np.full(len(distinct), 8 << 20))
+    for k, (p, want) in enumerate(distinct.items()):
+        assert got[k].tobytes().hex() == want, p
+
+
 def test_c3_lengths(oracle, golden):
     assert [oracle.c3_length(p) for p in range(64)] == golden["c3_lengths"]
     assert golden["c3_lengths"][:4] == [52996377, 9123323, 20283550, 58275873]  # SURVEY 8(d)

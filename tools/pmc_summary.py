@@ -2,7 +2,12 @@
 """Summarise rocprofv3 --pmc passes for the SHA-256 kernels into profiles/<name>.json.
 
     python tools/pmc_summary.py --fetch DIR --write DIR [--sq DIR] --kernel-stats CSV \
-        --bytes-per-launch B --out profiles/r01_c2_pmc.json
+        --bytes-per-launch B --bench-jsonl LINE --kernel-key skew --out profiles/r03_c2_skew_pmc.json
+
+Provenance: the summary records the kernel's code hash and the library sha256 that the
+profiled bench run loaded (its JSON line's `library` object, --bench-jsonl) and the git commit
+it was summarised at; bench.py uses a profile's traffic only for a build whose kernel code
+hash is the same (pmc_traffic).
 
 HBM traffic follows MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE (KiB) come from
 separate passes; on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced read, so
@@ -38,6 +43,9 @@ def main():
     ap.add_argument("--kernel-stats")
     ap.add_argument("--bytes-per-launch", type=float, required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--bench-jsonl", required=True,
+                    help="the profiled bench.py run's output (its `library` object)")
+    ap.add_argument("--kernel-key", required=True, help="tools/isa_counts.py ALL_KERNELS key")
     a = ap.parse_args()
     fetch = mean(per_dispatch(a.fetch, a.kernel), "FETCH_SIZE")
     write = mean(per_dispatch(a.write, a.kernel), "WRITE_SIZE")
@@ -49,6 +57,17 @@ def main():
            "algorithmic_bytes_per_launch": a.bytes_per_launch,
            "traffic_over_algorithmic": (read_bytes + write_bytes) / a.bytes_per_launch,
            "correction": "FETCH_SIZE x2 (gfx950 reports half of a 16-B/lane streaming read)"}
+    import subprocess
+    line = json.loads(open(a.bench_jsonl).read().strip().splitlines()[-1])
+    lib = line["library"]
+    out["kernel_key"] = a.kernel_key
+    out["kernel_code_hash"] = lib["kernel_code_hash"][a.kernel_key]
+    out["library_sha256"] = lib["sha256"]
+    out["library_path"] = lib["path"]
+    head = subprocess.run(["git", "rev-parse", "HEAD"], capture_output=True, text=True).stdout.strip()
+    dirty = subprocess.run(["git", "status", "--porcelain", "--untracked-files=no"],
+                           capture_output=True, text=True).stdout.strip()
+    out["git_head"] = head + ("+uncommitted" if dirty else "")
     if a.sq:
         sq = per_dispatch(a.sq, a.kernel)
         for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_WAVE_CYCLES",
