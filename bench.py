@@ -159,11 +159,11 @@ def pmc_traffic(cfg: str, kname: str, key: str, code_hash, algo_bytes: float):
         f"commit {str(s.get('git_head'))[:12]})")
 
 
-def clock_probe(torch, plan, info, data, digests, stream, dev):
+def clock_probe(torch, plan, info, data, digests, stream, dev, kname=None):
     """One extra launch (outside any timed region) on which every consumer wave of a skew /
-    skewp / skews plan records s_memtime and s_memrealtime around its chain loop -> the live
-    shader clock and cycles per block; None for kernels without the probe."""
-    if info["kernel"] not in ("skew", "skewp", "skews"):
+    skewp / skews / MD5 plan records s_memtime and s_memrealtime around its chain loop -> the
+    live shader clock and cycles per block; None for kernels without the probe."""
+    if (kname or info["kernel"]) not in ("skew", "skewp", "skews", "md5-pc"):
         return None
     clocks = torch.zeros(4 * 4 * max(info["grid"], info["groups"]), dtype=torch.int64, device=dev)
     waves = plan.set_clock_probe(clocks)
@@ -347,7 +347,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)  # max over ranks: the slowest GPU sets the time
     wall, kern_ms_max = float(t[0]), float(t[1])
 
-    probe = clock_probe(torch, plan, info, data, digests, stream, dev)
+    probe = clock_probe(torch, plan, info, data, digests, stream, dev, kname)
 
     # parity of the last timed step's digests against the reference fixtures, on EVERY rank
     # (tests/golden: C2/C4 parts and four parts of each rank's shard at N = 2, 4, 8)

@@ -1421,6 +1421,7 @@ int s3h_plan_launch_range(s3h_plan_t P, const void* d_base, uint32_t* d_digests,
 
 // Consumer waves (= groups) of a skew/skewp grid; 0 for the kernels without a clock probe.
 static uint32_t consumer_groups(const s3h_plan_s* P) {
+  if (P->algo == S3H_ALGO_MD5) return P->grid;  // md5_pc_kernel: one consumer wave per workgroup
   return (P->kernel == S3H_KERNEL_SKEW && P->quad_waves == 2) || P->kernel == S3H_KERNEL_SKEWS
              ? uint32_t((P->n + 7) / 8)
          : P->kernel == S3H_KERNEL_SKEW || P->kernel == S3H_KERNEL_SKEWP ? P->grid

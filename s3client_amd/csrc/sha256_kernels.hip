@@ -1312,10 +1312,34 @@ __device__ __forceinline__ void md5_steps(uint32_t& a, uint32_t& b, uint32_t& c,
                  [k13] "v"(km[16 * Q + 13]), [k14] "v"(km[16 * Q + 14]),                     \
                  [k15] "v"(km[16 * Q + 15]))
 
-__device__ __forceinline__ void md5_steps_asm(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d,
+// The first four steps read the block-start state s0..s3 and write fresh registers a..d, so
+// the state survives for the feed-forward without four register copies.
+#define S3H_MD5_ST_IO(TT, AIN, AOUT, B, C, D, K, R)                                      \
+  "v_bitop3_b32 %[f], %[" #B "], %[" #C "], %[" #D "] bitop3:" #TT "\n\t"               \
+  "v_add3_u32 %[t], %[" #AIN "], %[f], %[" #K "]\n\t"                                   \
+  "v_alignbit_b32 %[t], %[t], %[t], " #R "\n\t"                                         \
+  "v_add_u32_e64 %[" #AOUT "], %[" #B "], %[t]\n\t"
+
+// 64 steps from the state s0..s3 (unchanged) into a..d: the block's new state is s + (a..d).
+__device__ __forceinline__ void md5_steps_asm(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+                                              uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d,
                                               const uint32_t km[64]) {
   uint32_t f, t;
-  S3H_MD5_ROUND(0, 0xca, 25, 20, 15, 10);  // F = b ? c : d;       s = 7, 12, 17, 22
+  asm volatile(S3H_ALIGN8
+               S3H_MD5_ST_IO(0xca, s0, a, s1, s2, s3, k0, 25)
+               S3H_MD5_ST_IO(0xca, s3, d, a, s1, s2, k1, 20)
+               S3H_MD5_ST_IO(0xca, s2, c, d, a, s1, k2, 15)
+               S3H_MD5_ST_IO(0xca, s1, b, c, d, a, k3, 10)
+               S3H_MD5_4(0xca, k4, k5, k6, k7, 25, 20, 15, 10)
+               S3H_MD5_4(0xca, k8, k9, k10, k11, 25, 20, 15, 10)
+               S3H_MD5_4(0xca, k12, k13, k14, k15, 25, 20, 15, 10)
+               : [a] "=&v"(a), [b] "=&v"(b), [c] "=&v"(c), [d] "=&v"(d), [f] "=&v"(f), [t] "=&v"(t)
+               : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3),
+                 [k0] "v"(km[0]), [k1] "v"(km[1]), [k2] "v"(km[2]), [k3] "v"(km[3]),
+                 [k4] "v"(km[4]), [k5] "v"(km[5]), [k6] "v"(km[6]), [k7] "v"(km[7]),
+                 [k8] "v"(km[8]), [k9] "v"(km[9]), [k10] "v"(km[10]), [k11] "v"(km[11]),
+                 [k12] "v"(km[12]), [k13] "v"(km[13]), [k14] "v"(km[14]), [k15] "v"(km[15]));
+  // F = b ? c : d, s = 7, 12, 17, 22 (alignbit by 32 - s) above; then
   S3H_MD5_ROUND(1, 0xe4, 27, 23, 18, 12);  // G = d ? b : c;       s = 5, 9, 14, 20
   S3H_MD5_ROUND(2, 0x96, 28, 21, 16, 9);   // H = b ^ c ^ d;       s = 4, 11, 16, 23
   S3H_MD5_ROUND(3, 0x39, 26, 22, 17, 11);  // I = c ^ (b | ~d);    s = 6, 10, 15, 21
@@ -1493,25 +1517,54 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
       st[0] = v.x; st[1] = v.y; st[2] = v.z; st[3] = v.w;
     }
     __syncthreads();
-    for (uint64_t i = 0; i < iters; ++i) {
+    // slots are sorted by length: every chain of the group is live below the last one's end
+    const uint32_t last = (slot0 + 64u <= A.n ? slot0 + 64u : A.n) - 1;
+    const uint64_t live_end = slot_blocks(A, A.slots[last].len);
+    uint64_t clk0 = 0, rt0 = 0;  // clock probe (s3h_plan_set_clock_probe), as in skew_body
+    if (A.clocks) {
+      clk0 = __builtin_amdgcn_s_memtime();
+      rt0 = __builtin_amdgcn_s_memrealtime();
+    }
+    // One block: its 16 M+K rows from LDS, 64 steps, feed-forward (`check`: only the chains
+    // still live), then the block's barrier.  Blocks below live_end -- every chain of the
+    // group live -- run in their own loop with no per-lane test (the loop tools/isa_counts.py
+    // counts); the ragged tail and nothing else pays for the selects.
+    auto block = [&](uint64_t i, bool check) {
       uint32_t km[64];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const uint4 v = lds_km[i & 1][q][lane];
         km[4 * q] = v.x; km[4 * q + 1] = v.y; km[4 * q + 2] = v.z; km[4 * q + 3] = v.w;
       }
-      uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
 #if S3H_EXP_MD5_C_STEPS
+      uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
       md5_steps<0>(a, b, c, d, km);
 #else
-      md5_steps_asm(a, b, c, d, km);
+      uint32_t a, b, c, d;
+      md5_steps_asm(st[0], st[1], st[2], st[3], a, b, c, d, km);
 #endif
-      const bool live = (A.blk_begin + i) < nb;
-      st[0] = live ? st[0] + a : st[0];
-      st[1] = live ? st[1] + b : st[1];
-      st[2] = live ? st[2] + c : st[2];
-      st[3] = live ? st[3] + d : st[3];
+      if (!check) {
+        st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+      } else {
+        const bool live = (A.blk_begin + i) < nb;
+        st[0] = live ? st[0] + a : st[0];
+        st[1] = live ? st[1] + b : st[1];
+        st[2] = live ? st[2] + c : st[2];
+        st[3] = live ? st[3] + d : st[3];
+      }
       __syncthreads();
+    };
+    const uint64_t fast = live_end > A.blk_begin ? (live_end - A.blk_begin < iters
+                                                    ? live_end - A.blk_begin : iters) : 0;
+    uint64_t i = 0;
+    for (; i < fast; ++i) block(i, false);
+    for (; i < iters; ++i) block(i, true);
+    if (A.clocks) {
+      const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+      if (lane == 0) {
+        uint64_t* c = A.clocks + 4ull * group;
+        c[0] = clk0; c[1] = clk1; c[2] = rt0; c[3] = rt1;
+      }
     }
     if (valid && nb > A.blk_begin) {
       if (emits(A, nb))

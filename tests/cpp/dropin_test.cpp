@@ -122,6 +122,27 @@ int main(int argc, char** argv) {
                         to_little_endian(0x11223344u) == 0x44332211u &&
                         next_div_by(129, 64) == 192 && next_div_by(128, 64) == 128 &&
                         right_rotate(1u, 1) == 0x80000000u && lshift(0xff, 8) == 0xff00u);
+  // verify_payloads rejects a malformed expected digest -- a sign, whitespace, a 0x prefix, a
+  // non-hex digit, a wrong length -- before any GPU call, naming the part (CPU-only check)
+  {
+    const std::string good(64, 'a');
+    const std::string bad[] = {"-1" + std::string(62, '0'), " f" + std::string(62, '0'),
+                               "0x" + std::string(62, '0'), std::string(63, '0') + "g",
+                               std::string(63, '0')};
+    bool all_rejected = true;
+    for (const std::string& b : bad) {
+      const uint8_t byte = 0;
+      try {
+        (void)sha256::verify_payloads({&byte, &byte}, {1, 1}, {good, b});
+        all_rejected = false;
+      } catch (const std::invalid_argument& e) {
+        all_rejected &= std::string(e.what()).find("part 1") != std::string::npos;
+      } catch (...) {
+        all_rejected = false;  // the parse must fail first, not the (absent) GPU
+      }
+    }
+    report("verify_payloads rejects malformed hex", all_rejected);
+  }
   if (argc > 1 && std::string(argv[1]) == "--gpu") {
     std::vector<std::string> msgs = {s6, s14, s15, "", std::string(5 << 20, 'q')};
     std::vector<const uint8_t*> ptrs;

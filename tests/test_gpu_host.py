@@ -2,7 +2,9 @@
 per-device contexts that grow and are trimmed, many pageable parts, concurrent callers, parts
 read from a file, and plans launched on two streams at once.  Every digest vs the oracle or
 the lib/hash goldens (bit-exact)."""
+import os
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -209,6 +211,62 @@ def test_concurrent_bad_call_fails_alone(torch_cuda, oracle, tmp_path):
         x.join()
     assert all(res[k] for k in range(4)), res
     assert "past the end" in res["bad"], res
+
+
+def test_merged_batch_failure_is_rerun_per_caller(torch_cuda, oracle, tmp_path):
+    """A file shrinks AFTER its call passed the open-time range check and queued behind a busy
+    device: the merged batch it joins fails on the short read.  That batch is re-run one
+    request at a time (capi.hip run_batch), so the concurrent memory call queued with it gets
+    its digests and OK, and only the file call fails, with its own message."""
+    rng = np.random.default_rng(61)
+    path = tmp_path / "shrinks.bin"
+    np.frombuffer(rng.bytes(4 * MIB), dtype=np.uint8).tofile(path)
+    busy = [np.frombuffer(rng.bytes(8 * MIB), dtype=np.uint8) for _ in range(96)]
+    mem = [rng.integers(0, 256, int(L), dtype=np.uint8) for L in rng.integers(1, 200000, 24)]
+    want = np.stack([oracle.sha256(p.tobytes()) for p in mem])
+    res = {}
+
+    def run(name, fn):
+        try:
+            res[name] = fn()
+        except s3.S3HashError as e:
+            res[name] = e
+
+    t_busy = threading.Thread(target=run, args=("busy", lambda: s3.sha256_batch_host(busy)))
+    t_file = threading.Thread(target=run, args=("file", lambda: s3.sha256_file_parts(
+        str(path), [0, 2 * MIB], [1 * MIB, 2 * MIB])))
+    t_mem = threading.Thread(target=run, args=("mem", lambda: s3.sha256_batch_host(mem)))
+    t_busy.start()
+    time.sleep(0.03)   # the busy call leads the device queue
+    t_file.start()
+    time.sleep(0.03)   # the file call passed its range check and waits in the queue
+    os.truncate(path, 3 * MIB)
+    t_mem.start()
+    for t in (t_busy, t_file, t_mem):
+        t.join()
+    assert not isinstance(res["busy"], Exception), res["busy"]
+    assert not isinstance(res["mem"], Exception), res["mem"]
+    assert np.array_equal(res["mem"], want)
+    # the busy call holds the device for >= one 8 MiB chain (~120 ms), so the file call ran
+    # after the truncation -- merged with the memory call, then alone -- and failed by itself
+    assert isinstance(res["file"], s3.S3HashError), res["file"]
+    assert "reading a part failed" in str(res["file"]), res["file"]
+
+
+def test_file_parts_beyond_staging_cap(torch_cuda, oracle, tmp_path):
+    """More file ranges than 64-B slices of the 128 MiB staging slot hold (2,097,152): the
+    shard runs in passes of that many parts, so the pinned staging ring stays at 384 MiB
+    (capi.hip run_host_shard_passes).  3,000 sampled digests vs the oracle."""
+    rng = np.random.default_rng(62)
+    data = np.frombuffer(rng.bytes(8 * MIB), dtype=np.uint8)
+    path = tmp_path / "many.bin"
+    data.tofile(path)
+    n = 2_100_000
+    offs = rng.integers(0, 8 * MIB - 64, n).astype(np.uint64)
+    lens = rng.integers(0, 64, n).astype(np.uint64)
+    got = s3.sha256_file_parts(str(path), offs, lens)
+    idx = np.concatenate([rng.choice(n, 2990, replace=False), np.arange(n - 10, n)])
+    assert np.array_equal(got[idx], oracle.batch(data, offs[idx], lens[idx]))
 
 
 def test_file_parts_transfer_geometry(torch_cuda, golden, tmp_path):

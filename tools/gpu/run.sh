@@ -9,6 +9,7 @@
 #   pytest[:ARGS]        python -m pytest tests -m gpu -x -v ARGS            (900 s)
 #   smoke                __graft_entry__.smoke()                              (120 s)
 #   bench[:ARGS]         python bench.py ARGS -> one JSON line                (400 s)
+#   benchlib:LIB[:ARGS]  the same with S3H_LIBRARY=LIB (a `make exp` build)    (400 s)
 #   stats[:ARGS]         rocprofv3 --kernel-trace --stats of bench.py ARGS    (400 s)
 #   pmc[:CTRS[:ARGS]]    rocprofv3 --pmc CTRS (one pass, e.g. FETCH_SIZE) of bench.py ARGS (240 s)
 #   n2[:ARGS]            2-rank torch.distributed.run rehearsal of bench.py on the one GPU
@@ -33,6 +34,10 @@ for step in "$@"; do
       tail -1 $out.log ;;
     bench)
       timeout -k 10 400 python bench.py $rest > $out.jsonl 2> $out.err; rc=$?
+      [ $rc -eq 0 ] && python3 tools/gpu/summary.py $out.jsonl ;;
+    benchlib)  # benchlib:LIB:ARGS -- bench.py on an experiment build (S3H_LIBRARY=LIB)
+      lib=${rest%%:*}; args=""; [ "$rest" != "$lib" ] && args=${rest#*:}
+      S3H_LIBRARY=$lib timeout -k 10 400 python bench.py $args > $out.jsonl 2> $out.err; rc=$?
       [ $rc -eq 0 ] && python3 tools/gpu/summary.py $out.jsonl ;;
     stats)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d ${out}_prof -o run --output-format csv -- python3 bench.py $rest > $out.jsonl 2> $out.err; rc=$?

@@ -31,6 +31,7 @@ KERNELS = {
     "skew_nc2": ("_ZN3s3h24sha256_skew_pairs_kernelENS_10LaunchArgsE", 8),
     "skewp": ("_ZN3s3h18sha256_skew_kernelILi1ELb1EEEvNS_10LaunchArgsE", 4),
     "skews": ("_ZN3s3h25sha256_skew_shared_kernelENS_10LaunchArgsE", 8),
+    "md5-pc": ("_ZN3s3h13md5_pc_kernelENS_10LaunchArgsE", 1),
 }
 # every kernel a plan can launch (code hashes) and the flag-synchronised ones among them, whose
 # timed-out waits must reach the device error word (sha256_kernels.hip flag_wait_ge)
@@ -125,7 +126,13 @@ def main(lib, dst, dis_out=None):
         cand = [(n, o) for n, o in loops(function_body(lines, sym))
                 if not any(x.startswith(("ds_write_b128", "global_load", "global_store", "buffer_",
                                          "flat_")) for x in o)]
-        label, ops = max(cand, key=lambda x: len(x[1]))
+        if name == "md5-pc":
+            # the consumer's fast loop (every chain live: no per-lane select) comes first in
+            # the code, before the ragged-tail loop that is a few selects longer
+            cand = [x for x in cand if sum(o.startswith("v_") for o in x[1]) >= 256]
+            label, ops = cand[0]
+        else:
+            label, ops = max(cand, key=lambda x: len(x[1]))
         c = classify(ops)
         out["kernels"][name] = {
             "symbol": sym, "loop_label": label, "blocks_per_step": bps,
