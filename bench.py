@@ -843,6 +843,7 @@ def stream_mode(args, s3, torch, data, ids, lens, offs, rank, name, stream):
         one_object_pass()
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / max(1, args.steps)
+    st.status(stream)  # every update/final launch's device error word clear (raises otherwise)
     gd = out.cpu().numpy().view(np.uint32)
     fixtures = golden_fixtures(args.config, algo, args.part_bytes)
     checked = [int(p) for p in ids if int(p) in fixtures]

@@ -140,6 +140,45 @@ def test_other_rank_shards(torch_cuda, oracle, golden, cfg, world, rank):
         _release(torch)
 
 
+@pytest.mark.parametrize("cfg", ["c4", "c2"])
+def test_every_rank_of_eight_on_one_gpu(torch_cuda, oracle, golden, cfg):
+    """BASELINE configs[3] whole: all 65,536 x 8 MiB parts (512 GiB) hashed shard by shard on
+    the one GPU, each shard exactly as rank r of an 8-GPU run holds it (global part p on rank
+    p % 8, slot p // 8), and the same for the C2 weak-scaling job at N = 8 (8,192 parts).  Every
+    shard checked against its own lib/hash fixtures and the oracle on 16 random parts; the
+    multi-GPU run itself adds only concurrency on separate devices (no data-path exchange)."""
+    torch = torch_cuda
+    from s3client_amd.shard import shard_ids
+    world, per, L = 8, (8192 if cfg == "c4" else 1024), 8 * MIB
+    lens = np.full(per, L, dtype=np.uint64)
+    offs = np.arange(per, dtype=np.uint64) * np.uint64(L)
+    fx = {e["p"]: e["digest"] for e in golden["c2_parts"] + golden["c4_parts"] + golden["shard_parts"]}
+    data = torch.empty(per * L, dtype=torch.uint8, device="cuda")
+    out = torch.empty((per, 8), dtype=torch.int32, device="cuda")
+    checked = 0
+    try:
+        with s3.Plan(offs, lens) as plan:
+            for rank in range(world):
+                ids = shard_ids(per * world, rank, world)
+                s3.generate_parts(data, offs, lens, ids, SEED)
+                plan.launch(data, out)
+                plan.status()
+                txt = s3.digests_to_text(out.cpu().numpy().view(np.uint32))
+                mine = [k for k, p in enumerate(ids) if int(p) in fx]
+                assert len(mine) >= 4, rank
+                for k in mine:
+                    assert txt[k] == fx[int(ids[k])], (rank, int(ids[k]))
+                checked += len(mine)
+                rng = np.random.default_rng(700 + rank)
+                slots = np.sort(rng.choice(per, 16, replace=False))
+                got = out.cpu().numpy().view(np.uint32)[slots]
+                assert np.array_equal(got, _oracle_sample(torch, oracle, data, offs, lens, slots)), rank
+        assert checked >= 4 * world
+    finally:
+        del data, out
+        _release(torch)
+
+
 def _ragged_top(rng, n, top, top_len, rest_len):
     lens = rng.integers(*rest_len, n)
     lens[:top] = rng.integers(*top_len, top)

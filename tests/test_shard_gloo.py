@@ -76,3 +76,42 @@ def test_shards_partition_and_bench_workload_matches():
 def test_pack_offsets_alignment():
     offs = pack_offsets([0, 1, 255, 256, 257])
     assert offs.tolist() == [0, 0, 256, 512, 768]
+
+
+def test_every_rank_checks_its_own_fixtures():
+    """bench.py's parity check on every rank of an N-GPU run (N = 2, 4, 8; the C2 weak-scaling
+    job and C4) finds at least four lib/hash fixtures inside that rank's shard."""
+    import bench
+    from s3client_amd.shard import shard_ids
+    for cfg, per in (("c2", 1024), ("c4", 8192)):
+        fx = bench.golden_fixtures(cfg, "sha256")
+        for world in (2, 4, 8):
+            for r in range(world):
+                ids = shard_ids(per * world, r, world)
+                assert sum(int(p) in fx for p in ids) >= 4, (cfg, world, r)
+
+
+def _per_rank_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    got = bench.per_rank(dist, world, [rank, 10 + rank, 7])
+    if rank == 0:
+        q.put(got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_per_rank_gather_gloo():
+    """The gloo all_gather bench.py uses for per-rank parity and C4 timings (world size 2)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_per_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == [[0, 10, 7], [1, 11, 7]]
