@@ -47,6 +47,9 @@
 #ifndef S3H_EXP_MD5_C_STEPS
 #define S3H_EXP_MD5_C_STEPS 0  // 1: the MD5 consumer's steps as compiled C (round-2 form)
 #endif
+#ifndef S3H_EXP_MD5_ALL_ROWS
+#define S3H_EXP_MD5_ALL_ROWS 0  // 1: asm steps, but all 16 M+K rows read before the first step
+#endif
 #ifndef S3H_EXP_SPIN_LIMIT
 #define S3H_EXP_SPIN_LIMIT (1u << 24)  // flag waits: s_sleep 1 polls before a wait times out
 #endif
@@ -1345,6 +1348,60 @@ __device__ __forceinline__ void md5_steps_asm(uint32_t s0, uint32_t s1, uint32_t
   S3H_MD5_ROUND(3, 0x39, 26, 22, 17, 11);  // I = c ^ (b | ~d);    s = 6, 10, 15, 21
 }
 
+// The consumer's block with its M+K rows streamed in: each asm statement issues the two
+// ds_read_b128 the NEXT statement needs, runs 8 steps, and waits for its reads at its end
+// (s_waitcnt inside the statement, so its outputs are complete when it returns).  The
+// compiler, left to itself, reads all 16 rows after the block's barrier and waits for every
+// one before the first step (it drains the LDS counter before an inline asm statement): 16
+// KiB per wave at 128 B/clk of LDS plus the latency, ~190 cycles exposed per block.  Here
+// only rows 0-1 are waited for; the other 14 land behind the steps.  `ad`: this lane's LDS
+// byte address of row 0 (rows are 1,024 B apart: Md5Lds).
+#define S3H_MD5_LD2(OFF0, OFF1)                                                           \
+  "ds_read_b128 %[n0], %[ad] offset:" #OFF0 "\n\t"                                        \
+  "ds_read_b128 %[n1], %[ad] offset:" #OFF1 "\n\t"
+#define S3H_MD5_8(TT, R0, R1, R2, R3)                                                     \
+  S3H_MD5_4(TT, k0, k1, k2, k3, R0, R1, R2, R3) S3H_MD5_4(TT, k4, k5, k6, k7, R0, R1, R2, R3)
+#define S3H_MD5_KIN(P, Q)                                                                 \
+  [k0] "v"(P.x), [k1] "v"(P.y), [k2] "v"(P.z), [k3] "v"(P.w), [k4] "v"(Q.x), [k5] "v"(Q.y), \
+      [k6] "v"(Q.z), [k7] "v"(Q.w)
+#define S3H_MD5_PIPE(TT, R0, R1, R2, R3, OFF0, OFF1, P, Q, N0, N1)                        \
+  asm volatile(S3H_ALIGN8 S3H_MD5_LD2(OFF0, OFF1) S3H_MD5_8(TT, R0, R1, R2, R3)            \
+               "s_waitcnt lgkmcnt(0)\n\t"                                                 \
+               : [a] "+v"(a), [b] "+v"(b), [c] "+v"(c), [d] "+v"(d), [f] "=&v"(f),          \
+                 [t] "=&v"(t), [n0] "=&v"(N0), [n1] "=&v"(N1)                              \
+               : S3H_MD5_KIN(P, Q), [ad] "v"(ad)                                          \
+               : "memory")
+
+__device__ __forceinline__ void md5_block_streamed(uint32_t s0, uint32_t s1, uint32_t s2,
+                                                   uint32_t s3, uint32_t& a, uint32_t& b,
+                                                   uint32_t& c, uint32_t& d, v4u32 r0,
+                                                   v4u32 r1, uint32_t ad) {
+  uint32_t f, t;
+  v4u32 r2, r3, r4, r5, r6, r7, r8, r9, r10, r11, r12, r13, r14, r15;
+  // steps 0-7 (F) from the block-start state; rows 2-3 in flight
+  asm volatile(S3H_ALIGN8 S3H_MD5_LD2(2048, 3072)
+               S3H_MD5_ST_IO(0xca, s0, a, s1, s2, s3, k0, 25)
+               S3H_MD5_ST_IO(0xca, s3, d, a, s1, s2, k1, 20)
+               S3H_MD5_ST_IO(0xca, s2, c, d, a, s1, k2, 15)
+               S3H_MD5_ST_IO(0xca, s1, b, c, d, a, k3, 10)
+               S3H_MD5_4(0xca, k4, k5, k6, k7, 25, 20, 15, 10)
+               "s_waitcnt lgkmcnt(0)\n\t"
+               : [a] "=&v"(a), [b] "=&v"(b), [c] "=&v"(c), [d] "=&v"(d), [f] "=&v"(f),
+                 [t] "=&v"(t), [n0] "=&v"(r2), [n1] "=&v"(r3)
+               : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), S3H_MD5_KIN(r0, r1),
+                 [ad] "v"(ad)
+               : "memory");
+  S3H_MD5_PIPE(0xca, 25, 20, 15, 10, 4096, 5120, r2, r3, r4, r5);      // steps 8-15 (F)
+  S3H_MD5_PIPE(0xe4, 27, 23, 18, 12, 6144, 7168, r4, r5, r6, r7);      // 16-23 (G)
+  S3H_MD5_PIPE(0xe4, 27, 23, 18, 12, 8192, 9216, r6, r7, r8, r9);      // 24-31 (G)
+  S3H_MD5_PIPE(0x96, 28, 21, 16, 9, 10240, 11264, r8, r9, r10, r11);   // 32-39 (H)
+  S3H_MD5_PIPE(0x96, 28, 21, 16, 9, 12288, 13312, r10, r11, r12, r13); // 40-47 (H)
+  S3H_MD5_PIPE(0x39, 26, 22, 17, 11, 14336, 15360, r12, r13, r14, r15);// 48-55 (I)
+  asm volatile(S3H_ALIGN8 S3H_MD5_8(0x39, 26, 22, 17, 11)                // 56-63 (I)
+               : [a] "+v"(a), [b] "+v"(b), [c] "+v"(c), [d] "+v"(d), [f] "=&v"(f), [t] "=&v"(t)
+               : S3H_MD5_KIN(r14, r15));
+}
+
 // Decoded message words of MD5 block `blk` (zeros past the launch's range, padding at the end).
 __device__ __forceinline__ void md5_decode(const RawBlock& r, uint32_t sel, const uint8_t* bp,
                                            uint64_t len, uint64_t bits, uint64_t blk,
@@ -1530,18 +1587,28 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
     // group live -- run in their own loop with no per-lane test (the loop tools/isa_counts.py
     // counts); the ragged tail and nothing else pays for the selects.
     auto block = [&](uint64_t i, bool check) {
+#if S3H_EXP_MD5_C_STEPS || S3H_EXP_MD5_ALL_ROWS
       uint32_t km[64];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const uint4 v = lds_km[i & 1][q][lane];
         km[4 * q] = v.x; km[4 * q + 1] = v.y; km[4 * q + 2] = v.z; km[4 * q + 3] = v.w;
       }
+#endif
 #if S3H_EXP_MD5_C_STEPS
       uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
       md5_steps<0>(a, b, c, d, km);
-#else
+#elif S3H_EXP_MD5_ALL_ROWS
       uint32_t a, b, c, d;
       md5_steps_asm(st[0], st[1], st[2], st[3], a, b, c, d, km);
+#else
+      typedef __attribute__((address_space(3))) uint4 lds_u4;
+      const uint4* row0 = &lds_km[i & 1][0][lane];
+      const uint32_t ad = uint32_t(reinterpret_cast<uintptr_t>((const lds_u4*)row0));
+      const v4u32 r0 = *reinterpret_cast<const v4u32*>(row0);
+      const v4u32 r1 = *reinterpret_cast<const v4u32*>(&lds_km[i & 1][1][lane]);
+      uint32_t a, b, c, d;
+      md5_block_streamed(st[0], st[1], st[2], st[3], a, b, c, d, r0, r1, ad);
 #endif
       if (!check) {
         st[0] += a; st[1] += b; st[2] += c; st[3] += d;

@@ -15,6 +15,7 @@
 #   n2[:ARGS]            2-rank torch.distributed.run rehearsal of bench.py on the one GPU
 #                        (S3H_BENCH_SHARE_GPU=1, gloo collectives, as the driver's N>1 runs) (600 s)
 #   py:SCRIPT[:ARGS]     python SCRIPT ARGS                                  (600 s)
+#   exe:PROGRAM ARGS     a built tool, e.g. tools/ubench_dep                  (300 s)
 set -o pipefail
 TAG=${1:?usage: run.sh TAG STEP...}; shift
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
@@ -50,6 +51,9 @@ for step in "$@"; do
       S3H_BENCH_SHARE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 $rest > $out.jsonl 2> $out.err; rc=$?
       [ $rc -eq 0 ] && python3 tools/gpu/summary.py $out.jsonl ;;
+    exe)  # exe:PROGRAM [ARGS] -- a built tool (e.g. tools/ubench_dep), output to .log
+      timeout -k 10 300 $rest > $out.log 2>&1; rc=$?
+      tail -12 $out.log ;;
     py)
       script=${rest%%:*}; args=""; [ "$rest" != "$script" ] && args=${rest#*:}
       timeout -k 10 600 python -u $script $args > $out.log 2>&1; rc=$?
