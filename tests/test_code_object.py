@@ -98,3 +98,31 @@ def test_host_threads_respect_a_narrowed_affinity():
     assert r.returncode == 0, r.stderr
     per, cpus = map(int, r.stdout.split())
     assert cpus == min(2, _expected_cpus()) and per == cpus
+
+
+def test_pmc_profiles_carry_provenance_and_bench_checks_it():
+    """Every newest profiles/r*_<cfg>_<kernel>_pmc.json records the kernel it measured (isa key
+    + code hash), the library sha256 and the commit; bench.py takes its traffic only for a
+    build running the same kernel machine code and returns null with the reason otherwise."""
+    import glob
+    import bench
+    newest = {}
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_*_pmc.json"))):
+        parts = os.path.basename(f).split("_")
+        newest[(parts[1], "_".join(parts[2:-1]))] = f
+    with open(os.path.join(ROOT, "s3client_amd", "kernel_isa_counts.json")) as fh:
+        shipped = json.load(fh)["code_hash"]
+    for (cfg, kname), f in newest.items():
+        if os.path.basename(f)[:3] in ("r01", "r02"):
+            continue  # round 1-2 summaries predate provenance (bench gives them null traffic)
+        with open(f) as fh:
+            s = json.load(fh)
+        for k in ("kernel_key", "kernel_code_hash", "library_sha256", "git_head"):
+            assert s.get(k), (f, k)
+        key = s["kernel_key"]
+        t, src, note = bench.pmc_traffic(cfg, kname, key, s["kernel_code_hash"], 1e9)
+        assert t is not None and src.endswith(os.path.basename(f)), note
+        t2, _, note2 = bench.pmc_traffic(cfg, kname, key, "0" * 16, 1e9)
+        assert t2 is None and "0000000000000000" in note2
+        if shipped.get(key) == s["kernel_code_hash"]:
+            assert 0.999 < t / 1e9 < 1.01, (f, t)  # no re-reads: traffic == algorithmic bytes
