@@ -358,8 +358,11 @@ int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t
                 uint64_t b0, uint64_t b1, uint64_t origin, uint32_t flags, const uint64_t* d_bits,
                 hipStream_t stream) {
   const s3h::LaunchArgs A = make_args(P, d_base, d_digests, d_state, b0, b1, origin, flags, d_bits);
-  if (P->algo == S3H_ALGO_MD5)
-    hipLaunchKernelGGL(s3h::md5_pc_kernel, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
+  if (P->algo == S3H_ALGO_MD5 && P->grid <= uint64_t(device_cus(P->device)))
+    hipLaunchKernelGGL(s3h::md5_pc_kernel<s3h::kMd5Bps>, dim3(P->grid), dim3(s3h::kPcThreads), 0,
+                       stream, A);
+  else if (P->algo == S3H_ALGO_MD5)  // more workgroups than CUs: the 32 KiB form, several per CU
+    hipLaunchKernelGGL(s3h::md5_pc_kernel<1>, dim3(P->grid), dim3(s3h::kPcThreads), 0, stream, A);
   // The skew kernel counts a launch's blocks in 32 bits: a range of 2^31 blocks (128 GiB of
   // one part) or more runs on the quad kernel (same plan geometry, 64-bit counters).
   else if (P->kernel == S3H_KERNEL_SKEW && b1 - b0 >= (1ull << 31) && P->quad_waves == 1)

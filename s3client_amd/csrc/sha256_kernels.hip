@@ -44,11 +44,8 @@
 #ifndef S3H_EXP_MD5_SELF_DEPTH
 #define S3H_EXP_MD5_SELF_DEPTH 4  // self-fed MD5: blocks fetched ahead
 #endif
-#ifndef S3H_EXP_MD5_C_STEPS
-#define S3H_EXP_MD5_C_STEPS 0  // 1: the MD5 consumer's steps as compiled C (round-2 form)
-#endif
-#ifndef S3H_EXP_MD5_ALL_ROWS
-#define S3H_EXP_MD5_ALL_ROWS 0  // 1: asm steps, but all 16 M+K rows read before the first step
+#ifndef S3H_EXP_MD5_BPS
+#define S3H_EXP_MD5_BPS 4  // MD5 producer/consumer kernel: blocks per producer step
 #endif
 #ifndef S3H_EXP_SPIN_LIMIT
 #define S3H_EXP_SPIN_LIMIT (1u << 24)  // flag waits: s_sleep 1 polls before a wait times out
@@ -1276,22 +1273,10 @@ __device__ __forceinline__ void md5_steps_w(uint32_t& a, uint32_t& b, uint32_t& 
   }
 }
 
-template <int I>
-__device__ __forceinline__ void md5_steps(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d,
-                                          const uint32_t km[64]) {
-  if constexpr (I < 64) {
-    md5_step<I>(a, b, c, d, km[I]);      // (a,b,c,d) -> (d, a', b, c)
-    md5_steps<I + 1>(d, a, b, c, km);
-  }
-}
-
-// The same 64 steps as four asm statements of 16 steps, every instruction 8 bytes (v_add_u32
-// in its VOP3 encoding) and each statement 8-byte aligned.  Compiled C mixes the 4-byte VOP2
-// add into the 8-byte bitop3 / add3 / alignbit stream, so half the 8-byte instructions sit at
-// an address = 4 (mod 8), where a lone wave issues them in ~5 instead of ~4 cycles
-// (profiles/r01_ubench_alignment.txt) -- the standalone MD5 consumer ran 1,370 cycles per
-// block for ~280 instructions.  Step: f = F(b,c,d) (one bitop3), t = a + f + (M+K),
-// t = rotl(t, s) (alignbit by 32 - s), a = b + t; the names rotate (a,b,c,d) -> (d,a,b,c).
+// MD5 steps in aligned 8-byte asm: every instruction 8 bytes (v_add_u32 in its VOP3
+// encoding), each statement 8-byte aligned.  Step: f = F(b,c,d) (one bitop3), t = a + f +
+// (M+K), t = rotl(t, s) (alignbit by 32 - s), a = b + t; the names rotate (a,b,c,d) ->
+// (d,a,b,c).
 #define S3H_MD5_ST(TT, A, B, C, D, K, R)                                                 \
   "v_bitop3_b32 %[f], %[" #B "], %[" #C "], %[" #D "] bitop3:" #TT "\n\t"               \
   "v_add3_u32 %[t], %[" #A "], %[f], %[" #K "]\n\t"                                     \
@@ -1300,21 +1285,6 @@ __device__ __forceinline__ void md5_steps(uint32_t& a, uint32_t& b, uint32_t& c,
 #define S3H_MD5_4(TT, K0, K1, K2, K3, R0, R1, R2, R3)                                    \
   S3H_MD5_ST(TT, a, b, c, d, K0, R0) S3H_MD5_ST(TT, d, a, b, c, K1, R1)                   \
   S3H_MD5_ST(TT, c, d, a, b, K2, R2) S3H_MD5_ST(TT, b, c, d, a, K3, R3)
-// 16 steps of one round: truth table TT, rotations (as alignbit amounts 32 - s) R0..R3
-#define S3H_MD5_16(TT, R0, R1, R2, R3)                                                   \
-  S3H_MD5_4(TT, k0, k1, k2, k3, R0, R1, R2, R3) S3H_MD5_4(TT, k4, k5, k6, k7, R0, R1, R2, R3) \
-  S3H_MD5_4(TT, k8, k9, k10, k11, R0, R1, R2, R3) S3H_MD5_4(TT, k12, k13, k14, k15, R0, R1, R2, R3)
-#define S3H_MD5_ROUND(Q, TT, R0, R1, R2, R3)                                              \
-  asm volatile(S3H_ALIGN8 S3H_MD5_16(TT, R0, R1, R2, R3)                                  \
-               : [a] "+v"(a), [b] "+v"(b), [c] "+v"(c), [d] "+v"(d), [f] "=&v"(f), [t] "=&v"(t) \
-               : [k0] "v"(km[16 * Q]), [k1] "v"(km[16 * Q + 1]), [k2] "v"(km[16 * Q + 2]),   \
-                 [k3] "v"(km[16 * Q + 3]), [k4] "v"(km[16 * Q + 4]), [k5] "v"(km[16 * Q + 5]), \
-                 [k6] "v"(km[16 * Q + 6]), [k7] "v"(km[16 * Q + 7]), [k8] "v"(km[16 * Q + 8]), \
-                 [k9] "v"(km[16 * Q + 9]), [k10] "v"(km[16 * Q + 10]),                       \
-                 [k11] "v"(km[16 * Q + 11]), [k12] "v"(km[16 * Q + 12]),                     \
-                 [k13] "v"(km[16 * Q + 13]), [k14] "v"(km[16 * Q + 14]),                     \
-                 [k15] "v"(km[16 * Q + 15]))
-
 // The first four steps read the block-start state s0..s3 and write fresh registers a..d, so
 // the state survives for the feed-forward without four register copies.
 #define S3H_MD5_ST_IO(TT, AIN, AOUT, B, C, D, K, R)                                      \
@@ -1323,83 +1293,107 @@ __device__ __forceinline__ void md5_steps(uint32_t& a, uint32_t& b, uint32_t& c,
   "v_alignbit_b32 %[t], %[t], %[t], " #R "\n\t"                                         \
   "v_add_u32_e64 %[" #AOUT "], %[" #B "], %[t]\n\t"
 
-// 64 steps from the state s0..s3 (unchanged) into a..d: the block's new state is s + (a..d).
-__device__ __forceinline__ void md5_steps_asm(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
-                                              uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d,
-                                              const uint32_t km[64]) {
-  uint32_t f, t;
-  asm volatile(S3H_ALIGN8
-               S3H_MD5_ST_IO(0xca, s0, a, s1, s2, s3, k0, 25)
-               S3H_MD5_ST_IO(0xca, s3, d, a, s1, s2, k1, 20)
-               S3H_MD5_ST_IO(0xca, s2, c, d, a, s1, k2, 15)
-               S3H_MD5_ST_IO(0xca, s1, b, c, d, a, k3, 10)
-               S3H_MD5_4(0xca, k4, k5, k6, k7, 25, 20, 15, 10)
-               S3H_MD5_4(0xca, k8, k9, k10, k11, 25, 20, 15, 10)
-               S3H_MD5_4(0xca, k12, k13, k14, k15, 25, 20, 15, 10)
-               : [a] "=&v"(a), [b] "=&v"(b), [c] "=&v"(c), [d] "=&v"(d), [f] "=&v"(f), [t] "=&v"(t)
-               : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3),
-                 [k0] "v"(km[0]), [k1] "v"(km[1]), [k2] "v"(km[2]), [k3] "v"(km[3]),
-                 [k4] "v"(km[4]), [k5] "v"(km[5]), [k6] "v"(km[6]), [k7] "v"(km[7]),
-                 [k8] "v"(km[8]), [k9] "v"(km[9]), [k10] "v"(km[10]), [k11] "v"(km[11]),
-                 [k12] "v"(km[12]), [k13] "v"(km[13]), [k14] "v"(km[14]), [k15] "v"(km[15]));
-  // F = b ? c : d, s = 7, 12, 17, 22 (alignbit by 32 - s) above; then
-  S3H_MD5_ROUND(1, 0xe4, 27, 23, 18, 12);  // G = d ? b : c;       s = 5, 9, 14, 20
-  S3H_MD5_ROUND(2, 0x96, 28, 21, 16, 9);   // H = b ^ c ^ d;       s = 4, 11, 16, 23
-  S3H_MD5_ROUND(3, 0x39, 26, 22, 17, 11);  // I = c ^ (b | ~d);    s = 6, 10, 15, 21
-}
+// The consumer's block with its M+K rows streamed in: five asm statements, each issuing the
+// ds_read_b128 of the rows the NEXT statement needs, running its steps, and waiting for its
+// reads in its last step (so its outputs are complete when it returns).  The compiler, left
+// to itself, reads all 16 rows and waits for every one before the first step (it drains the
+// LDS counter before an inline asm statement): 16 KiB per wave at 128 B/clk of LDS plus the
+// latency exposed per block.  Statement boundaries cost an alignment s_nop whenever the
+// compiler puts an odd number of 4-byte scalar instructions between two statements, so the
+// block is cut into as few statements as the 30-operand limit allows: steps 0-7 | 8-23 |
+// 24-39 | 40-55 | 56-63 (rows 0-1 | 2-5 | 6-9 | 10-13 | 14-15).  With kNext the fourth
+// statement also reads rows 0-1 of the NEXT block (LDS byte address adn: the same producer
+// step, so already published), so only a step's first block waits for rows after the barrier.
+// `ad`: this lane's LDS byte address of row 0 (rows are 1,024 B apart: Md5Lds).
+//
+// S3H_MD5_ST_W ends a statement: its s_waitcnt (4 B) and the step's VOP2 add (4 B) keep the
+// statement a multiple of 8 bytes (the reads were issued a statement earlier: nothing waits).
+#define S3H_MD5_ST_W(TT, A, B, C, D, K, R)                                               \
+  "v_bitop3_b32 %[f], %[" #B "], %[" #C "], %[" #D "] bitop3:" #TT "\n\t"               \
+  "v_add3_u32 %[t], %[" #A "], %[f], %[" #K "]\n\t"                                     \
+  "v_alignbit_b32 %[t], %[t], %[t], " #R "\n\t"                                         \
+  "s_waitcnt lgkmcnt(0)\n\t"                                                            \
+  "v_add_u32_e32 %[" #A "], %[" #B "], %[t]\n\t"
+#define S3H_MD5_4W(TT, K0, K1, K2, K3, R0, R1, R2, R3)                                   \
+  S3H_MD5_ST(TT, a, b, c, d, K0, R0) S3H_MD5_ST(TT, d, a, b, c, K1, R1)                   \
+  S3H_MD5_ST(TT, c, d, a, b, K2, R2) S3H_MD5_ST_W(TT, b, c, d, a, K3, R3)
+#define S3H_MD5_LD(N, ADR, OFF) "ds_read_b128 %[" #N "], %[" #ADR "] offset:" #OFF "\n\t"
+#define S3H_MD5_K16(P0, P1, P2, P3)                                                       \
+  [k0] "v"(P0.x), [k1] "v"(P0.y), [k2] "v"(P0.z), [k3] "v"(P0.w), [k4] "v"(P1.x),          \
+      [k5] "v"(P1.y), [k6] "v"(P1.z), [k7] "v"(P1.w), [k8] "v"(P2.x), [k9] "v"(P2.y),      \
+      [k10] "v"(P2.z), [k11] "v"(P2.w), [k12] "v"(P3.x), [k13] "v"(P3.y), [k14] "v"(P3.z), \
+      [k15] "v"(P3.w)
+#define S3H_MD5_STATE [a] "+v"(a), [b] "+v"(b), [c] "+v"(c), [d] "+v"(d), [f] "=&v"(f), [t] "=&v"(t)
+#define S3H_MD5_NEXT4(N0, N1, N2, N3) [n0] "=&v"(N0), [n1] "=&v"(N1), [n2] "=&v"(N2), [n3] "=&v"(N3)
+// 16 steps: two groups of 4 in round TT1 (rotations R*), two in TT2 (rotations Q*), the last
+// step of the statement waiting for its reads
+#define S3H_MD5_16(TT1, R0, R1, R2, R3, TT2, Q0, Q1, Q2, Q3)                               \
+  S3H_MD5_4(TT1, k0, k1, k2, k3, R0, R1, R2, R3) S3H_MD5_4(TT1, k4, k5, k6, k7, R0, R1, R2, R3) \
+  S3H_MD5_4(TT2, k8, k9, k10, k11, Q0, Q1, Q2, Q3)                                        \
+  S3H_MD5_4W(TT2, k12, k13, k14, k15, Q0, Q1, Q2, Q3)
+#define S3H_MD5_F 0xca, 25, 20, 15, 10  // F = b ? c : d;    s = 7, 12, 17, 22 (alignbit 32 - s)
+#define S3H_MD5_G 0xe4, 27, 23, 18, 12  // G = d ? b : c;    s = 5, 9, 14, 20
+#define S3H_MD5_H 0x96, 28, 21, 16, 9   // H = b ^ c ^ d;    s = 4, 11, 16, 23
+#define S3H_MD5_I 0x39, 26, 22, 17, 11  // I = c ^ (b | ~d); s = 6, 10, 15, 21
+#define S3H_MD5_16X(A, B) S3H_MD5_16(A, B)  // expands the round macros into arguments
 
-// The consumer's block with its M+K rows streamed in: each asm statement issues the two
-// ds_read_b128 the NEXT statement needs, runs 8 steps, and waits for its reads at its end
-// (s_waitcnt inside the statement, so its outputs are complete when it returns).  The
-// compiler, left to itself, reads all 16 rows after the block's barrier and waits for every
-// one before the first step (it drains the LDS counter before an inline asm statement): 16
-// KiB per wave at 128 B/clk of LDS plus the latency, ~190 cycles exposed per block.  Here
-// only rows 0-1 are waited for; the other 14 land behind the steps.  `ad`: this lane's LDS
-// byte address of row 0 (rows are 1,024 B apart: Md5Lds).
-#define S3H_MD5_LD2(OFF0, OFF1)                                                           \
-  "ds_read_b128 %[n0], %[ad] offset:" #OFF0 "\n\t"                                        \
-  "ds_read_b128 %[n1], %[ad] offset:" #OFF1 "\n\t"
-#define S3H_MD5_8(TT, R0, R1, R2, R3)                                                     \
-  S3H_MD5_4(TT, k0, k1, k2, k3, R0, R1, R2, R3) S3H_MD5_4(TT, k4, k5, k6, k7, R0, R1, R2, R3)
-#define S3H_MD5_KIN(P, Q)                                                                 \
-  [k0] "v"(P.x), [k1] "v"(P.y), [k2] "v"(P.z), [k3] "v"(P.w), [k4] "v"(Q.x), [k5] "v"(Q.y), \
-      [k6] "v"(Q.z), [k7] "v"(Q.w)
-#define S3H_MD5_PIPE(TT, R0, R1, R2, R3, OFF0, OFF1, P, Q, N0, N1)                        \
-  asm volatile(S3H_ALIGN8 S3H_MD5_LD2(OFF0, OFF1) S3H_MD5_8(TT, R0, R1, R2, R3)            \
-               "s_waitcnt lgkmcnt(0)\n\t"                                                 \
-               : [a] "+v"(a), [b] "+v"(b), [c] "+v"(c), [d] "+v"(d), [f] "=&v"(f),          \
-                 [t] "=&v"(t), [n0] "=&v"(N0), [n1] "=&v"(N1)                              \
-               : S3H_MD5_KIN(P, Q), [ad] "v"(ad)                                          \
-               : "memory")
-
+template <bool kNext>
 __device__ __forceinline__ void md5_block_streamed(uint32_t s0, uint32_t s1, uint32_t s2,
                                                    uint32_t s3, uint32_t& a, uint32_t& b,
                                                    uint32_t& c, uint32_t& d, v4u32 r0,
-                                                   v4u32 r1, uint32_t ad) {
+                                                   v4u32 r1, uint32_t ad, uint32_t adn,
+                                                   v4u32& n0, v4u32& n1) {
   uint32_t f, t;
   v4u32 r2, r3, r4, r5, r6, r7, r8, r9, r10, r11, r12, r13, r14, r15;
-  // steps 0-7 (F) from the block-start state; rows 2-3 in flight
-  asm volatile(S3H_ALIGN8 S3H_MD5_LD2(2048, 3072)
+  // steps 0-7 (F) from the block-start state (rows 0-1); rows 2-5 in flight
+  asm volatile(S3H_ALIGN8 S3H_MD5_LD(n0, ad, 2048) S3H_MD5_LD(n1, ad, 3072)
+               S3H_MD5_LD(n2, ad, 4096) S3H_MD5_LD(n3, ad, 5120)
                S3H_MD5_ST_IO(0xca, s0, a, s1, s2, s3, k0, 25)
                S3H_MD5_ST_IO(0xca, s3, d, a, s1, s2, k1, 20)
                S3H_MD5_ST_IO(0xca, s2, c, d, a, s1, k2, 15)
                S3H_MD5_ST_IO(0xca, s1, b, c, d, a, k3, 10)
-               S3H_MD5_4(0xca, k4, k5, k6, k7, 25, 20, 15, 10)
-               "s_waitcnt lgkmcnt(0)\n\t"
+               S3H_MD5_4W(0xca, k4, k5, k6, k7, 25, 20, 15, 10)
                : [a] "=&v"(a), [b] "=&v"(b), [c] "=&v"(c), [d] "=&v"(d), [f] "=&v"(f),
-                 [t] "=&v"(t), [n0] "=&v"(r2), [n1] "=&v"(r3)
-               : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), S3H_MD5_KIN(r0, r1),
-                 [ad] "v"(ad)
+                 [t] "=&v"(t), S3H_MD5_NEXT4(r2, r3, r4, r5)
+               : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [k0] "v"(r0.x),
+                 [k1] "v"(r0.y), [k2] "v"(r0.z), [k3] "v"(r0.w), [k4] "v"(r1.x), [k5] "v"(r1.y),
+                 [k6] "v"(r1.z), [k7] "v"(r1.w), [ad] "v"(ad)
                : "memory");
-  S3H_MD5_PIPE(0xca, 25, 20, 15, 10, 4096, 5120, r2, r3, r4, r5);      // steps 8-15 (F)
-  S3H_MD5_PIPE(0xe4, 27, 23, 18, 12, 6144, 7168, r4, r5, r6, r7);      // 16-23 (G)
-  S3H_MD5_PIPE(0xe4, 27, 23, 18, 12, 8192, 9216, r6, r7, r8, r9);      // 24-31 (G)
-  S3H_MD5_PIPE(0x96, 28, 21, 16, 9, 10240, 11264, r8, r9, r10, r11);   // 32-39 (H)
-  S3H_MD5_PIPE(0x96, 28, 21, 16, 9, 12288, 13312, r10, r11, r12, r13); // 40-47 (H)
-  S3H_MD5_PIPE(0x39, 26, 22, 17, 11, 14336, 15360, r12, r13, r14, r15);// 48-55 (I)
-  asm volatile(S3H_ALIGN8 S3H_MD5_8(0x39, 26, 22, 17, 11)                // 56-63 (I)
-               : [a] "+v"(a), [b] "+v"(b), [c] "+v"(c), [d] "+v"(d), [f] "=&v"(f), [t] "=&v"(t)
-               : S3H_MD5_KIN(r14, r15));
+  // steps 8-23: F (rows 2-3), G (rows 4-5); rows 6-9 in flight
+  asm volatile(S3H_ALIGN8 S3H_MD5_LD(n0, ad, 6144) S3H_MD5_LD(n1, ad, 7168)
+               S3H_MD5_LD(n2, ad, 8192) S3H_MD5_LD(n3, ad, 9216)
+               S3H_MD5_16X(S3H_MD5_F, S3H_MD5_G)
+               : S3H_MD5_STATE, S3H_MD5_NEXT4(r6, r7, r8, r9)
+               : S3H_MD5_K16(r2, r3, r4, r5), [ad] "v"(ad)
+               : "memory");
+  // steps 24-39: G (rows 6-7), H (rows 8-9); rows 10-13 in flight
+  asm volatile(S3H_ALIGN8 S3H_MD5_LD(n0, ad, 10240) S3H_MD5_LD(n1, ad, 11264)
+               S3H_MD5_LD(n2, ad, 12288) S3H_MD5_LD(n3, ad, 13312)
+               S3H_MD5_16X(S3H_MD5_G, S3H_MD5_H)
+               : S3H_MD5_STATE, S3H_MD5_NEXT4(r10, r11, r12, r13)
+               : S3H_MD5_K16(r6, r7, r8, r9), [ad] "v"(ad)
+               : "memory");
+  // steps 40-55: H (rows 10-11), I (rows 12-13); rows 14-15 (+ the next block's 0-1) in flight
+  if constexpr (kNext) {
+    asm volatile(S3H_ALIGN8 S3H_MD5_LD(n0, ad, 14336) S3H_MD5_LD(n1, ad, 15360)
+                 S3H_MD5_LD(n2, adn, 0) S3H_MD5_LD(n3, adn, 1024)
+                 S3H_MD5_16X(S3H_MD5_H, S3H_MD5_I)
+                 : S3H_MD5_STATE, S3H_MD5_NEXT4(r14, r15, n0, n1)
+                 : S3H_MD5_K16(r10, r11, r12, r13), [ad] "v"(ad), [adn] "v"(adn)
+                 : "memory");
+  } else {
+    asm volatile(S3H_ALIGN8 S3H_MD5_LD(n0, ad, 14336) S3H_MD5_LD(n1, ad, 15360)
+                 S3H_MD5_16X(S3H_MD5_H, S3H_MD5_I)
+                 : S3H_MD5_STATE, [n0] "=&v"(r14), [n1] "=&v"(r15)
+                 : S3H_MD5_K16(r10, r11, r12, r13), [ad] "v"(ad)
+                 : "memory");
+  }
+  // steps 56-63: I (rows 14-15)
+  asm volatile(S3H_ALIGN8 S3H_MD5_4(0x39, k0, k1, k2, k3, 26, 22, 17, 11)
+               S3H_MD5_4(0x39, k4, k5, k6, k7, 26, 22, 17, 11)
+               : S3H_MD5_STATE
+               : [k0] "v"(r14.x), [k1] "v"(r14.y), [k2] "v"(r14.z), [k3] "v"(r14.w),
+                 [k4] "v"(r15.x), [k5] "v"(r15.y), [k6] "v"(r15.z), [k7] "v"(r15.w));
 }
 
 // Decoded message words of MD5 block `blk` (zeros past the launch's range, padding at the end).
@@ -1517,13 +1511,21 @@ md5_done:
 }
 
 // MD5 group: one consumer wave (role 0) and one producer wave (role 1) over 64 chains (one
-// lane each; slots group*64...), an s_barrier per block.
+// lane each; slots group*64...).  The producer writes kBps blocks' M+K rows per step into one
+// of two LDS buffers; one s_barrier per step.  Round 2 synchronised every block: the
+// consumer's loop trip (a taken branch), the barrier and the first rows' LDS read cost ~150
+// cycles per 1,200-cycle block on top of the 4-cycle issue of its 289 instructions
+// (profiles/r03_exp_md5_rows.jsonl; a dependent MD5 step chain itself issues at 4.02 cycles
+// per instruction, profiles/r03_ubench_dep.txt).  Now the consumer runs a step's blocks
+// back to back, each block's last asm statement reading the next block's first rows.
+template <int kBps>
 struct Md5Lds {
-  uint4 km[2][16][64];
+  uint4 km[2][kBps][16][64];  // [buffer][block of the step][row][lane]: kBps x 32 KiB
 };
 
+template <int kBps>
 __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t group,
-                                            const uint32_t role, Md5Lds& L) {
+                                            const uint32_t role, Md5Lds<kBps>& L) {
   auto& lds_km = L.km;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t slot0 = group * 64u;
@@ -1536,36 +1538,44 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
   const uint64_t wg_end = wg_nb < A.blk_end ? wg_nb : A.blk_end;
   if (wg_end <= A.blk_begin) return;
   const uint64_t iters = wg_end - A.blk_begin;
+  const uint64_t nsteps = (iters + kBps - 1) / kBps;  // the same in both waves: equal barriers
 
   if (role == 1) {
-    // An MD5 block takes the consumer only ~0.9 us, less than an HBM round trip under load,
-    // so the producer keeps TWO blocks in flight: three register sets rotate, and the load
-    // for block j+2 is issued while block j is produced.
+    // Step k's blocks are fetched one step (kBps blocks, ~5 us of chain time) before they are
+    // decoded: two named register sets alternate (no dynamic indexing -> no scratch).
     const uint64_t b0 = A.blk_begin;
     const uint8_t* p = A.base + s.off + 64ull * (b0 - A.blk_origin);
     const uint32_t sel = le_selector(uint32_t(reinterpret_cast<uintptr_t>(p) & 3));
     const uint64_t fend = fetch_end(s.len, A.blk_end);
     const uint64_t bits = valid ? msg_bits(A, slot, s.len) : 0;
     const uint64_t dl = decode_len(valid, s.len);
-    RawBlock ra, rb, rc;
-    fetch_full(p, b0 < fend, A.zero, ra);
-    fetch_full(p + 64, b0 + 1 < fend, A.zero, rb);
-    fetch_full(p + 128, b0 + 2 < fend, A.zero, rc);
-    md5_produce(ra, sel, p, dl, bits, b0, A.blk_end, lds_km[0], lane);
+    RawBlock ra[kBps], rb[kBps];
+#define S3H_MD5_FETCH(R, K)                                                                  \
+    _Pragma("unroll") for (int h = 0; h < kBps; ++h)                                        \
+      fetch_full(p + 64 * ((K) * kBps + h), b0 + (K) * kBps + h < fend, A.zero, R[h]);
+#define S3H_MD5_MAKE(R, K)                                                                   \
+    _Pragma("unroll") for (int h = 0; h < kBps; ++h)                                        \
+      md5_produce(R[h], sel, p + 64 * ((K) * kBps + h), dl, bits, b0 + (K) * kBps + h,      \
+                  A.blk_end, lds_km[(K) & 1][h], lane);
+    S3H_MD5_FETCH(ra, 0)
+    S3H_MD5_FETCH(rb, 1)
+    S3H_MD5_MAKE(ra, 0)
     __syncthreads();
-#define S3H_MD5_PSTEP(J, NEXT, CUR)                                                        \
-    if ((J) < iters) {                                                                     \
-      fetch_full(p + 64 * ((J) + 2), b0 + (J) + 2 < fend, A.zero, NEXT);                    \
-      md5_produce(CUR, sel, p + 64 * (J), dl, bits, b0 + (J), A.blk_end, lds_km[(J) & 1], lane); \
-    }                                                                                      \
-    __syncthreads();                                                                       \
-    if ((J) + 1 > iters) break;
-    for (uint64_t j = 1;; j += 3) {
-      S3H_MD5_PSTEP(j, ra, rb)
-      S3H_MD5_PSTEP(j + 1, rb, rc)
-      S3H_MD5_PSTEP(j + 2, rc, ra)
+    for (uint64_t k = 1;; k += 2) {
+      if (k < nsteps) {
+        S3H_MD5_FETCH(ra, k + 1)
+        S3H_MD5_MAKE(rb, k)
+      }
+      __syncthreads();
+      if (k + 1 > nsteps) break;
+      if (k + 1 < nsteps) {
+        S3H_MD5_FETCH(rb, k + 2)
+        S3H_MD5_MAKE(ra, k + 1)
+      }
+      __syncthreads();
     }
-#undef S3H_MD5_PSTEP
+#undef S3H_MD5_FETCH
+#undef S3H_MD5_MAKE
   } else {
     __builtin_amdgcn_s_setprio(3);
     uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
@@ -1582,50 +1592,49 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
       clk0 = __builtin_amdgcn_s_memtime();
       rt0 = __builtin_amdgcn_s_memrealtime();
     }
-    // One block: its 16 M+K rows from LDS, 64 steps, feed-forward (`check`: only the chains
-    // still live), then the block's barrier.  Blocks below live_end -- every chain of the
-    // group live -- run in their own loop with no per-lane test (the loop tools/isa_counts.py
-    // counts); the ragged tail and nothing else pays for the selects.
-    auto block = [&](uint64_t i, bool check) {
-#if S3H_EXP_MD5_C_STEPS || S3H_EXP_MD5_ALL_ROWS
-      uint32_t km[64];
+    typedef __attribute__((address_space(3))) uint4 lds_u4;
+    auto row_addr = [&](uint32_t buf, int h) {
+      return uint32_t(reinterpret_cast<uintptr_t>((const lds_u4*)&lds_km[buf][h][0][lane]));
+    };
+    // One step: its kBps blocks back to back (`check`: only the chains still live are fed
+    // forward, and blocks past the launch's range are skipped), then the step's barrier.
+    // Steps whose every block lies below live_end -- every chain live -- run in their own loop
+    // with no test (the loop tools/isa_counts.py counts); the ragged tail pays the selects.
+    auto step = [&](uint64_t j, bool check) {
+      const uint32_t buf = uint32_t(j & 1);
+      v4u32 r0 = *reinterpret_cast<const v4u32*>(&lds_km[buf][0][0][lane]);
+      v4u32 r1 = *reinterpret_cast<const v4u32*>(&lds_km[buf][0][1][lane]);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const uint4 v = lds_km[i & 1][q][lane];
-        km[4 * q] = v.x; km[4 * q + 1] = v.y; km[4 * q + 2] = v.z; km[4 * q + 3] = v.w;
-      }
-#endif
-#if S3H_EXP_MD5_C_STEPS
-      uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
-      md5_steps<0>(a, b, c, d, km);
-#elif S3H_EXP_MD5_ALL_ROWS
-      uint32_t a, b, c, d;
-      md5_steps_asm(st[0], st[1], st[2], st[3], a, b, c, d, km);
-#else
-      typedef __attribute__((address_space(3))) uint4 lds_u4;
-      const uint4* row0 = &lds_km[i & 1][0][lane];
-      const uint32_t ad = uint32_t(reinterpret_cast<uintptr_t>((const lds_u4*)row0));
-      const v4u32 r0 = *reinterpret_cast<const v4u32*>(row0);
-      const v4u32 r1 = *reinterpret_cast<const v4u32*>(&lds_km[i & 1][1][lane]);
-      uint32_t a, b, c, d;
-      md5_block_streamed(st[0], st[1], st[2], st[3], a, b, c, d, r0, r1, ad);
-#endif
-      if (!check) {
-        st[0] += a; st[1] += b; st[2] += c; st[3] += d;
-      } else {
-        const bool live = (A.blk_begin + i) < nb;
-        st[0] = live ? st[0] + a : st[0];
-        st[1] = live ? st[1] + b : st[1];
-        st[2] = live ? st[2] + c : st[2];
-        st[3] = live ? st[3] + d : st[3];
+      for (int h = 0; h < kBps; ++h) {
+        const uint64_t i = j * kBps + h;
+        if (check && i >= iters) break;  // uniform: the launch's last step may be partial
+        v4u32 n0, n1;
+        uint32_t a, b, c, d;
+        if (h + 1 < kBps)
+          md5_block_streamed<true>(st[0], st[1], st[2], st[3], a, b, c, d, r0, r1,
+                                   row_addr(buf, h), row_addr(buf, h + 1), n0, n1);
+        else
+          md5_block_streamed<false>(st[0], st[1], st[2], st[3], a, b, c, d, r0, r1,
+                                    row_addr(buf, h), 0u, n0, n1);
+        if (!check) {
+          st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+        } else {
+          const bool live = (A.blk_begin + i) < nb;
+          st[0] = live ? st[0] + a : st[0];
+          st[1] = live ? st[1] + b : st[1];
+          st[2] = live ? st[2] + c : st[2];
+          st[3] = live ? st[3] + d : st[3];
+        }
+        r0 = n0;
+        r1 = n1;
       }
       __syncthreads();
     };
     const uint64_t fast = live_end > A.blk_begin ? (live_end - A.blk_begin < iters
                                                     ? live_end - A.blk_begin : iters) : 0;
-    uint64_t i = 0;
-    for (; i < fast; ++i) block(i, false);
-    for (; i < iters; ++i) block(i, true);
+    uint64_t j = 0;
+    for (; j < fast / kBps; ++j) step(j, false);
+    for (; j < nsteps; ++j) step(j, true);
     if (A.clocks) {
       const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
       if (lane == 0) {
@@ -1644,9 +1653,13 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
   }
 }
 
+// kBps = kMd5Bps (128 KiB of LDS: one workgroup per CU) while the grid fits one workgroup per
+// CU (<= 64 x CUs parts); kBps = 1 (32 KiB, several per CU) for larger batches (capi.hip).
+constexpr int kMd5Bps = S3H_EXP_MD5_BPS;
+template <int kBps>
 __global__ __launch_bounds__(kPcThreads) void md5_pc_kernel(LaunchArgs A) {
-  __shared__ Md5Lds L;
-  md5_pc_body(A, blockIdx.x, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L);
+  __shared__ Md5Lds<kBps> L;
+  md5_pc_body<kBps>(A, blockIdx.x, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L);
 }
 
 // ------------------------------------------------------------- dual digest (SHA-256 + MD5)
@@ -1663,12 +1676,12 @@ template <bool PAIR>
 __global__ __launch_bounds__(128) void sha256_md5_dual_kernel(LaunchArgs S, LaunchArgs M,
                                                               uint32_t sha_grid) {
   __shared__ SkewLds<1, PAIR> LS;
-  __shared__ Md5Lds LM;
+  __shared__ Md5Lds<2> LM;  // 64 KiB beside the skew group's 36 KiB
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (blockIdx.x < sha_grid)
     skew_body<1, PAIR, false>(S, blockIdx.x, wave, LS, nullptr);
   else
-    md5_pc_body(M, blockIdx.x - sha_grid, wave, LM);
+    md5_pc_body<2>(M, blockIdx.x - sha_grid, wave, LM);
 }
 
 // sha256_md5_group_kernel: every workgroup holds BOTH digests of the same kParts parts -- a

@@ -31,7 +31,7 @@ KERNELS = {
     "skew_nc2": ("_ZN3s3h24sha256_skew_pairs_kernelENS_10LaunchArgsE", 8),
     "skewp": ("_ZN3s3h18sha256_skew_kernelILi1ELb1EEEvNS_10LaunchArgsE", 4),
     "skews": ("_ZN3s3h25sha256_skew_shared_kernelENS_10LaunchArgsE", 8),
-    "md5-pc": ("_ZN3s3h13md5_pc_kernelENS_10LaunchArgsE", 1),
+    "md5-pc": ("_ZN3s3h13md5_pc_kernelILi4EEEvNS_10LaunchArgsE", 4),  # S3H_EXP_MD5_BPS
 }
 # every kernel a plan can launch (code hashes) and the flag-synchronised ones among them, whose
 # timed-out waits must reach the device error word (sha256_kernels.hip flag_wait_ge)
@@ -43,7 +43,8 @@ ALL_KERNELS = {
     "quad_nc2": "_ZN3s3h18sha256_quad_kernelILi2EEEvNS_10LaunchArgsE",
     "skew": KERNELS["skew"][0], "skew_nc2": KERNELS["skew_nc2"][0],
     "skewp": KERNELS["skewp"][0], "skews": KERNELS["skews"][0],
-    "md5-pc": "_ZN3s3h13md5_pc_kernelENS_10LaunchArgsE",
+    "md5-pc": "_ZN3s3h13md5_pc_kernelILi4EEEvNS_10LaunchArgsE",
+    "md5-pc1": "_ZN3s3h13md5_pc_kernelILi1EEEvNS_10LaunchArgsE",
     "dual_split": "_ZN3s3h22sha256_md5_dual_kernelILb0EEEvNS_10LaunchArgsES1_j",
     "dual_group": "_ZN3s3h23sha256_md5_group_kernelILb1EEEvNS_10LaunchArgsES1_",
     "dual_group_skew": "_ZN3s3h23sha256_md5_group_kernelILb0EEEvNS_10LaunchArgsES1_",
@@ -129,7 +130,7 @@ def main(lib, dst, dis_out=None):
         if name == "md5-pc":
             # the consumer's fast loop (every chain live: no per-lane select) comes first in
             # the code, before the ragged-tail loop that is a few selects longer
-            cand = [x for x in cand if sum(o.startswith("v_") for o in x[1]) >= 256]
+            cand = [x for x in cand if sum(o.startswith("v_") for o in x[1]) >= 256 * bps]
             label, ops = cand[0]
         else:
             label, ops = max(cand, key=lambda x: len(x[1]))
