@@ -1411,17 +1411,36 @@ __device__ __forceinline__ void md5_decode(const RawBlock& r, uint32_t sel, cons
   }
 }
 
+// Rows Q.. of M[g(i)] + K[i] written to LDS, unrolled by recursion (a #pragma unroll over the
+// 64 words was left rolled -- dynamic register indexing and a scratch array -- once the
+// multi-block producer's loop grew past the unroller's budget).
+template <int Q>
+__device__ __forceinline__ void md5_km_rows(const uint32_t w[16], uint4 (*buf)[64], uint32_t lane) {
+  if constexpr (Q < 16) {
+    buf[Q][lane] = make_uint4(w[md5_g(4 * Q)] + S3H_MD5_K(4 * Q),
+                              w[md5_g(4 * Q + 1)] + S3H_MD5_K(4 * Q + 1),
+                              w[md5_g(4 * Q + 2)] + S3H_MD5_K(4 * Q + 2),
+                              w[md5_g(4 * Q + 3)] + S3H_MD5_K(4 * Q + 3));
+    md5_km_rows<Q + 1>(w, buf, lane);
+  }
+}
+
+// kFull: the block is known to be a whole data block of every lane's part (the producer's
+// fast steps), so only the v_perm decode is emitted -- not the padding path's 64 predicated
+// byte loads, which, inlined at every unrolled produce site, made the multi-block producer's
+// loop the bulk of the kernel's code.
+template <bool kFull = false>
 __device__ __forceinline__ void md5_produce(const RawBlock& r, uint32_t sel, const uint8_t* bp,
                                             uint64_t len, uint64_t bits, uint64_t blk,
                                             uint64_t limit, uint4 (*buf)[64], uint32_t lane) {
   uint32_t w[16];
-  md5_decode(r, sel, bp, len, bits, blk, limit, w);
-  uint32_t km[64];
+  if constexpr (kFull) {
 #pragma unroll
-  for (int i = 0; i < 64; ++i) km[i] = w[md5_g(i)] + S3H_MD5_K(i);
-#pragma unroll
-  for (int q = 0; q < 16; ++q)
-    buf[q][lane] = make_uint4(km[4 * q], km[4 * q + 1], km[4 * q + 2], km[4 * q + 3]);
+    for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_perm(r.d[j + 1], r.d[j], sel);
+  } else {
+    md5_decode(r, sel, bp, len, bits, blk, limit, w);
+  }
+  md5_km_rows<0>(w, buf, lane);
 }
 
 // Self-fed MD5: one wave, one lane per chain (kChains <= 64, slots group*kChains...), each lane
@@ -1553,15 +1572,31 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
 #define S3H_MD5_FETCH(R, K)                                                                  \
     _Pragma("unroll") for (int h = 0; h < kBps; ++h)                                        \
       fetch_full(p + 64 * ((K) * kBps + h), b0 + (K) * kBps + h < fend, A.zero, R[h]);
-#define S3H_MD5_MAKE(R, K)                                                                   \
+#define S3H_MD5_MAKE_T(R, K, FULL)                                                           \
     _Pragma("unroll") for (int h = 0; h < kBps; ++h)                                        \
-      md5_produce(R[h], sel, p + 64 * ((K) * kBps + h), dl, bits, b0 + (K) * kBps + h,      \
-                  A.blk_end, lds_km[(K) & 1][h], lane);
+      md5_produce<FULL>(R[h], sel, p + 64 * ((K) * kBps + h), dl, bits, b0 + (K) * kBps + h, \
+                        A.blk_end, lds_km[(K) & 1][h], lane);
+#define S3H_MD5_MAKE(R, K) S3H_MD5_MAKE_T(R, K, false)
+    // Steps below `full_steps` hold whole data blocks of every lane's part (slots are sorted
+    // by length; the group's last valid slot is the shortest; lanes past n decode_len past
+    // everything): a compact loop with the perm-only decode runs them in pairs.
+    const uint32_t lastv = (slot0 + 64u <= A.n ? slot0 + 64u : A.n) - 1;
+    const uint64_t fabs = A.slots[lastv].len >> 6 < A.blk_end ? A.slots[lastv].len >> 6 : A.blk_end;
+    const uint64_t full_steps = fabs > b0 ? (fabs - b0) / kBps : 0;
     S3H_MD5_FETCH(ra, 0)
     S3H_MD5_FETCH(rb, 1)
     S3H_MD5_MAKE(ra, 0)
     __syncthreads();
-    for (uint64_t k = 1;; k += 2) {
+    uint64_t k = 1;
+    for (; k + 1 < full_steps; k += 2) {  // steps k and k + 1: whole blocks, both produced
+      S3H_MD5_FETCH(ra, k + 1)
+      S3H_MD5_MAKE_T(rb, k, true)
+      __syncthreads();
+      S3H_MD5_FETCH(rb, k + 2)
+      S3H_MD5_MAKE_T(ra, k + 1, true)
+      __syncthreads();
+    }
+    for (;; k += 2) {  // k odd: the same register roles as the loop above
       if (k < nsteps) {
         S3H_MD5_FETCH(ra, k + 1)
         S3H_MD5_MAKE(rb, k)
@@ -1576,6 +1611,7 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
     }
 #undef S3H_MD5_FETCH
 #undef S3H_MD5_MAKE
+#undef S3H_MD5_MAKE_T
   } else {
     __builtin_amdgcn_s_setprio(3);
     uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};

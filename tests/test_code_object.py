@@ -126,3 +126,15 @@ def test_pmc_profiles_carry_provenance_and_bench_checks_it():
         assert t2 is None and "0000000000000000" in note2
         if shipped.get(key) == s["kernel_code_hash"]:
             assert 0.999 < t / 1e9 < 1.01, (f, t)  # no re-reads: traffic == algorithmic bytes
+
+
+def test_no_kernel_uses_scratch():
+    """Every kernel of the shipped code object runs without scratch memory and without VGPR
+    spills: a spill or a dynamically indexed register array (the MD5 producer's M+K rows once
+    fell back to one when its loop outgrew the unroller) would put a memory round trip on
+    the chains."""
+    md = code_object.kernel_metadata(_native.LIB_PATH)
+    assert len(md) >= 15
+    for sym, m in md.items():
+        assert m["private_segment_fixed_size"] == 0, (sym, m)
+        assert m["vgpr_spill_count"] == 0, (sym, m)

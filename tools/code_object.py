@@ -36,6 +36,27 @@ def extract(lib: str, out: str) -> str:
     return out
 
 
+def kernel_metadata(lib: str) -> dict[str, dict]:
+    """{kernel symbol: {private_segment_fixed_size, vgpr_count, vgpr_spill_count, ...}} from the
+    shipped code object's AMDGPU metadata note (llvm-readelf --notes)."""
+    with tempfile.TemporaryDirectory() as td:
+        co = extract(lib, os.path.join(td, "co.o"))
+        text = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True,
+                              capture_output=True, text=True).stdout
+    out, cur = {}, {}
+    for line in text.splitlines():
+        m = re.match(r"\s*\.(\w+):\s+(\S+)\s*$", line)
+        if not m:
+            continue
+        key, val = m.groups()
+        if key == "name" and val.startswith("_Z"):
+            cur = out.setdefault(val, {})
+        elif key in ("private_segment_fixed_size", "vgpr_count", "sgpr_count",
+                     "vgpr_spill_count", "sgpr_spill_count"):  # (keys sorted after .name)
+            cur[key] = int(val)
+    return out
+
+
 def disassemble(lib: str, dis_out: str | None = None) -> list[str]:
     """llvm-objdump -d --symbolize-operands of the shipped code object, as lines."""
     with tempfile.TemporaryDirectory() as td:
