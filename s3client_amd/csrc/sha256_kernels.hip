@@ -1396,6 +1396,32 @@ __device__ __forceinline__ void md5_block_streamed(uint32_t s0, uint32_t s1, uin
                  [k4] "v"(r15.x), [k5] "v"(r15.y), [k6] "v"(r15.z), [k7] "v"(r15.w));
 }
 
+// The consumer's fast step: all kBps blocks of one producer step, fed forward, in ONE asm
+// statement generated by tools/gen_md5.py (rows in fixed registers v[200:231] that never leave
+// the statement; rows 0-1 of block 0 pinned to v[232:239], loaded after the step's barrier).
+// The per-block statements above cost a wait state plus an alignment s_nop at each of their
+// boundaries; this has one boundary per step.  `ad`: row 0 of block 0 of the step's buffer.
+// Not for kBps = 1 (md5_pc_kernel<1>, several workgroups per CU): the fixed registers would
+// raise its 128 VGPRs to 240 and cost it occupancy.
+#include "md5_step_asm.inc"
+#define S3H_MD5_STEP_OPERANDS                                                                 \
+  : [s0] "+v"(s0), [s1] "+v"(s1), [s2] "+v"(s2), [s3] "+v"(s3), [a] "=&v"(a), [b] "=&v"(b),   \
+    [c] "=&v"(c), [d] "=&v"(d), [f] "=&v"(f), [t] "=&v"(t), "+{v[232:235]}"(r0),              \
+    "+{v[236:239]}"(r1)                                                                       \
+  : [ad] "v"(ad)                                                                              \
+  : S3H_MD5_STEP_CLOBBERS, "memory"
+template <int kBps>
+__device__ __forceinline__ void md5_step_fused(uint32_t& s0, uint32_t& s1, uint32_t& s2,
+                                               uint32_t& s3, v4u32& r0, v4u32& r1, uint32_t ad) {
+  uint32_t a, b, c, d, f, t;
+  static_assert(kBps == 2 || kBps == 4, "fused MD5 steps are generated for 2 and 4 blocks");
+  if constexpr (kBps == 4)
+    asm volatile(S3H_ALIGN8 S3H_MD5_STEP_ASM_4 S3H_MD5_STEP_OPERANDS);
+  else
+    asm volatile(S3H_ALIGN8 S3H_MD5_STEP_ASM_2 S3H_MD5_STEP_OPERANDS);
+}
+#undef S3H_MD5_STEP_OPERANDS
+
 // Decoded message words of MD5 block `blk` (zeros past the launch's range, padding at the end).
 __device__ __forceinline__ void md5_decode(const RawBlock& r, uint32_t sel, const uint8_t* bp,
                                            uint64_t len, uint64_t bits, uint64_t blk,
@@ -1640,6 +1666,15 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
       const uint32_t buf = uint32_t(j & 1);
       v4u32 r0 = *reinterpret_cast<const v4u32*>(&lds_km[buf][0][0][lane]);
       v4u32 r1 = *reinterpret_cast<const v4u32*>(&lds_km[buf][0][1][lane]);
+#ifdef S3H_EXP_MD5_NOFUSE  // experiment: the per-block statements in the fast loop too
+      if (false) {
+#else
+      if (kBps > 1 && !check) {
+#endif
+        md5_step_fused<(kBps > 1 ? kBps : 2)>(st[0], st[1], st[2], st[3], r0, r1, row_addr(buf, 0));
+        __syncthreads();
+        return;
+      }
 #pragma unroll
       for (int h = 0; h < kBps; ++h) {
         const uint64_t i = j * kBps + h;
