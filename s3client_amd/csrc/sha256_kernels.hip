@@ -1568,6 +1568,14 @@ struct Md5Lds {
   uint4 km[2][kBps][16][64];  // [buffer][block of the step][row][lane]: kBps x 32 KiB
 };
 
+// Experiments (timing only, wrong digests): S3H_EXP_MD5_NOSYNC drops every barrier of both
+// waves (consumer speed with the producer's LDS traffic beside it but no waiting for it);
+// S3H_EXP_MD5_NOPROD also removes the producer (the consumer alone).
+#if defined(S3H_EXP_MD5_NOSYNC) || defined(S3H_EXP_MD5_NOPROD)
+#define S3H_MD5_SYNC() ((void)0)
+#else
+#define S3H_MD5_SYNC() __syncthreads()
+#endif
 template <int kBps>
 __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t group,
                                             const uint32_t role, Md5Lds<kBps>& L) {
@@ -1585,6 +1593,9 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
   const uint64_t iters = wg_end - A.blk_begin;
   const uint64_t nsteps = (iters + kBps - 1) / kBps;  // the same in both waves: equal barriers
 
+#ifdef S3H_EXP_MD5_NOPROD  // experiment (timing only, wrong digests): no producer at all
+  if (role == 1) return;
+#endif
   if (role == 1) {
     // Step k's blocks are fetched one step (kBps blocks, ~5 us of chain time) before they are
     // decoded: two named register sets alternate (no dynamic indexing -> no scratch).
@@ -1612,28 +1623,28 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
     S3H_MD5_FETCH(ra, 0)
     S3H_MD5_FETCH(rb, 1)
     S3H_MD5_MAKE(ra, 0)
-    __syncthreads();
+    S3H_MD5_SYNC();
     uint64_t k = 1;
     for (; k + 1 < full_steps; k += 2) {  // steps k and k + 1: whole blocks, both produced
       S3H_MD5_FETCH(ra, k + 1)
       S3H_MD5_MAKE_T(rb, k, true)
-      __syncthreads();
+      S3H_MD5_SYNC();
       S3H_MD5_FETCH(rb, k + 2)
       S3H_MD5_MAKE_T(ra, k + 1, true)
-      __syncthreads();
+      S3H_MD5_SYNC();
     }
     for (;; k += 2) {  // k odd: the same register roles as the loop above
       if (k < nsteps) {
         S3H_MD5_FETCH(ra, k + 1)
         S3H_MD5_MAKE(rb, k)
       }
-      __syncthreads();
+      S3H_MD5_SYNC();
       if (k + 1 > nsteps) break;
       if (k + 1 < nsteps) {
         S3H_MD5_FETCH(rb, k + 2)
         S3H_MD5_MAKE(ra, k + 1)
       }
-      __syncthreads();
+      S3H_MD5_SYNC();
     }
 #undef S3H_MD5_FETCH
 #undef S3H_MD5_MAKE
@@ -1645,7 +1656,7 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
       const uint4 v = reinterpret_cast<const uint4*>(A.state + 8ull * A.out_idx[slot])[0];
       st[0] = v.x; st[1] = v.y; st[2] = v.z; st[3] = v.w;
     }
-    __syncthreads();
+    S3H_MD5_SYNC();
     // slots are sorted by length: every chain of the group is live below the last one's end
     const uint32_t last = (slot0 + 64u <= A.n ? slot0 + 64u : A.n) - 1;
     const uint64_t live_end = slot_blocks(A, A.slots[last].len);
@@ -1672,7 +1683,7 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
       if (kBps > 1 && !check) {
 #endif
         md5_step_fused<(kBps > 1 ? kBps : 2)>(st[0], st[1], st[2], st[3], r0, r1, row_addr(buf, 0));
-        __syncthreads();
+        S3H_MD5_SYNC();
         return;
       }
 #pragma unroll
@@ -1699,7 +1710,7 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
         r0 = n0;
         r1 = n1;
       }
-      __syncthreads();
+      S3H_MD5_SYNC();
     };
     const uint64_t fast = live_end > A.blk_begin ? (live_end - A.blk_begin < iters
                                                     ? live_end - A.blk_begin : iters) : 0;
