@@ -47,6 +47,12 @@
 #ifndef S3H_EXP_MD5_BPS
 #define S3H_EXP_MD5_BPS 4  // MD5 producer/consumer kernel: blocks per producer step
 #endif
+#ifndef S3H_EXP_MD5_ROLL
+#define S3H_EXP_MD5_ROLL 1  // MD5 consumer: the rolling fused step (0: the chunked one)
+#endif
+#ifndef S3H_EXP_MD5_PSETS
+#define S3H_EXP_MD5_PSETS 2  // MD5 producer: raw-block register sets (3: loads two steps ahead)
+#endif
 #ifndef S3H_EXP_SPIN_LIMIT
 #define S3H_EXP_SPIN_LIMIT (1u << 24)  // flag waits: s_sleep 1 polls before a wait times out
 #endif
@@ -1403,7 +1409,11 @@ __device__ __forceinline__ void md5_block_streamed(uint32_t s0, uint32_t s1, uin
 // boundaries; this has one boundary per step.  `ad`: row 0 of block 0 of the step's buffer.
 // Not for kBps = 1 (md5_pc_kernel<1>, several workgroups per CU): the fixed registers would
 // raise its 128 VGPRs to 240 and cost it occupancy.
+#ifdef S3H_EXP_MD5_INC  // experiment builds: another generated schedule (tools/gen_md5.py)
+#include S3H_EXP_MD5_INC
+#else
 #include "md5_step_asm.inc"
+#endif
 #define S3H_MD5_STEP_OPERANDS                                                                 \
   : [s0] "+v"(s0), [s1] "+v"(s1), [s2] "+v"(s2), [s3] "+v"(s3), [a] "=&v"(a), [b] "=&v"(b),   \
     [c] "=&v"(c), [d] "=&v"(d), [f] "=&v"(f), [t] "=&v"(t), "+{v[232:235]}"(r0),              \
@@ -1421,6 +1431,26 @@ __device__ __forceinline__ void md5_step_fused(uint32_t& s0, uint32_t& s1, uint3
     asm volatile(S3H_ALIGN8 S3H_MD5_STEP_ASM_2 S3H_MD5_STEP_OPERANDS);
 }
 #undef S3H_MD5_STEP_OPERANDS
+
+// The rolling form of the fused step (tools/gen_md5.py roll_text, round 3): the statement reads
+// every row itself, ROLL_DEPTH rows ahead into a ring of fixed registers, with counted waits
+// every 4 rows -- no row read has less than ~20 steps to land, block boundaries included.
+template <int kBps>
+__device__ __forceinline__ void md5_step_roll(uint32_t& s0, uint32_t& s1, uint32_t& s2,
+                                              uint32_t& s3, uint32_t ad) {
+  uint32_t a, b, c, d, f, t;
+  static_assert(kBps == 2 || kBps == 4, "rolling MD5 steps are generated for 2 and 4 blocks");
+#define S3H_MD5_ROLL_OPERANDS                                                                 \
+  : [s0] "+v"(s0), [s1] "+v"(s1), [s2] "+v"(s2), [s3] "+v"(s3), [a] "=&v"(a), [b] "=&v"(b),   \
+    [c] "=&v"(c), [d] "=&v"(d), [f] "=&v"(f), [t] "=&v"(t)                                    \
+  : [ad] "v"(ad)                                                                              \
+  : S3H_MD5_ROLL_CLOBBERS, "memory"
+  if constexpr (kBps == 4)
+    asm volatile(S3H_ALIGN8 S3H_MD5_ROLL_ASM_4 S3H_MD5_ROLL_OPERANDS);
+  else
+    asm volatile(S3H_ALIGN8 S3H_MD5_ROLL_ASM_2 S3H_MD5_ROLL_OPERANDS);
+#undef S3H_MD5_ROLL_OPERANDS
+}
 
 // Decoded message words of MD5 block `blk` (zeros past the launch's range, padding at the end).
 __device__ __forceinline__ void md5_decode(const RawBlock& r, uint32_t sel, const uint8_t* bp,
@@ -1620,6 +1650,52 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
     const uint32_t lastv = (slot0 + 64u <= A.n ? slot0 + 64u : A.n) - 1;
     const uint64_t fabs = A.slots[lastv].len >> 6 < A.blk_end ? A.slots[lastv].len >> 6 : A.blk_end;
     const uint64_t full_steps = fabs > b0 ? (fabs - b0) / kBps : 0;
+#if S3H_EXP_MD5_PSETS == 3
+    // Experiment (S3H_EXP_MD5_PSETS=3): three register sets, loads two steps (~4 us of chain
+    // time) ahead of their decode.  Measured no faster (C2 114.2-114.6 vs 114.4-114.7 GiB/s,
+    // C4 shard 811 vs 815; profiles/r03_exp_md5_roll.jsonl): one step of lead already hides
+    // the loads, and the producer's loop (118 instructions per block) has slack.
+    RawBlock rc[kBps];
+    S3H_MD5_FETCH(ra, 0)
+    S3H_MD5_FETCH(rb, 1)
+    S3H_MD5_FETCH(rc, 2)
+    S3H_MD5_MAKE(ra, 0)
+    S3H_MD5_SYNC();
+    uint64_t k = 1;  // step s lives in set s % 3: ra, rb, rc
+    for (; k + 2 < full_steps; k += 3) {  // steps k, k + 1, k + 2: whole blocks
+      S3H_MD5_FETCH(ra, k + 2)
+      S3H_MD5_MAKE_T(rb, k, true)
+      S3H_MD5_SYNC();
+      S3H_MD5_FETCH(rb, k + 3)
+      S3H_MD5_MAKE_T(rc, k + 1, true)
+      S3H_MD5_SYNC();
+      S3H_MD5_FETCH(rc, k + 4)
+      S3H_MD5_MAKE_T(ra, k + 2, true)
+      S3H_MD5_SYNC();
+    }
+    // k = 1 (mod 3): the same set roles.  One barrier per step k = 1 .. nsteps, as the
+    // consumer's (one after each of its nsteps steps, the first after its state load).
+    for (;; k += 3) {
+      if (k < nsteps) {
+        S3H_MD5_FETCH(ra, k + 2)
+        S3H_MD5_MAKE(rb, k)
+      }
+      S3H_MD5_SYNC();
+      if (k + 1 > nsteps) break;
+      if (k + 1 < nsteps) {
+        S3H_MD5_FETCH(rb, k + 3)
+        S3H_MD5_MAKE(rc, k + 1)
+      }
+      S3H_MD5_SYNC();
+      if (k + 2 > nsteps) break;
+      if (k + 2 < nsteps) {
+        S3H_MD5_FETCH(rc, k + 4)
+        S3H_MD5_MAKE(ra, k + 2)
+      }
+      S3H_MD5_SYNC();
+      if (k + 3 > nsteps) break;
+    }
+#else
     S3H_MD5_FETCH(ra, 0)
     S3H_MD5_FETCH(rb, 1)
     S3H_MD5_MAKE(ra, 0)
@@ -1645,7 +1721,9 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
         S3H_MD5_MAKE(ra, k + 1)
       }
       S3H_MD5_SYNC();
+      if (k + 2 > nsteps) break;
     }
+#endif
 #undef S3H_MD5_FETCH
 #undef S3H_MD5_MAKE
 #undef S3H_MD5_MAKE_T
@@ -1675,6 +1753,13 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
     // with no test (the loop tools/isa_counts.py counts); the ragged tail pays the selects.
     auto step = [&](uint64_t j, bool check) {
       const uint32_t buf = uint32_t(j & 1);
+#if S3H_EXP_MD5_ROLL
+      if (kBps > 1 && !check) {
+        md5_step_roll<(kBps > 1 ? kBps : 2)>(st[0], st[1], st[2], st[3], row_addr(buf, 0));
+        S3H_MD5_SYNC();
+        return;
+      }
+#endif
       v4u32 r0 = *reinterpret_cast<const v4u32*>(&lds_km[buf][0][0][lane]);
       v4u32 r1 = *reinterpret_cast<const v4u32*>(&lds_km[buf][0][1][lane]);
 #ifdef S3H_EXP_MD5_NOFUSE  // experiment: the per-block statements in the fast loop too

@@ -1,6 +1,7 @@
-"""CPU checks of the MD5 consumer's fused step (tools/gen_md5.py), the asm statement that
-s3client_amd/csrc/md5_step_asm.inc holds: executed lane by lane against hashlib's MD5, with
-every LDS read landing only at its wait, and the committed .inc equal to the generator's."""
+"""CPU checks of the MD5 consumer's fused step (tools/gen_md5.py), the asm statements that
+s3client_amd/csrc/md5_step_asm.inc holds (the chunked form and the rolling form the product
+runs): executed lane by lane against hashlib's MD5, with every LDS read landing only at its
+counted wait, and the committed .inc equal to the generator's."""
 import hashlib
 import os
 import random
@@ -21,8 +22,11 @@ def _padded_blocks(msg: bytes) -> list[bytes]:
     return [m[i:i + 64] for i in range(0, len(m), 64)]
 
 
+@pytest.mark.parametrize("roll", [False, True])
 @pytest.mark.parametrize("bps", [1, 2, 4])
-def test_fused_step_matches_hashlib(bps):
+def test_fused_step_matches_hashlib(bps, roll):
+    if roll and bps == 1:
+        pytest.skip("the rolling step is generated for 2 and 4 blocks")
     rng = random.Random(bps)
     for n in (55, 64 * bps - 9, 64 * 3 * bps - 9, 64 * 2 * bps + 7):
         msg = bytes(rng.getrandbits(8) for _ in range(n))
@@ -37,8 +41,8 @@ def test_fused_step_matches_hashlib(bps):
                 for b in (b for b in step if b is not None):
                     st = gen_md5.simulate_step(st, [b])
             else:
-                st = gen_md5.simulate_step(st, step)
-        assert struct.pack("<4I", *st) == hashlib.md5(msg).digest(), (bps, n)
+                st = gen_md5.simulate_step(st, step, roll=roll)
+        assert struct.pack("<4I", *st) == hashlib.md5(msg).digest(), (bps, n, roll)
 
 
 def test_reads_never_used_or_overwritten_in_flight():
@@ -50,6 +54,37 @@ def test_reads_never_used_or_overwritten_in_flight():
     i = next(k for k, op in enumerate(ops) if op.startswith("s_waitcnt"))
     with pytest.raises(AssertionError, match="read before"):
         gen_md5.simulate(ops[:i] + ops[i + 1:], dict(regs, **{f"v{gen_md5.PIN0 + q}": 0 for q in range(8)}), lds)
+
+
+@pytest.mark.parametrize("k", [0, 1, 4, -1])
+def test_rolling_waits_are_exact(k):
+    """Loosen any one counted wait by one: some row is then read before it landed."""
+    ops = gen_md5.roll_text(4)
+    regs = {f"%[s{q}]": 0 for q in range(4)}
+    regs["%[ad]"] = 0
+    lds = gen_md5.lds_image([bytes(64)] * 4, 0)
+    waits = [i for i, op in enumerate(ops) if op.startswith("s_waitcnt")]
+    i = waits[k]
+    n = int(ops[i].split("(")[1].rstrip(")"))
+    loose = ops[:i] + [f"s_waitcnt lgkmcnt({n + 1})"] + ops[i + 1:]
+    with pytest.raises(AssertionError, match="read before"):
+        gen_md5.simulate(loose, regs, lds)
+
+
+def test_rolling_statement_shape():
+    for bps in (2, 4):
+        ops = gen_md5.roll_text(bps)
+        assert sum(o.startswith("v_") for o in ops) == bps * (256 + 4)
+        assert sum(o.startswith("ds_read_b128") for o in ops) == bps * 16
+        # waits: the step's first row, rows 1..W-1, then every W rows
+        assert sum(o.startswith("s_waitcnt") for o in ops) == 2 + (bps * 16 - 1) // gen_md5.ROLL_WAIT
+        small = [o.startswith(("s_waitcnt", "v_add_u32_e32", "s_nop")) for o in ops]
+        assert sum(small) % 2 == 0
+        for k, o in enumerate(ops):
+            if o.startswith("s_waitcnt"):
+                assert ops[k + 1].startswith(("v_add_u32_e32", "s_nop"))
+        regs = {int(o.split("v[")[1].split(":")[0]) for o in ops if o.startswith("ds_read")}
+        assert regs <= {int(c[1:]) for c in gen_md5.ROLL_CLOBBERS[::4]}
 
 
 def test_statement_shape():

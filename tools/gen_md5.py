@@ -79,12 +79,18 @@ def chunk_reads(c: int, h: int, nxt: bool) -> list[tuple[int, int]]:
 
 
 def step_ops(i: int, wait: bool) -> list[str]:
+    ops = step_ops_k(i, f"v{row_reg(i // 4) + i % 4}")
+    if wait:
+        ops[3:] = ["s_waitcnt lgkmcnt(0)", ops[3].replace("_e64", "_e32")]
+    return ops
+
+
+def step_ops_k(i: int, k: str) -> list[str]:
     """MD5 step i: f = F(b,c,d); t = a + f + (M+K)[i]; t = rotl(t, s); a = b + t.  The names
     rotate (a,b,c,d) -> (d,a,b,c) each step; steps 0-3 read the block-start state s0..s3 and
     write fresh a..d (so s0..s3 survive for the feed-forward)."""
     tt, rot = ROUNDS[i // 16]
     names = "abcd"
-    k = f"v{row_reg(i // 4) + i % 4}"
     if i < 4:
         # live value of each name before step i: s-registers until written
         cur = {"a": "%[s0]", "b": "%[s1]", "c": "%[s2]", "d": "%[s3]"}
@@ -95,14 +101,10 @@ def step_ops(i: int, wait: bool) -> list[str]:
     else:
         A, B, C, D = (f"%[{names[(4 - i + q) % 4]}]" for q in range(4))
         out = A
-    ops = [f"v_bitop3_b32 %[f], {B}, {C}, {D} bitop3:0x{tt:02x}",
-           f"v_add3_u32 %[t], {A}, %[f], {k}",
-           f"v_alignbit_b32 %[t], %[t], %[t], {rot[i % 4]}"]
-    if wait:
-        ops += ["s_waitcnt lgkmcnt(0)", f"v_add_u32_e32 {out}, {B}, %[t]"]
-    else:
-        ops += [f"v_add_u32_e64 {out}, {B}, %[t]"]
-    return ops
+    return [f"v_bitop3_b32 %[f], {B}, {C}, {D} bitop3:0x{tt:02x}",
+            f"v_add3_u32 %[t], {A}, %[f], {k}",
+            f"v_alignbit_b32 %[t], %[t], %[t], {rot[i % 4]}",
+            f"v_add_u32_e64 {out}, {B}, %[t]"]
 
 
 def block_ops(h: int, nxt: bool) -> list[str]:
@@ -123,6 +125,64 @@ def step_text(bps: int) -> list[str]:
     return ops
 
 
+# ----------------------------------------------------------------------------- rolling schedule
+# Round 3 (later): the chunked statement above waits at the end of every chunk for ALL the rows
+# it issued; chunk 0's rows 2-5 have only steps 0-7 (~130 cycles) to land, and the chunked
+# reads leave nothing in flight at a block boundary.  The rolling statement keeps ROLL_DEPTH
+# rows in flight: row g (counting rows over the whole step, 16 per block) is read into slot
+# g % (ROLL_DEPTH + 1) when row g - ROLL_DEPTH starts, and a counted `s_waitcnt lgkmcnt(n)`
+# (LDS reads of one wave return in order) before every ROLL_WAIT-th row lands the next
+# ROLL_WAIT rows, each read >= ROLL_DEPTH - ROLL_WAIT + 1 rows (>= 20 steps) earlier.  Only the
+# step's first row waits a whole LDS latency (the producer writes the step's buffer before
+# the barrier).  Depth 12 / a wait every 8 rows was the best of eight shapes measured
+# (profiles/r03_exp_md5_roll.jsonl: waits cost issue slots, short leads cost stalls):
+# C2 1,278-1,286 -> 1,246 cycles per block (114.2 -> 116.8-117.1 GiB/s), C4 shard 815 -> 845.
+ROLL_DEPTH = int(os.environ.get("S3H_GEN_ROLL_DEPTH", 12))  # (env: experiment builds only)
+ROLL_WAIT = int(os.environ.get("S3H_GEN_ROLL_WAIT", 8))
+ROLL_BASE = min(200, 256 - 4 * (ROLL_DEPTH + 1))  # the ring ends at or below v255
+ROLL_CLOBBERS = [f"v{r}" for r in range(ROLL_BASE, ROLL_BASE + 4 * (ROLL_DEPTH + 1))]
+
+
+def roll_text(bps: int, depth: int = ROLL_DEPTH, wait: int = ROLL_WAIT) -> list[str]:
+    total = 16 * bps
+    slots = depth + 1
+    assert 1 <= wait <= depth <= 15
+
+    def reg(g: int) -> int:
+        return ROLL_BASE + 4 * (g % slots)
+
+    def read(g: int) -> str:
+        off = (g // 16) * BLOCK_BYTES + (g % 16) * ROW_BYTES
+        return f"ds_read_b128 v[{reg(g)}:{reg(g) + 3}], %[ad] offset:{off}"
+
+    def land(b: int) -> str | None:
+        """The wait before row b, or None: rows below `upto` must have landed, and the
+        reads issued so far are rows below min(b + depth, total) (in order)."""
+        if b == 0:
+            upto = 1
+        elif b == 1 or b % wait == 0:
+            upto = min(total, (b // wait + 1) * wait)
+        else:
+            return None
+        return f"s_waitcnt lgkmcnt({min(b + depth, total) - upto})"
+
+    ops = [read(g) for g in range(min(depth, total))]
+    ops += [land(0), "s_nop 0"]  # 4 + 4 bytes: the statement stays 8-byte aligned
+    for h in range(bps):
+        for i in range(64):
+            g = 16 * h + i // 4
+            if i % 4 == 0 and g + depth < total:
+                ops.append(read(g + depth))
+            step = step_ops_k(i, f"v{reg(g) + i % 4}")
+            w = land(g + 1) if i % 4 == 3 and i < 63 else None
+            # a wait goes before the step's last add, re-encoded as 4-byte VOP2 (pairs of 4 B)
+            ops += step if w is None else step[:3] + [w, step[3].replace("_e64", "_e32")]
+        ff = [f"v_add_u32_e64 %[s{q}], %[s{q}], %[{n}]" for q, n in enumerate("abcd")]
+        w = land(16 * (h + 1)) if h + 1 < bps else None
+        ops += ff if w is None else ff[:3] + [w, ff[3].replace("_e64", "_e32")]
+    return ops
+
+
 def emit_inc(path: str) -> None:
     lines = ["// Generated by tools/gen_md5.py -- do not edit.  The MD5 consumer's fused step: all",
              "// kBps blocks of one producer step in one asm statement (rows in fixed registers; see",
@@ -132,6 +192,11 @@ def emit_inc(path: str) -> None:
         ops = step_text(bps)
         lines.append(f"#define S3H_MD5_STEP_ASM_{bps} \\")
         lines += [f'  "{op}\\n\\t" \\' for op in ops]
+        lines.append('  ""')
+    lines.append(f"#define S3H_MD5_ROLL_CLOBBERS {', '.join(chr(34) + c + chr(34) for c in ROLL_CLOBBERS)}")
+    for bps in (2, 4):
+        lines.append(f"#define S3H_MD5_ROLL_ASM_{bps} \\")
+        lines += [f'  "{op}\\n\\t" \\' for op in roll_text(bps)]
         lines.append('  ""')
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
@@ -152,10 +217,11 @@ def _bitop3(tt: int, x: int, y: int, z: int) -> int:
 def simulate(ops: list[str], regs: dict[str, int], lds: dict[int, int]) -> dict[str, int]:
     """Execute `ops` for one lane.  `regs`: named operands ('%[s0]', '%[ad]', ...) and 'vN'
     registers; `lds`: byte address -> 32-bit word.  A ds_read lands at the next
-    s_waitcnt lgkmcnt(0): reading or overwriting one of its registers before that is an error,
+    s_waitcnt lgkmcnt(n) that leaves at most n newer reads in flight: reading or overwriting one of its registers before that is an error,
     as is a read still in flight at the end."""
     regs = dict(regs)
     pending: dict[str, int] = {}
+    fifo: list[list[str]] = []  # registers of each read in flight, oldest first
 
     def get(x: str) -> int:
         x = x.strip()
@@ -174,9 +240,13 @@ def simulate(ops: list[str], regs: dict[str, int], lds: dict[int, int]) -> dict[
         m = re.match(r"(\S+)\s+(.*)$", op)
         name, rest = m.group(1), m.group(2)
         if name == "s_waitcnt":
-            assert rest == "lgkmcnt(0)"
-            regs.update(pending)
-            pending.clear()
+            n = int(re.fullmatch(r"lgkmcnt\((\d+)\)", rest).group(1))
+            assert n <= 15, "lgkmcnt is a 4-bit counter"
+            while len(fifo) > n:  # LDS reads of one wave return in order
+                for reg in fifo.pop(0):
+                    regs[reg] = pending.pop(reg)
+            continue
+        if name == "s_nop":
             continue
         if name == "ds_read_b128":
             mm = re.fullmatch(r"v\[(\d+):(\d+)\], (\S+) offset:(\d+)", rest)
@@ -188,6 +258,8 @@ def simulate(ops: list[str], regs: dict[str, int], lds: dict[int, int]) -> dict[
                 if reg in pending:
                     raise AssertionError(f"two LDS reads in flight into {reg}")
                 pending[reg] = lds[base + 4 * q]
+            fifo.append([f"v{r0 + q}" for q in range(4)])
+            assert len(fifo) <= 15, "more LDS reads in flight than lgkmcnt can count"
             continue
         tt = None
         if " bitop3:" in rest:
@@ -230,12 +302,17 @@ def lds_image(blocks: list[bytes], ad: int) -> dict[int, int]:
     return lds
 
 
-def simulate_step(state: list[int], blocks: list[bytes], ad: int = 0x400) -> list[int]:
+def simulate_step(state: list[int], blocks: list[bytes], ad: int = 0x400,
+                  roll: bool = False) -> list[int]:
     """MD5 state after the fused step over len(blocks) whole blocks (as the kernel runs it:
-    rows 0-1 of block 0 in the pinned registers before the statement)."""
+    chunked -- rows 0-1 of block 0 in the pinned registers before the statement; rolling --
+    the statement reads every row itself)."""
     lds = lds_image(blocks, ad)
     regs = {f"%[s{q}]": state[q] for q in range(4)}
     regs["%[ad]"] = ad
+    if roll:
+        out = simulate(roll_text(len(blocks)), regs, lds)
+        return [out[f"%[s{q}]"] for q in range(4)]
     for q in range(4):
         regs[f"v{PIN0 + q}"] = lds[ad + 4 * q]
         regs[f"v{PIN1 + q}"] = lds[ad + ROW_BYTES + 4 * q]
