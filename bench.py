@@ -298,7 +298,7 @@ def main():
     gpu = local % torch.cuda.device_count() if share else local
     torch.cuda.set_device(gpu)
     if world > 1:
-        dist.init_process_group("gloo")
+        init_gloo(dist)
     dev = torch.device("cuda", gpu)
     local = gpu
 
@@ -467,6 +467,20 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def init_gloo(dist) -> None:
+    """init_process_group("gloo") with the process's stdout pointed at stderr meanwhile: gloo
+    prints "[Gloo] Rank r is connected to ..." on stdout (fd 1, from C++) in every rank, and
+    the bench's stdout must hold exactly one line -- rank 0's JSON."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo")
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def per_rank(dist, world: int, vals):

@@ -6,6 +6,8 @@ shards partition the batch, the reassembled table equals the oracle's, and bench
 workload() uses the same partition."""
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -115,3 +117,22 @@ def test_bench_per_rank_gather_gloo():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got == [[0, 10, 7], [1, 11, 7]]
+
+
+def test_bench_gloo_init_keeps_stdout_clean():
+    """gloo prints "[Gloo] Rank r is connected ..." on stdout from C++ in every rank; bench.py's
+    init_gloo keeps it off stdout, which must carry only rank 0's JSON line (world size 2)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, torch.distributed as dist; sys.path.insert(0, %r); import bench; "
+            "bench.init_gloo(dist); dist.barrier(); "
+            "print('{}') if dist.get_rank() == 0 else None; dist.destroy_process_group()" % root)
+    port = _free_port()
+    procs = [subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True,
+                              env={**os.environ, "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                                   "RANK": str(r), "WORLD_SIZE": "2"})
+             for r in range(2)]
+    outs = [p.communicate(timeout=120) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [o[1][-500:] for o in outs]
+    assert outs[0][0] == "{}\n" and outs[1][0] == ""
+    assert all("[Gloo]" in o[1] for o in outs)  # still printed, on stderr
