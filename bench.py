@@ -437,6 +437,9 @@ def main():
             line["host_resident"] = host_resident(s3, torch, data, ids, lens, offs, gd)
             if not args.no_c5:
                 line["c5_loopback"] = c5_loopback(data, offs, lens, gd)
+        if (world == 1 and args.config == "c2" and args.algo == "sha256" and not args.parts_per_gpu
+                and not args.part_bytes and not args.no_configs):
+            line["f_rows"] = f_rows_c2(s3, torch, data, ids, lens, offs, dev, stream)
         if world == 1 and not args.no_cpu_baseline:
             n = min(args.cpu_sample_parts, len(lens))
             end = int(offs[n - 1] + lens[n - 1])
@@ -518,6 +521,52 @@ def host_resident(s3, torch, data, ids, lens, offs, gd, reps: int = 3):
            "fixture_mismatches": _fixture_mismatches(s3, ids, out),
            "digests_match_device_run": bool(np.array_equal(out, gd))}
     del host, h, views
+    return res
+
+
+def f_rows_c2(s3, torch, data, ids, lens, offs, dev, stream, steps: int = 3) -> dict:
+    """SURVEY 8(f) kernels on the C2 parts already resident, so the driver's default run also
+    records them: Content-MD5 alone (md5_pc_kernel, HIP-event kernel time) and both upload
+    digests from one pass (s3h_sha256_md5_batch_device, wall time per call incl. its sync),
+    each with fixture parity (lib/hash SHA-256 and md5_file goldens)."""
+    gib = float(lens.sum()) / 2**30
+    plan = s3.Plan(offs, lens, device=dev.index, algo="md5")
+    out = torch.zeros((len(lens), plan.words), dtype=torch.int32, device=dev)
+    plan.launch(data, out, stream)
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    for a, b in ev:
+        a.record(stream)
+        plan.launch(data, out, stream)
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    plan.status(stream)  # device error word clear (raises otherwise)
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    m5 = out.cpu().numpy().view(np.uint32)
+    mf = golden_fixtures("c2", "md5")
+    chk = [k for k, p in enumerate(ids) if int(p) in mf]
+    bad = sum(s3.digests_to_text(m5[k:k + 1], 4)[0] != mf[int(ids[k])] for k in chk)
+    plan.close()
+    res = {"md5": {"metric": "device-resident MD5 GiB/s (Content-MD5), C2 parts",
+                   "kernel": "md5-pc", "GiBps": round(gib / (kern_ms / 1e3), 3),
+                   "kernel_ms": round(kern_ms, 3), "steps": steps,
+                   "parity": {"fixtures_checked": len(chk), "mismatches": int(bad)}}}
+    del out
+    sha, m5 = s3.sha256_md5_batch_device(data, offs, lens, stream=stream)
+    torch.cuda.synchronize(dev)
+    times = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        sha, m5 = s3.sha256_md5_batch_device(data, offs, lens, stream=stream)
+        times.append(time.perf_counter() - t0)
+    bad = _fixture_mismatches(s3, ids, sha.cpu().numpy().view(np.uint32), m5.cpu().numpy().view(np.uint32))
+    wall = float(np.mean(times))
+    res["sha256_md5"] = {"metric": "device-resident SHA-256 + MD5 GiB/s (both digests, one pass), "
+                                   "C2 parts", "GiBps": round(gib / wall, 3),
+                         "ms_per_call": round(wall * 1e3, 3), "steps": steps,
+                         "fixture_mismatches": int(bad)}
+    del sha, m5
     return res
 
 
