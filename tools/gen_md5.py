@@ -168,6 +168,34 @@ def roll_text(bps: int, depth: int = ROLL_DEPTH, wait: int = ROLL_WAIT) -> list[
 
     ops = [read(g) for g in range(min(depth, total))]
     ops += [land(0), "s_nop 0"]  # 4 + 4 bytes: the statement stays 8-byte aligned
+    ops = _exp(ops + _roll_body(bps, depth, total, read, land, reg))
+    return ops
+
+
+def _exp(ops: list[str]) -> list[str]:
+    """Timing-only experiment variants (S3H_GEN_EXP; wrong digests, never the product):
+    nowait0 -- the step's first wait removed; nolds -- every ds_read_b128 becomes an 8-byte
+    v_mov_b32_e64 of its first register (one issue slot, no LDS traffic) and every wait an
+    s_nop 0."""
+    mode = os.environ.get("S3H_GEN_EXP", "")
+    if mode == "nowait0":
+        i = next(k for k, o in enumerate(ops) if o.startswith("s_waitcnt"))
+        return ops[:i] + ["s_nop 0"] + ops[i + 1:]
+    if mode == "nolds":
+        out = []
+        for o in ops:
+            if o.startswith("ds_read"):
+                out.append(f"v_mov_b32_e64 v{o.split('v[')[1].split(':')[0]}, 0")
+            elif o.startswith("s_waitcnt"):
+                out.append("s_nop 0")
+            else:
+                out.append(o)
+        return out
+    return ops
+
+
+def _roll_body(bps, depth, total, read, land, reg) -> list[str]:
+    ops = []
     for h in range(bps):
         for i in range(64):
             g = 16 * h + i // 4
