@@ -290,6 +290,25 @@ def test_md5_host_path_transfer_etag(torch_cuda, golden):
         assert s3.multipart_etag(d) == golden["md5"]["transfer_etag"]
 
 
+@pytest.mark.parametrize("slice_blocks", [5, 7, 9])
+def test_md5_odd_slices_mix_full_and_partial_steps(torch_cuda, oracle, slice_blocks):
+    """Host path with slices of an odd number of 64-B blocks: every resumable launch starts
+    mid-part at a block offset that is not a multiple of the 4-block producer step, so each
+    one runs full steps through the rolling fused statement and a partial step through the
+    checked per-block path, the chaining state carried between launches (MD5 alone and both
+    digests), vs the oracle."""
+    rng = np.random.default_rng(slice_blocks)
+    lens = rng.integers(0, 5000, 90)
+    lens[:3] = [0, 64 * slice_blocks, 64 * slice_blocks * 3 + 55]
+    parts = [rng.integers(0, 256, int(L), dtype=np.uint8) for L in lens]
+    want = np.stack([oracle.md5(p.tobytes()) for p in parts])
+    got = s3.md5_batch_host(parts, slice_bytes=64 * slice_blocks)
+    assert np.array_equal(got, want)
+    sha, m5 = s3.sha256_md5_batch_host(parts, slice_bytes=64 * slice_blocks)
+    assert np.array_equal(m5, want)
+    assert np.array_equal(sha, np.stack([oracle.sha256(p.tobytes()) for p in parts]))
+
+
 def test_verify_download_parts(torch_cuda, golden):
     """Download-side verification: one corrupted byte flags exactly its part."""
     t = golden["transfer"]
