@@ -117,6 +117,10 @@ int s3h_plan_info(s3h_plan_t plan, uint64_t *n, uint64_t *total_blocks, uint64_t
  * many leading workgroups of the two-group skew kernel run one group on a CU of their own
  * (the groups of the longest parts of a ragged batch). */
 int s3h_plan_groups(s3h_plan_t plan, uint32_t *groups, uint32_t *solo);
+/* SHA-256 + MD5 of a SHA-256 plan's parts (s3h_sha256_md5_batch_*): how many leading
+ * workgroups of the one-grid dual kernel run the longest parts as 8-part skew groups (a
+ * ragged batch of 2,049 - 32 x CUs parts); 0 when the dual pass uses another form. */
+int s3h_plan_dual_solo(s3h_plan_t plan, uint32_t *solo);
 
 /* Measurement hook (not part of the lib/hash surface): while d_clocks (device memory,
  * 4 x *waves uint64) is set, every launch of a plan on the skew kernel records, per consumer

@@ -37,6 +37,7 @@ C_ABI_SYMBOLS = (
     "s3h_sha256_md5_batch_host", "s3h_sha256_md5_batch_device", "s3h_trim",
     "s3h_sha256_file_parts", "s3h_sha256_batch_host_on", "s3h_plan_groups",
     "s3h_sha256_md5_file_parts", "s3h_plan_status", "s3h_stream_status", "s3h_host_threads",
+    "s3h_plan_dual_solo",
 )
 ALGO_SHA256, ALGO_MD5 = 0, 1
 ALGO_IDS = {"sha256": ALGO_SHA256, "md5": ALGO_MD5}
@@ -101,6 +102,7 @@ def lib() -> ctypes.CDLL:
             L.s3h_plan_info.argtypes = [ctypes.c_void_p, u64p, u64p, u64p,
                                         ctypes.POINTER(ctypes.c_int), u32p]
             L.s3h_plan_groups.argtypes = [ctypes.c_void_p, u32p, u32p]
+            L.s3h_plan_dual_solo.argtypes = [ctypes.c_void_p, u32p]
             L.s3h_sha256_batch_device.argtypes = [ctypes.c_int, ctypes.c_void_p, u64p, u64p,
                                                   ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
             for name in ("s3h_sha256_batch_host", "s3h_md5_batch_host"):

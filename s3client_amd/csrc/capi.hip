@@ -92,6 +92,7 @@ struct s3h_plan_s {
   uint8_t* d_zero = nullptr;    // 256 zero bytes: load target for out-of-range lanes
   int quad_waves = 1;           // skew / quad kernels: consumer waves per workgroup (1-2)
   uint32_t solo = 0;            // two-group skew grid: leading one-group workgroups (plan_solo)
+  uint32_t dual_solo = 0;       // SHA-256 + MD5 of a ragged batch: skew groups of the mixed grid
   uint64_t* d_clocks = nullptr; // clock probe buffer (caller-owned), see s3h_plan_set_clock_probe
   uint32_t* d_err = nullptr;    // device error word (s3h::kErr* bits), read by plan_check
 };
@@ -187,6 +188,31 @@ uint32_t plan_solo(const s3h::Slot* slots, uint64_t n, uint64_t cus) {
   return 0;
 }
 
+// Both digests of 2,049-8,192 parts (sha256_md5_group_kernel) run every chain at skewp's rate
+// beside a self-fed MD5 wave: ~2,550 cycles per block (C4 shard, 457 GiB/s for both), against
+// ~2,280 for a skew group with its MD5 wave on a CU of its own (kDualGroupSkew: 125 vs 121.5
+// ms for 8 MiB parts).  A ragged batch is timed by its longest parts, so
+// sha256_md5_group_mixed_kernel gives the longest F x 8 slots skew groups and the rest skewp
+// groups: F = the fewest 8-slot groups after which every remaining part, at the skewp rate,
+// ends before the longest part does at the skew rate; 0 (the plain group kernel) when that
+// grid would not fit one workgroup per CU (e.g. equal lengths) or there is nothing to gain.
+constexpr double kDualSkewpOverSkew = 2550.0 / 2280.0;
+uint32_t dual_mixed_solo(const s3h::Slot* slots, uint64_t n, uint64_t cus) {
+  constexpr uint64_t kSkew = 8, kSkewp = 32;
+  if (n <= 2048 || cus == 0 || (n + kSkewp - 1) / kSkewp > cus) return 0;
+  const double longest = double(s3h::nblocks(slots[0].len));
+  uint64_t lo = 0, hi = n;  // first slot whose part ends in time at the skewp rate
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) / 2;
+    if (double(s3h::nblocks(slots[mid].len)) * kDualSkewpOverSkew > longest) lo = mid + 1;
+    else hi = mid;
+  }
+  const uint64_t F = (lo + kSkew - 1) / kSkew;
+  if (F == 0 || F * kSkew >= n) return 0;
+  const uint64_t wgs = F + (n - F * kSkew + kSkewp - 1) / kSkewp;
+  return wgs <= cus ? uint32_t(F) : 0u;
+}
+
 uint64_t sort_slots(const uint64_t* offsets, const uint64_t* lengths, uint64_t n, bool nopad,
                     s3h::Slot* slots, uint32_t* order) {
   std::iota(order, order + n, 0u);
@@ -272,6 +298,7 @@ int plan_geometry(s3h_plan_s* P, const uint64_t* offsets, const uint64_t* length
     P->solo = plan_solo(h_slots, n, uint64_t(device_cus(P->device)));
 #endif
   }
+  P->dual_solo = P->algo == S3H_ALGO_SHA256 ? dual_mixed_solo(h_slots, n, uint64_t(device_cus(P->device))) : 0;
   P->grid = P->solo ? P->solo + uint32_t(((n + 7) / 8 - P->solo + 1) / 2)
             : P->kernel == S3H_KERNEL_PC ? uint32_t((n + 63) / 64)
             : P->kernel == S3H_KERNEL_PAIR || P->kernel == S3H_KERNEL_SKEWP
@@ -353,6 +380,9 @@ int plan_check(s3h_plan_s* P, hipStream_t s) {
 // Dynamic LDS added to a grid with solo workgroups: 72 KiB of groups + 12 KiB > half of the
 // CU's 160 KiB, so one workgroup per CU and a solo group never shares its CU.
 constexpr uint32_t kSoloLdsPad = 12 * 1024;
+// sha256_md5_group_mixed_kernel: 66 KiB of skewp LDS + this > half of the CU's 160 KiB.
+constexpr uint32_t kMixedLdsPad = 16 * 1024;
+static_assert(sizeof(s3h::SkewLds<1, true>) + kMixedLdsPad > 80 * 1024, "one mixed workgroup per CU");
 
 int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t* d_state,
                 uint64_t b0, uint64_t b1, uint64_t origin, uint32_t flags, const uint64_t* d_bits,
@@ -417,7 +447,9 @@ int plan_launch(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint64_t
 // S's workgroups then M's, all within one workgroup per CU); kDualGroup =
 // sha256_md5_group_kernel (skewp: each workgroup runs a SHA-256 group and a self-fed MD5 wave
 // over the same 32 parts, S->grid <= one per CU); kDualNone = two launches on two streams.
-enum DualMode { kDualNone = 0, kDualSplit = 1, kDualGroup = 2, kDualGroupSkew = 3 };
+// kDualGroupMixed = sha256_md5_group_mixed_kernel (ragged 2,049-8,192 parts: the longest
+// parts in skew groups, the rest as kDualGroup; S->dual_solo skew workgroups).
+enum DualMode { kDualNone = 0, kDualSplit = 1, kDualGroup = 2, kDualGroupSkew = 3, kDualGroupMixed = 4 };
 
 DualMode dual_mode(const s3h_plan_s* S, const s3h_plan_s* M, uint64_t b0, uint64_t b1) {
   if (M->algo != S3H_ALGO_MD5 || S->algo != S3H_ALGO_SHA256 || b1 - b0 >= (1ull << 31) ||
@@ -443,6 +475,9 @@ DualMode dual_mode(const s3h_plan_s* S, const s3h_plan_s* M, uint64_t b0, uint64
 #ifdef S3H_EXP_NO_GROUP_NC2  // tools/ experiment builds only: round-2 behaviour
   if (S->kernel == S3H_KERNEL_SKEW) return kDualNone;
 #endif
+#ifndef S3H_EXP_NO_DUAL_MIXED  // tools/ experiment builds only: round-2/3 behaviour
+  if (group_ok && S->dual_solo > 0) return kDualGroupMixed;
+#endif
   if (group_ok && (S->n + 31) / 32 <= cus) return kDualGroup;
   return kDualNone;
 }
@@ -463,6 +498,10 @@ int dual_launch(s3h_plan_s* S, s3h_plan_s* M, const void* d_base, uint32_t* d_sh
   if (mode == kDualGroup)
     hipLaunchKernelGGL(s3h::sha256_md5_group_kernel<true>, dim3(uint32_t((S->n + 31) / 32)),
                        dim3(192), 0, stream, A, B);
+  else if (mode == kDualGroupMixed)  // the LDS pad keeps one workgroup per CU
+    hipLaunchKernelGGL(s3h::sha256_md5_group_mixed_kernel,
+                       dim3(uint32_t(S->dual_solo + (S->n - 8ull * S->dual_solo + 31) / 32)),
+                       dim3(192), kMixedLdsPad, stream, A, B, S->dual_solo);
   else if (mode == kDualGroupSkew)
     hipLaunchKernelGGL(s3h::sha256_md5_group_kernel<false>, dim3(uint32_t((S->n + 7) / 8)),
                        dim3(192), 0, stream, A, B);
@@ -1033,6 +1072,8 @@ int plan_refill(s3h_plan_s* P, const uint64_t* offsets, const uint64_t* lengths,
     const uint64_t groups = (P->n + 7) / 8;
     P->grid = uint32_t(P->solo + (groups - P->solo + 1) / 2);
   }
+  P->dual_solo = P->algo == S3H_ALGO_SHA256 && !nopad
+                     ? dual_mixed_solo(h_slots, P->n, uint64_t(device_cus(P->device))) : 0;
   HIP_TRY(hipMemcpyAsync(P->d_slots, h_slots, P->n * sizeof(s3h::Slot), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(P->d_out_idx, h_order, P->n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   return S3H_OK;
@@ -1442,6 +1483,12 @@ int s3h_plan_groups(s3h_plan_t P, uint32_t* groups, uint32_t* solo) {
   if (!P) return fail(S3H_EINVAL, "null plan");
   if (groups) *groups = consumer_groups(P);
   if (solo) *solo = P->solo;
+  return S3H_OK;
+}
+
+int s3h_plan_dual_solo(s3h_plan_t P, uint32_t* solo) {
+  if (!P || !solo) return fail(S3H_EINVAL, "plan dual solo: null argument");
+  *solo = P->dual_solo;
   return S3H_OK;
 }
 

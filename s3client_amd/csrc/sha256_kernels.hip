@@ -1873,6 +1873,44 @@ __global__ __launch_bounds__(192) void sha256_md5_group_kernel(LaunchArgs S, Lau
     skew_body<1, PAIR, true>(S, blockIdx.x, wave >> 1, LS, flags);
 }
 
+// sha256_md5_group_mixed_kernel: both digests of a RAGGED batch (2,049-8,192 parts, e.g.
+// BASELINE C3) whose time is set by its longest parts.  The group kernel above runs every part
+// at skewp's chain rate (2,476 cycles/block); here the first `F` workgroups take the 8F
+// longest slots as skew-layout groups (8 parts, one consumer at the skew kernel's 8 VALU per
+// round, ~2,280 cycles/block beside its MD5 wave), the rest the group kernel's 32-part skewp
+// groups over slots 8F.. (their shorter parts finish in time at the slower rate).  The host
+// picks F (capi.hip dual_mixed_solo) and launches at most one workgroup per CU (LDS pad).
+// Both bodies index slots from their own group number, so the skewp half runs on LaunchArgs
+// whose slot / out_idx arrays start at slot 8F; the clock probe is off (two group numberings).
+__global__ __launch_bounds__(192) void sha256_md5_group_mixed_kernel(LaunchArgs S, LaunchArgs M,
+                                                                    uint32_t F) {
+  __shared__ union {
+    SkewLds<1, false> skew;
+    SkewLds<1, true> skewp;
+  } L;
+  __shared__ uint32_t flags[2];
+  if (threadIdx.x < 2) flags[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  S.clocks = nullptr;
+  if (blockIdx.x < F) {
+    if (wave == 1)
+      md5_self_body<SkewGeom<1, false>::kParts>(M, blockIdx.x);
+    else
+      skew_body<1, false, true>(S, blockIdx.x, wave >> 1, L.skew, flags);
+    return;
+  }
+  constexpr uint32_t kSolo = SkewGeom<1, false>::kParts;
+  const uint32_t shift = kSolo * F;
+  if (shift >= S.n) return;
+  S.slots += shift; S.out_idx += shift; S.n -= shift;
+  M.slots += shift; M.out_idx += shift; M.n -= shift;
+  if (wave == 1)
+    md5_self_body<SkewGeom<1, true>::kParts>(M, blockIdx.x - F);
+  else
+    skew_body<1, true, true>(S, blockIdx.x - F, wave >> 1, L.skewp, flags);
+}
+
 // ------------------------------------------------------------- verification
 // Download-side verification (ranged GETs of lib/src/download.cpp:88-103):
 // mismatch[i] = digest(i) != expected(i), words compared as stored.

@@ -79,9 +79,11 @@ class Plan:
                                   ctypes.byref(k), ctypes.byref(g)))
         groups, solo = ctypes.c_uint32(), ctypes.c_uint32()
         check(lib().s3h_plan_groups(self._h, ctypes.byref(groups), ctypes.byref(solo)))
+        dual_solo = ctypes.c_uint32()
+        check(lib().s3h_plan_dual_solo(self._h, ctypes.byref(dual_solo)))
         return {"n": n.value, "total_blocks": tb.value, "max_blocks": mb.value,
                 "kernel": _native.KERNEL_NAMES[k.value], "grid": g.value,
-                "groups": groups.value, "solo": solo.value}
+                "groups": groups.value, "solo": solo.value, "dual_solo": dual_solo.value}
 
     def set_clock_probe(self, clocks=None) -> int:
         """Record per-consumer-wave clock counters on later launches (skew kernel only):

@@ -290,6 +290,33 @@ def test_md5_host_path_transfer_etag(torch_cuda, golden):
         assert s3.multipart_etag(d) == golden["md5"]["transfer_etag"]
 
 
+@pytest.mark.parametrize("n", [2100, 3000, 6000])
+def test_dual_mixed_grid_ragged(torch_cuda, oracle, n):
+    """SHA-256 + MD5 of a ragged batch in the skewp-group range (C3-like lengths, scaled):
+    the one-grid mixed kernel (the longest parts in skew groups, the rest in skewp groups,
+    slot arrays offset for the second half) vs the oracle, device- and host-resident; equal
+    lengths keep the plain group kernel (dual_solo 0)."""
+    rng = np.random.default_rng(n)
+    lens = 5 * 1024 + rng.integers(0, 59 * 1024 + 1, n)
+    lens[:5] = [64 * 1024, 64 * 1024 - 1, 0, 55, 64 * 1024 + 9]
+    offs = np.concatenate([[0], np.cumsum(lens + 7)[:-1]])
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    with s3.Plan(offs, lens) as plan:
+        solo = plan.info()["dual_solo"]
+    assert 0 < solo and 8 * solo < n
+    data = _dev_buffer(torch_cuda, host)
+    sha, m5 = s3.sha256_md5_batch_device(data, offs, lens)
+    want_sha, want_md5 = oracle.batch(host, offs, lens), oracle.md5_batch(host, offs, lens)
+    assert np.array_equal(sha.cpu().numpy().view(np.uint32), want_sha)
+    assert np.array_equal(m5.cpu().numpy().view(np.uint32), want_md5)
+    views = [host[int(o):int(o) + int(L)] for o, L in zip(offs, lens)]
+    hsha, hm5 = s3.sha256_md5_batch_host(views)
+    assert np.array_equal(hsha, want_sha) and np.array_equal(hm5, want_md5)
+    eq = np.full(n, 20000, dtype=np.uint64)
+    with s3.Plan(np.arange(n, dtype=np.uint64) * 20000, eq) as plan:
+        assert plan.info()["dual_solo"] == 0
+
+
 @pytest.mark.parametrize("slice_blocks", [5, 7, 9])
 def test_md5_odd_slices_mix_full_and_partial_steps(torch_cuda, oracle, slice_blocks):
     """Host path with slices of an odd number of 64-B blocks: every resumable launch starts
