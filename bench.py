@@ -607,17 +607,47 @@ def single_gpu_config(s3, torch, dev, cfg: str, steps: int = 2) -> dict:
     bad = sum(s3_hex(gd[k]) != fx[int(ids[k])] for k in checked)
     info = plan.info()
     plan.close()
+    dual = _dual_on(s3, torch, dev, data, ids, lens, offs, cfg, stream, gd, info) if cfg == "c3" else None
     del data, out
     torch.cuda.empty_cache()
     part_bytes = float(lens.sum())
     algo = part_bytes + 32 * len(lens)
-    return {"workload": name, "kernel": info["kernel"], "grid": info["grid"],
+    res = {"workload": name, "kernel": info["kernel"], "grid": info["grid"],
             "solo_workgroups": info["solo"], "steps": steps,
             "GiBps": round(part_bytes / 2**30 / wall, 3), "ms_per_step": round(1e3 * wall, 3),
             "kernel_ms": round(kern_ms, 3),
             "hbm_roofline_frac": round(algo / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5),
             "bound": "the longest part's chain" if cfg == "c3" else "per-wave issue of 8,192 chains",
             "parity": {"fixtures_checked": len(checked), "mismatches": int(bad)}}
+    if dual:
+        res["sha256_md5"] = dual
+    return res
+
+
+def _dual_on(s3, torch, dev, data, ids, lens, offs, cfg, stream, gd, info, steps: int = 2) -> dict:
+    """SHA-256 + MD5 of the same resident parts in one pass (s3h_sha256_md5_batch_device: for
+    C3 the mixed grid, info["dual_solo"] skew workgroups), wall time per call incl. its sync;
+    SHA-256 digests must equal the SHA-256-only run's, MD5 checked against the lib/hash
+    md5_file fixtures."""
+    sha, m5 = s3.sha256_md5_batch_device(data, offs, lens, stream=stream)
+    torch.cuda.synchronize(dev)
+    times = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        sha, m5 = s3.sha256_md5_batch_device(data, offs, lens, stream=stream)
+        times.append(time.perf_counter() - t0)
+    wall = float(np.mean(times))
+    same = bool(np.array_equal(sha.cpu().numpy().view(np.uint32), gd))
+    mf = golden_fixtures(cfg, "md5")
+    m5h = m5.cpu().numpy().view(np.uint32)
+    chk = [k for k, p in enumerate(ids) if int(p) in mf]
+    bad = sum(s3.digests_to_text(m5h[k:k + 1], 4)[0] != mf[int(ids[k])] for k in chk)
+    del sha, m5
+    return {"metric": "device-resident SHA-256 + MD5 GiB/s (both digests, one pass)",
+            "GiBps": round(float(lens.sum()) / 2**30 / wall, 3), "ms_per_call": round(wall * 1e3, 2),
+            "steps": steps, "dual_solo_workgroups": info.get("dual_solo", 0),
+            "sha256_equals_sha256_only_run": same,
+            "md5_parity": {"fixtures_checked": len(chk), "mismatches": int(bad)}}
 
 
 def c5_loopback(data, offs, lens, gd, nparts: int = 128, jobs: int = 16, repeat: int = 2):
@@ -835,14 +865,14 @@ def host_mode(args, s3, torch, dist, data, ids, lens, offs, world, rank, name):
 def golden_fixtures(cfg: str, algo: str, part_bytes: int = 0) -> dict:
     """{global part id: hex digest} of the committed lib/hash fixtures that apply to this
     workload's parts: generator-G 8 MiB parts (C2 / C4 ids and four parts of every rank's
-    shard at N = 2, 4, 8; MD5: the C2 ids) or the C3 parts (SHA-256 only); none for a
-    --part-bytes override."""
+    shard at N = 2, 4, 8; MD5: the C2 ids) or the C3 parts; none for a --part-bytes
+    override."""
     if part_bytes:
         return {}
     with open(os.path.join(ROOT, "tests", "golden", "sha256_golden.json")) as f:
         gold = json.load(f)
     if algo == "md5":
-        src = [] if cfg == "c3" else gold["md5"]["c2_parts"]
+        src = gold["md5"]["c3_parts"] if cfg == "c3" else gold["md5"]["c2_parts"]
     else:
         src = (gold["c3_parts"] if cfg == "c3"
                else gold["c2_parts"] + gold["c4_parts"] + gold["shard_parts"])

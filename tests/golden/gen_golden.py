@@ -207,7 +207,7 @@ def main():
 
     # 9. MD5 (lib/hash/md5.cpp, SURVEY 8(f) "next"): md5_file digests (empty files make the
     #    reference exit, so L >= 1), md5_stream whole-block states, C2/transfer parts, ETag
-    md = {"edge": [], "stream": [], "c2_parts": [], "transfer": []}
+    md = {"edge": [], "stream": [], "c2_parts": [], "c3_parts": [], "transfer": []}
     for L in [1, 3, 55, 56, 57, 63, 64, 65, 119, 120, 128, 1000, 4096, 65536, (1 << 20) + 13,
               (16 << 20), (16 << 20) + 1]:
         md["edge"].append({"p": 7, "L": L, "digest": ref_md5(ref, big[:L] if L <= len(big)
@@ -218,6 +218,9 @@ def main():
         md["stream"].append({"p": 7, "L": L, "state": [int(x) for x in h]})
     for p in (0, 1, 1023):
         md["c2_parts"].append({"p": p, "L": L8, "digest": ref_md5(ref, gen(orc, p, L8))})
+    # the C3 fixture parts (the dual SHA-256 + MD5 pass over BASELINE configs[2])
+    for p in c3ids:
+        md["c3_parts"].append({"p": p, "L": c3all[p], "digest": ref_md5(ref, gen(orc, p, c3all[p]))})
     size = 38000007
     tdata = (np.arange(size, dtype=np.uint64) % 128).astype(np.uint8).tobytes()
     for prt in out["transfer"]["parts"]:

@@ -107,6 +107,10 @@ def test_md5_oracle_golden(oracle, golden):
         assert list(oracle.md5_stream(iv, big[:s["L"]])) == s["state"], s["L"]
     for e in md["c2_parts"][:1]:
         assert oracle.md5(oracle.generate(e["p"], e["L"])).tobytes().hex() == e["digest"]
+    # C3 fixture parts (the shortest and part 0; the rest are checked on the GPU by bench.py)
+    c3 = sorted(md["c3_parts"], key=lambda e: e["L"])
+    for e in (c3[0], next(x for x in md["c3_parts"] if x["p"] == 0)):
+        assert oracle.md5(oracle.generate(e["p"], e["L"])).tobytes().hex() == e["digest"], e["p"]
 
 
 def test_cpu_baseline_restatement_matches_goldens(oracle, golden):
