@@ -463,7 +463,10 @@ def main():
         if not args.no_host_resident:
             dist.barrier()  # the other ranks wait while rank 0 drives every GPU from the host
             if rank == 0:
-                line["host_resident"] = host_resident_multi(s3, torch, dev, world)
+                try:  # rank 0 alone between two barriers: a failure here must not lose the line
+                    line["host_resident"] = host_resident_multi(s3, torch, dev, world)
+                except Exception as e:  # noqa: BLE001 -- reported in the line instead
+                    line["host_resident"] = {"error": f"{type(e).__name__}: {e}"}
             dist.barrier()
     if rank == 0:
         print(json.dumps(line), flush=True)
