@@ -434,24 +434,24 @@ def main():
         }
         if (world == 1 and args.config == "c2" and args.algo == "sha256" and not args.parts_per_gpu
                 and not args.part_bytes and not args.no_host_resident):
-            line["host_resident"] = host_resident(s3, torch, data, ids, lens, offs, gd)
+            line["host_resident"] = _guard(host_resident, s3, torch, data, ids, lens, offs, gd)
             if not args.no_c5:
-                line["c5_loopback"] = c5_loopback(data, offs, lens, gd)
+                line["c5_loopback"] = _guard(c5_loopback, data, offs, lens, gd)
         if (world == 1 and args.config == "c2" and args.algo == "sha256" and not args.parts_per_gpu
                 and not args.part_bytes and not args.no_configs):
-            line["f_rows"] = f_rows_c2(s3, torch, data, ids, lens, offs, dev, stream)
+            line["f_rows"] = _guard(f_rows_c2, s3, torch, data, ids, lens, offs, dev, stream)
         if world == 1 and not args.no_cpu_baseline:
             n = min(args.cpu_sample_parts, len(lens))
             end = int(offs[n - 1] + lens[n - 1])
             host = data[:end].cpu().numpy()
-            line["cpu_baseline"] = cpu_baseline(host, offs, lens, gd, n, args.algo)
+            line["cpu_baseline"] = _guard(cpu_baseline, host, offs, lens, gd, n, args.algo)
             del host
         if (world == 1 and args.config == "c2" and args.algo == "sha256" and not args.parts_per_gpu
                 and not args.part_bytes and not args.no_configs):
             del data, digests
             plan.close()
             torch.cuda.empty_cache()
-            line["configs"] = {c: single_gpu_config(s3, torch, dev, c) for c in ("c3", "c4")}
+            line["configs"] = {c: _guard(single_gpu_config, s3, torch, dev, c) for c in ("c3", "c4")}
     if world > 1 and args.config == "c2" and args.algo == "sha256":
         del data, digests
         plan.close()
@@ -473,6 +473,17 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def _guard(fn, *args):
+    """A sub-measurement of the line (rank 0, after the timed region and its parity): an
+    exception is reported in its place instead of losing the metric line."""
+    try:
+        return fn(*args)
+    except Exception as e:  # noqa: BLE001 -- reported in the line
+        import traceback
+        traceback.print_exc(file=sys.stderr)
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
 def init_gloo(dist) -> None:

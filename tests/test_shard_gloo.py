@@ -136,3 +136,11 @@ def test_bench_gloo_init_keeps_stdout_clean():
     assert all(p.returncode == 0 for p in procs), [o[1][-500:] for o in outs]
     assert outs[0][0] == "{}\n" and outs[1][0] == ""
     assert all("[Gloo]" in o[1] for o in outs)  # still printed, on stderr
+
+
+def test_bench_guard_reports_a_failed_sub_measurement():
+    """A sub-measurement that raises becomes {"error": ...} in the line; the metric survives."""
+    import bench
+    assert bench._guard(lambda a, b: a + b, 2, 3) == 5
+    got = bench._guard(lambda: 1 / 0)
+    assert got == {"error": "ZeroDivisionError: division by zero"}
