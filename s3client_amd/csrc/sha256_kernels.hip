@@ -1445,12 +1445,31 @@ __device__ __forceinline__ void md5_step_roll(uint32_t& s0, uint32_t& s1, uint32
     [c] "=&v"(c), [d] "=&v"(d), [f] "=&v"(f), [t] "=&v"(t)                                    \
   : [ad] "v"(ad)                                                                              \
   : S3H_MD5_ROLL_CLOBBERS, "memory"
+#ifndef S3H_MD5_VMEM  // (the VMEM experiment's statements take other operands)
   if constexpr (kBps == 4)
     asm volatile(S3H_ALIGN8 S3H_MD5_ROLL_ASM_4 S3H_MD5_ROLL_OPERANDS);
   else
     asm volatile(S3H_ALIGN8 S3H_MD5_ROLL_ASM_2 S3H_MD5_ROLL_OPERANDS);
+#endif
 #undef S3H_MD5_ROLL_OPERANDS
 }
+
+#ifdef S3H_MD5_VMEM  // experiment (timing only; tools/gen_md5.py S3H_GEN_EXP=vmem): rows from L2
+__device__ __forceinline__ void md5_step_vmem(uint32_t& s0, uint32_t& s1, uint32_t& s2,
+                                              uint32_t& s3, uint32_t voff, const uint8_t* region) {
+  uint32_t a, b, c, d, f, t;
+  const uint64_t r = uint64_t(reinterpret_cast<uintptr_t>(region));
+#define S3H_SB(k) [sb##k] "s"(r + (k) * 4096ull)
+  asm volatile(S3H_ALIGN8 S3H_MD5_ROLL_ASM_4
+               : [s0] "+v"(s0), [s1] "+v"(s1), [s2] "+v"(s2), [s3] "+v"(s3), [a] "=&v"(a),
+                 [b] "=&v"(b), [c] "=&v"(c), [d] "=&v"(d), [f] "=&v"(f), [t] "=&v"(t)
+               : [voff] "v"(voff), S3H_SB(0), S3H_SB(1), S3H_SB(2), S3H_SB(3), S3H_SB(4),
+                 S3H_SB(5), S3H_SB(6), S3H_SB(7), S3H_SB(8), S3H_SB(9), S3H_SB(10), S3H_SB(11),
+                 S3H_SB(12), S3H_SB(13), S3H_SB(14), S3H_SB(15)
+               : S3H_MD5_ROLL_CLOBBERS, "memory");
+#undef S3H_SB
+}
+#endif
 
 // Decoded message words of MD5 block `blk` (zeros past the launch's range, padding at the end).
 __device__ __forceinline__ void md5_decode(const RawBlock& r, uint32_t sel, const uint8_t* bp,
@@ -1753,6 +1772,13 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
     // with no test (the loop tools/isa_counts.py counts); the ragged tail pays the selects.
     auto step = [&](uint64_t j, bool check) {
       const uint32_t buf = uint32_t(j & 1);
+#ifdef S3H_MD5_VMEM
+      if (kBps == 4 && !check) {  // timing only: rows from a 64 KiB region per workgroup
+        md5_step_vmem(st[0], st[1], st[2], st[3], lane * 16u, A.base + 65536ull * group);
+        S3H_MD5_SYNC();
+        return;
+      }
+#endif
 #if S3H_EXP_MD5_ROLL
       if (kBps > 1 && !check) {
         md5_step_roll<(kBps > 1 ? kBps : 2)>(st[0], st[1], st[2], st[3], row_addr(buf, 0));

@@ -178,6 +178,22 @@ def _exp(ops: list[str]) -> list[str]:
     v_mov_b32_e64 of its first register (one issue slot, no LDS traffic) and every wait an
     s_nop 0."""
     mode = os.environ.get("S3H_GEN_EXP", "")
+    if mode == "vmem":
+        # rows from global memory instead of LDS (timing only): row g of the step is at byte
+        # g * 1024 of a per-workgroup region; base %[sb<g//4>] (SGPR pair) + lane offset
+        # %[voff] + immediate (g % 4) * 1024 (the 13-bit signed immediate holds < 4 KiB)
+        out = []
+        for o in ops:
+            if o.startswith("ds_read"):
+                reg = o.split(" ")[1].rstrip(",")
+                off = int(o.rsplit(":", 1)[1])
+                g = (off // BLOCK_BYTES) * 16 + (off % BLOCK_BYTES) // ROW_BYTES
+                out.append(f"global_load_dwordx4 {reg}, %[voff], %[sb{g // 4}] offset:{(g % 4) * 1024}")
+            elif o.startswith("s_waitcnt lgkmcnt"):
+                out.append(o.replace("lgkmcnt", "vmcnt"))
+            else:
+                out.append(o)
+        return out
     if mode == "nowait0":
         i = next(k for k, o in enumerate(ops) if o.startswith("s_waitcnt"))
         return ops[:i] + ["s_nop 0"] + ops[i + 1:]
@@ -221,6 +237,8 @@ def emit_inc(path: str) -> None:
         lines.append(f"#define S3H_MD5_STEP_ASM_{bps} \\")
         lines += [f'  "{op}\\n\\t" \\' for op in ops]
         lines.append('  ""')
+    if os.environ.get("S3H_GEN_EXP") == "vmem":
+        lines.append("#define S3H_MD5_VMEM 1")
     lines.append(f"#define S3H_MD5_ROLL_CLOBBERS {', '.join(chr(34) + c + chr(34) for c in ROLL_CLOBBERS)}")
     for bps in (2, 4):
         lines.append(f"#define S3H_MD5_ROLL_ASM_{bps} \\")
