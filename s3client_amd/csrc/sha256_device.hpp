@@ -122,18 +122,31 @@ typedef const __attribute__((address_space(1))) uint32_t gu32;
 // the compiler can keep COUNTED vmcnt waits (a divergent branch around the loads makes it
 // drain vmcnt(0) at every use, i.e. no prefetch).  The 17th dword is read from the block
 // only when p is not dword aligned, so no dword without a part byte is ever touched.
+// Cached loads (round 3): a lane's 64-byte block arrives as four 16-B loads; non-temporal ones
+// reached L2 separately, and a producer whose 64 lanes read 64 different parts (md5_pc_kernel)
+// paced the C4 shard at 1,390 cycles per block against its consumer's 1,236 alone; cached, L1
+// merges them: MD5 C4 shard 836 -> 934 GiB/s, SHA-256 skews C4 503 -> 507, C2 / C3 unchanged
+// (profiles/r03_exp_fetch_temporal*.jsonl, alternating on one box).
 __device__ __forceinline__ void fetch_full(const uint8_t* p, bool ok, const uint8_t* zero,
                                            RawBlock& r) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(ok ? p : zero);
   gv4u32* q = reinterpret_cast<gv4u32*>(a & ~uintptr_t(3));
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
+#ifdef S3H_EXP_NONTEMPORAL_FETCH  // experiment: round 1-3's non-temporal loads
     const v4u32 v = __builtin_nontemporal_load(q + i);
+#else
+    const v4u32 v = q[i];
+#endif
     r.d[4 * i + 0] = v.x; r.d[4 * i + 1] = v.y; r.d[4 * i + 2] = v.z; r.d[4 * i + 3] = v.w;
   }
   gu32* x = reinterpret_cast<gu32*>((a & 3) ? reinterpret_cast<uintptr_t>(q + 4)
                                              : reinterpret_cast<uintptr_t>(zero));
+#ifdef S3H_EXP_NONTEMPORAL_FETCH
   r.d[16] = __builtin_nontemporal_load(x);
+#else
+  r.d[16] = *x;
+#endif
 }
 
 // v_perm selector turning {d[j+1]:d[j]} into the big-endian word at byte shift `sh`.
