@@ -3,6 +3,7 @@
 #   make            -> s3client_amd/lib/libs3hash.so  (C-ABI + lib/hash C++ drop-in + kernels)
 #                      oracle/liboracle.so (+ oracle/_ref when /root/reference exists)
 #                      tests/cpp binaries (drop-in link tests)
+#   make stall      -> tests/cpp/build/libs3hash_stall.so (forced-fault build, GPU tests only)
 HIPCC   ?= /opt/rocm/bin/hipcc
 CXX     ?= g++
 ARCH    ?= gfx950
@@ -49,7 +50,7 @@ $(STALL): $(KSRC) $(LIBDIR)/lib_hash.o $(LIBDIR)/lib_md5.o
 oracle: $(LIB)
 	$(MAKE) -C oracle
 
-CPPTESTS := tests/cpp/build/dropin_test tests/cpp/build/sign_test $(STALL)
+CPPTESTS := tests/cpp/build/dropin_test tests/cpp/build/sign_test
 cpptests: $(CPPTESTS) apps/build/s3-upload-hash
 
 apps/build/s3-upload-hash: apps/s3_upload_hash.cpp s3client_amd/host/aws_sign.cpp s3client_amd/host/aws_sign.h include/s3hash_batch.hpp $(LIB)
@@ -68,6 +69,9 @@ tests/cpp/build/sign_test: tests/cpp/sign_test.cpp s3client_amd/host/aws_sign.cp
 
 isa: $(LIBDIR)/capi.o
 
+# the forced-stall library on its own target (test-only; __graft_entry__.build() asks for it)
+stall: $(STALL)
+
 # Kernel experiment builds (never the product): make exp TAG=name EXPFLAGS="-DS3H_EXP_..."
 # -> tools/exp/libs3hash_<TAG>.so, loaded with S3H_LIBRARY=... python bench.py ...
 exp: $(LIBDIR)/lib_hash.o $(LIBDIR)/lib_md5.o
@@ -79,4 +83,4 @@ clean:
 	rm -rf $(LIBDIR) tests/cpp/build apps/build build
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle cpptests isa exp clean
+.PHONY: all oracle cpptests isa stall exp clean

@@ -10,7 +10,10 @@ already resident in HBM (generated in place by generator G).
 
 N>1: one process per GPU, parts sharded round-robin (global part p -> rank p % N, slot
 p // N), per-GPU work fixed (weak scaling), no collective on the data path -- only a barrier
-and a max-reduction of the timing.  Rank 0 prints ONE JSON line.
+and a max-reduction of the timing.  Rank 0 prints ONE JSON line, which lists every rank's
+device (PCI address) and how many distinct devices ran.  `python bench.py --gpus N` without a
+launcher starts the N ranks itself (launch_ranks: a child torch.distributed.run, started
+before this process makes any GPU call).
 """
 from __future__ import annotations
 
@@ -50,7 +53,7 @@ def chain_instr_per_block(kname: str, quad_waves: int):
         return HAND_INSTR_PER_BLOCK[kname], "round-1 hand count"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -78,7 +81,49 @@ def parse():
                     help="skip the config-5 loopback upload sub-measurement of the default line")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the C3 / C4-shard sub-measurements of the default N=1 line")
-    return ap.parse_args()
+    ap.add_argument("--print-launch", action="store_true",
+                    help="--gpus N > 1 without a launcher: print the child launch command "
+                         "and exit (tests)")
+    ap.add_argument("--rank-dry-run", action="store_true",
+                    help="tests: every rank joins the gloo group and rank 0 prints the ranks' "
+                         "identities -- the launch path without any GPU call")
+    return ap.parse_args(argv)
+
+
+def launch_command(n: int, argv: list[str], port: int) -> tuple[list[str], dict]:
+    """The child that runs `bench.py <argv>` as N ranks on one node: torch.distributed.run
+    with one process per GPU and rendezvous on 127.0.0.1:port.  Returns (argv, env
+    overrides); the child's ranks find WORLD_SIZE set and run the benchmark itself."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__), *argv]
+    # dmabuf IPC only on these hosts (a rank that shares device memory needs it), and the
+    # launcher must not pick its own OMP thread count for the ranks' CPU work
+    env = {"HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
+           "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS", "1"),
+           "S3H_BENCH_LAUNCHED": "1"}
+    return cmd, env
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv: list[str]) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher.  This process has made no GPU
+    call (no torch.cuda, no s3h_*: torch is not even imported), so it may start the N ranks
+    as ONE child process -- never an exec -- whose stdout (rank 0's JSON line) goes straight
+    to ours; it exits with the child's return code."""
+    import subprocess
+    cmd, env = launch_command(args.gpus, argv, free_port())
+    if args.print_launch:
+        print(json.dumps({"cmd": cmd, "env": env, "torch_imported": "torch" in sys.modules}))
+        return 0
+    print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env={**os.environ, **env}).returncode
 
 
 def c3_length(p: int) -> int:
@@ -279,15 +324,22 @@ def cpu_baseline(host: np.ndarray, offs, lens, gpu_digests: np.ndarray, nsample:
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args, sys.argv[1:])  # parent: no GPU call has been made
     import torch
     import torch.distributed as dist
-
-    import s3client_amd as s3
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rank_dry_run:
+        return rank_dry_run(dist, world, rank, local)
+
+    import s3client_amd as s3
+    ph = Phases(rank)
+    errors: list = []  # sub-measurements that failed (rank 0): the line says so, rc != 0
     if world != args.gpus and rank == 0:
+        errors.append({"where": "launch", "error": f"--gpus {args.gpus} but WORLD_SIZE={world}"})
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     # One process per GPU.  S3H_BENCH_SHARE_GPU=1 (rehearsal on a 1-GPU box only) maps ranks
     # onto the visible devices modulo their count.  The timing collectives (barrier, max over
@@ -301,6 +353,12 @@ def main():
         init_gloo(dist)
     dev = torch.device("cuda", gpu)
     local = gpu
+    devices = gather_obj(dist, world, device_identity(torch, s3, gpu, rank))
+    distinct = len({d["pci_bus_id"] for d in devices})
+    if rank == 0 and distinct != world and not share:
+        errors.append({"where": "devices", "error": f"{world} ranks ran on {distinct} distinct "
+                                                    "devices (S3H_BENCH_SHARE_GPU unset)"})
+    ph.mark("init")
 
     ids, lens, offs, name = workload(args.config, rank, world, args.parts_per_gpu,
                                     args.part_bytes)
@@ -323,31 +381,36 @@ def main():
     for _ in range(args.warmup):
         plan.launch(data, digests, stream)
     torch.cuda.synchronize(dev)
-    plan.status(stream)
+    status_all(dist, world, lambda: plan.status(stream))
+    ph.mark("setup+warmup")
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        plan.launch(data, digests, stream)
-        ev[i][1].record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    # every timed launch's device error word (a timed-out producer/consumer wait): raises
-    plan.status(stream)
+    with power_sampler(devices[rank]) as pw:
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            ev[i][0].record(stream)
+            plan.launch(data, digests, stream)
+            ev[i][1].record(stream)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        wall = time.perf_counter() - t0
+    # every timed launch's device error word (a timed-out producer/consumer wait), gathered
+    # from every rank before any rank raises (no rank is left waiting in a collective)
+    status_all(dist, world, lambda: plan.status(stream))
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     t = torch.tensor([wall, kern_ms], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)  # max over ranks: the slowest GPU sets the time
     wall, kern_ms_max = float(t[0]), float(t[1])
+    ph.mark(f"timed {args.steps} steps")
 
     probe = clock_probe(torch, plan, info, data, digests, stream, dev, kname)
+    power = gather_obj(dist, world, pw.summary())
 
     # parity of the last timed step's digests against the reference fixtures, on EVERY rank
     # (tests/golden: C2/C4 parts and four parts of each rank's shard at N = 2, 4, 8)
@@ -375,28 +438,8 @@ def main():
     # one part = one sequential chain on one lane: report what one chain sustains and how
     # many of the chip's 256 CU x 4 SIMD x 64 = 65,536 lanes the batch can occupy
     chain_gbps = float(lens.max()) / (kern_ms / 1e3) / 1e9
-    if probe:
-        cyc_per_block, clock_src = probe["cycles_per_block"], "in-kernel s_memtime probe"
-    else:
-        cyc_per_block = kern_ms / 1e3 * CLOCK_GHZ * 1e9 / info["max_blocks"]
-        clock_src = f"kernel time x assumed {CLOCK_GHZ} GHz"
-    ipb, ipb_src = chain_instr_per_block(kname, 2 if (kname == "skew" and len(lens) > 2048) else 1)
-    cpi = cyc_per_block / ipb
-    issue = {"bound": "per-wave instruction issue of each part's sequential chain",
-             "chain_instr_per_block": ipb, "chain_instr_source": ipb_src,
-             "cycles_per_block": round(cyc_per_block, 1), "cycles_source": clock_src,
-             "cycles_per_instr": round(cpi, 3),
-             # floor: one wave issues at most one instruction per 4 cycles (MI355X_MICROARCH.md
-             # 'vector-instruction ISSUE cost'; 4.05 measured on an aligned lone-wave stream,
-             # profiles/r01_ubench_alignment.txt)
-             "issue_floor_cycles_per_instr": ISSUE_FLOOR_CPI,
-             "frac": round(ISSUE_FLOOR_CPI / cpi, 4),
-             "clock_GHz": probe["clock_GHz"] if probe else CLOCK_GHZ,
-             # chip-wide INT32-VALU roof (256 CU x 64 lanes x clock / VALU per
-             # block of the one-lane-per-part kernel x 64 B) and the parallelism ceiling
-             "valu_roof_GBps": round(256 * 64 * CLOCK_GHZ * 1e9 / HAND_INSTR_PER_BLOCK["lane"]
-                                     * 64 / 1e9, 1),
-             "parallelism_ceiling": round(min(len(lens), 65536) / 65536, 5)}
+    issue = issue_model(kname, len(lens), kern_ms, info, probe)
+    ph.mark("parity+probe")
 
     line = None
     if rank == 0:
@@ -413,11 +456,12 @@ def main():
                        "kernel": kname, "grid": info["grid"], "groups": info["groups"],
                        "solo_workgroups": info["solo"],
                        "parallelism": f"parts sharded round-robin over {world} GPU(s), no collective"},
+            "devices": devices, "distinct_devices": distinct,
             "parity": {"fixtures_checked": sum(r[0] for r in par),
                        "mismatches": sum(r[1] for r in par),
                        "per_rank": [{"rank": k, "fixtures_checked": r[0], "mismatches": r[1]}
                                     for k, r in enumerate(par)]},
-            "status": "ok: device error word clear after every launch (s3h_plan_status)",
+            "status": "ok: device error word clear after every launch on every rank (s3h_plan_status)",
             "library": lib_info,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -431,59 +475,208 @@ def main():
                          "per_chain_GBps": round(chain_gbps, 4),
                          "lanes_occupied_frac": round(min(len(lens), 65536) / 65536, 5)},
             "issue": issue,
+            "power": power[0] if world == 1 else power,
         }
-        if (world == 1 and args.config == "c2" and args.algo == "sha256" and not args.parts_per_gpu
-                and not args.part_bytes and not args.no_host_resident):
-            line["host_resident"] = _guard(host_resident, s3, torch, data, ids, lens, offs, gd)
+        default_c2 = (world == 1 and args.config == "c2" and args.algo == "sha256"
+                      and not args.parts_per_gpu and not args.part_bytes)
+        if default_c2 and not args.no_host_resident:
+            line["host_resident"] = _guard(errors, "host_resident", host_resident, s3, torch,
+                                           data, ids, lens, offs, gd)
+            ph.mark("host_resident")
             if not args.no_c5:
-                line["c5_loopback"] = _guard(c5_loopback, data, offs, lens, gd)
-        if (world == 1 and args.config == "c2" and args.algo == "sha256" and not args.parts_per_gpu
-                and not args.part_bytes and not args.no_configs):
-            line["f_rows"] = _guard(f_rows_c2, s3, torch, data, ids, lens, offs, dev, stream)
+                line["c5_loopback"] = _guard(errors, "c5_loopback", c5_loopback, data, offs,
+                                             lens, gd)
+                ph.mark("c5_loopback")
+        if default_c2 and not args.no_configs:
+            line["f_rows"] = _guard(errors, "f_rows", f_rows_c2, s3, torch, data, ids, lens,
+                                    offs, dev, stream)
+            ph.mark("f_rows")
         if world == 1 and not args.no_cpu_baseline:
             n = min(args.cpu_sample_parts, len(lens))
             end = int(offs[n - 1] + lens[n - 1])
             host = data[:end].cpu().numpy()
-            line["cpu_baseline"] = _guard(cpu_baseline, host, offs, lens, gd, n, args.algo)
+            line["cpu_baseline"] = _guard(errors, "cpu_baseline", cpu_baseline, host, offs,
+                                          lens, gd, n, args.algo)
             del host
-        if (world == 1 and args.config == "c2" and args.algo == "sha256" and not args.parts_per_gpu
-                and not args.part_bytes and not args.no_configs):
+            ph.mark("cpu_baseline")
+        if default_c2 and not args.no_configs:
             del data, digests
             plan.close()
             torch.cuda.empty_cache()
-            line["configs"] = {c: _guard(single_gpu_config, s3, torch, dev, c) for c in ("c3", "c4")}
+            line["configs"] = {}
+            for c in ("c3", "c4"):
+                line["configs"][c] = _guard(errors, f"configs.{c}", single_gpu_config, s3,
+                                            torch, dev, c, devices[0])
+                ph.mark(f"configs.{c}")
     if world > 1 and args.config == "c2" and args.algo == "sha256":
         del data, digests
         plan.close()
         torch.cuda.empty_cache()
         if not args.no_c4:
-            c4 = c4_shard(args, s3, torch, dist, dev, rank, world, local)
+            try:  # a device fault raises on EVERY rank together (status_all), so all catch it
+                c4 = c4_shard(args, s3, torch, dist, dev, rank, world, local, devices[rank], ph)
+            except DeviceFault as e:
+                c4 = {"error": str(e)}
+                if rank == 0:
+                    errors.append({"where": "c4", "error": str(e), "device_fault": True})
             if rank == 0:
                 line["c4"] = c4
         if not args.no_host_resident:
             dist.barrier()  # the other ranks wait while rank 0 drives every GPU from the host
             if rank == 0:
-                try:  # rank 0 alone between two barriers: a failure here must not lose the line
-                    line["host_resident"] = host_resident_multi(s3, torch, dev, world)
-                except Exception as e:  # noqa: BLE001 -- reported in the line instead
-                    line["host_resident"] = {"error": f"{type(e).__name__}: {e}"}
+                line["host_resident"] = _guard(errors, "host_resident", host_resident_multi,
+                                               s3, torch, dev, world, ph)
+                ph.mark("host_resident (N devices)")
             dist.barrier()
+    rc = 0
     if rank == 0:
+        errors += parity_failures(line)
+        line["phases_s"] = ph.times
+        if errors:
+            line["errors"] = errors
+            rc = 3
         print(json.dumps(line), flush=True)
+    if world > 1:
+        rc = max(x[0] for x in per_rank(dist, world, [rc]))
+        dist.destroy_process_group()
+    return rc
+
+
+def rank_dry_run(dist, world: int, rank: int, local: int) -> int:
+    """--rank-dry-run: the multi-rank plumbing of a bench run (gloo group, gathered per-rank
+    records, one line from rank 0, exit code agreed over ranks) with no GPU call, so the
+    self-launch is testable on a CPU-only host."""
+    import socket
+    if world > 1:
+        init_gloo(dist)
+    me = {"rank": rank, "local_rank": local, "pid": os.getpid(), "host": socket.gethostname(),
+          "launched_by_bench": os.environ.get("S3H_BENCH_LAUNCHED") == "1"}
+    ranks = gather_obj(dist, world, me)
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks": ranks}), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0
 
 
-def _guard(fn, *args):
+class DeviceFault(RuntimeError):
+    """A device error word (or another status check) failed on at least one rank."""
+
+
+class Phases:
+    """Seconds per phase of this rank's run, to stderr as they end (rank 0) and into the line:
+    an N-GPU line's time is accounted for against the driver's clock."""
+
+    def __init__(self, rank: int):
+        self.rank, self.t, self.times = rank, time.perf_counter(), {}
+
+    def mark(self, name: str) -> None:
+        now = time.perf_counter()
+        self.times[name] = round(now - self.t, 3)
+        if self.rank == 0:
+            print(f"[bench rank 0] {name}: {now - self.t:.2f} s", file=sys.stderr, flush=True)
+        self.t = now
+
+
+def device_identity(torch, s3, gpu: int, rank: int) -> dict:
+    """Which physical GPU this rank hashed on: the PCI address as libs3hash's own HIP context
+    reports it (s3h_device_pci_bus_id), the name and UUID torch reports, host and pid."""
+    import socket
+    p = torch.cuda.get_device_properties(gpu)
+    return {"rank": rank, "device_index": gpu, "pci_bus_id": s3.device_pci_bus_id(gpu),
+            "torch_pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+            "name": p.name, "arch": getattr(p, "gcnArchName", ""), "uuid": str(p.uuid),
+            "cus": p.multi_processor_count, "host": socket.gethostname(), "pid": os.getpid()}
+
+
+def gather_obj(dist, world: int, obj):
+    """[obj of rank 0, obj of rank 1, ...] over gloo; [obj] at N = 1."""
+    if world == 1:
+        return [obj]
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def status_all(dist, world: int, check) -> None:
+    """Run a status check (plan.status: the device error word) on every rank and gather every
+    rank's outcome BEFORE raising, so a fault on one rank fails all of them together instead
+    of leaving the others blocked in the next collective."""
+    err = ""
+    try:
+        check()
+    except Exception as e:  # noqa: BLE001 -- re-raised on every rank below
+        err = f"{type(e).__name__}: {e}"
+    bad = [(k, e) for k, e in enumerate(gather_obj(dist, world, err)) if e]
+    if bad:
+        raise DeviceFault("; ".join(f"rank {k}: {e}" for k, e in bad))
+
+
+def power_sampler(ident: dict):
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from power import PowerSampler
+    return PowerSampler(ident["pci_bus_id"])
+
+
+def issue_model(kname: str, nparts: int, kern_ms: float, info: dict, probe) -> dict:
+    """Per-wave issue roof of the chain loop: cycles per block (clock probe, else kernel time x
+    the assumed clock) over the instructions per block read from the shipped code object."""
+    if probe:
+        cyc_per_block, clock_src = probe["cycles_per_block"], "in-kernel s_memtime probe"
+    else:
+        cyc_per_block = kern_ms / 1e3 * CLOCK_GHZ * 1e9 / info["max_blocks"]
+        clock_src = f"kernel time x assumed {CLOCK_GHZ} GHz"
+    ipb, ipb_src = chain_instr_per_block(kname, 2 if (kname == "skew" and nparts > 2048) else 1)
+    cpi = cyc_per_block / ipb
+    return {"bound": "per-wave instruction issue of each part's sequential chain",
+            "chain_instr_per_block": ipb, "chain_instr_source": ipb_src,
+            "cycles_per_block": round(cyc_per_block, 1), "cycles_source": clock_src,
+            "cycles_per_instr": round(cpi, 3),
+            # floor: one wave issues at most one instruction per 4 cycles (MI355X_MICROARCH.md
+            # 'vector-instruction ISSUE cost'; 4.05 measured on an aligned lone-wave stream,
+            # profiles/r01_ubench_alignment.txt)
+            "issue_floor_cycles_per_instr": ISSUE_FLOOR_CPI,
+            "frac": round(ISSUE_FLOOR_CPI / cpi, 4),
+            "clock_GHz": probe["clock_GHz"] if probe else CLOCK_GHZ,
+            # SURVEY 8(d): chip-wide INT32-VALU roof (256 CU x 64 lanes x clock / VALU per
+            # block of the one-lane-per-part kernel x 64 B) and the parallelism ceiling
+            "valu_roof_GBps": round(256 * 64 * CLOCK_GHZ * 1e9 / HAND_INSTR_PER_BLOCK["lane"]
+                                    * 64 / 1e9, 1),
+            "parallelism_ceiling": round(min(nparts, 65536) / 65536, 5)}
+
+
+def parity_failures(obj, path: str = "") -> list:
+    """Every digest comparison in the line that failed: a non-zero mismatch count or a false
+    digests-match flag anywhere in the nested sub-measurements."""
+    out = []
+    if isinstance(obj, dict):
+        for k, v in obj.items():
+            p = f"{path}.{k}" if path else k
+            if k in ("mismatches", "fixture_mismatches") and isinstance(v, int) and v > 0:
+                out.append({"where": p, "error": f"{v} digest mismatches"})
+            elif (k.startswith("digests_match") or k.endswith("_equals_sha256_only_run")) and v is False:
+                out.append({"where": p, "error": "digests differ"})
+            elif isinstance(v, (dict, list)):
+                out += parity_failures(v, p)
+    elif isinstance(obj, list):
+        for i, v in enumerate(obj):
+            out += parity_failures(v, f"{path}[{i}]")
+    return out
+
+
+def _guard(errors: list, where: str, fn, *args):
     """A sub-measurement of the line (rank 0, after the timed region and its parity): an
-    exception is reported in its place instead of losing the metric line."""
+    exception is reported in its place AND in the line's top-level `errors` (the process then
+    exits non-zero) instead of losing the metric line."""
     try:
         return fn(*args)
     except Exception as e:  # noqa: BLE001 -- reported in the line
         import traceback
         traceback.print_exc(file=sys.stderr)
-        return {"error": f"{type(e).__name__}: {e}"}
+        from s3client_amd import S3HashError
+        msg = f"{type(e).__name__}: {e}"
+        errors.append({"where": where, "error": msg, "device_fault": isinstance(e, S3HashError)})
+        return {"error": msg}
 
 
 def init_gloo(dist) -> None:
@@ -584,11 +777,15 @@ def f_rows_c2(s3, torch, data, ids, lens, offs, dev, stream, steps: int = 3) -> 
     return res
 
 
-def single_gpu_config(s3, torch, dev, cfg: str, steps: int = 2) -> dict:
+def single_gpu_config(s3, torch, dev, cfg: str, ident: dict, steps: int = 2) -> dict:
     """BASELINE configs 3 and 4 beside the C2 headline of the default N=1 line, so every
     single-GPU configuration has a driver-run number: C3 = 4,096 x U[5,64] MiB (~138 GiB
-    resident), C4 = rank 0's shard of 65,536 x 8 MiB over 8 GPUs (parts 8k, 64 GiB).  HIP-event
-    kernel time on the launch stream, AUTO kernel, fixture parity."""
+    resident), C4 = rank 0's shard of 65,536 x 8 MiB over 8 GPUs (parts 8k, 64 GiB).  Each
+    kernel timed with HIP events on the launch stream, then the in-kernel clock probe (live
+    shader clock, cycles per block -> fraction of the issue floor) and the board power over the
+    timed launches (amdsmi), fixture parity.  C3: AUTO.  C4: AUTO (skews, shared-SIMD
+    producers) AND skewp beside it, so the line itself shows what the C4 kernel choice buys and
+    at what power."""
     from s3client_amd.shard import pack_offsets, shard_ids
     if cfg == "c3":
         ids, lens, offs, name = workload("c3", 0, 1, 0)
@@ -600,39 +797,62 @@ def single_gpu_config(s3, torch, dev, cfg: str, steps: int = 2) -> dict:
     data = torch.empty(int(offs[-1] + lens[-1]) + 256, dtype=torch.uint8, device=dev)
     s3.generate_parts(data, offs, lens, ids, SEED)
     stream = torch.cuda.current_stream(dev)
-    plan = s3.Plan(offs, lens, device=dev.index)
-    out = torch.zeros((len(lens), 8), dtype=torch.int32, device=dev)
-    plan.launch(data, out, stream)
-    torch.cuda.synchronize(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps)]
-    t0 = time.perf_counter()
-    for a, b in ev:
-        a.record(stream)
-        plan.launch(data, out, stream)
-        b.record(stream)
-    torch.cuda.synchronize(dev)
-    wall = (time.perf_counter() - t0) / steps
-    plan.status(stream)  # device error word clear (raises otherwise)
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    gd = out.cpu().numpy().view(np.uint32)
     fx = golden_fixtures(cfg, "sha256")
-    checked = [k for k, p in enumerate(ids) if int(p) in fx]
-    bad = sum(s3_hex(gd[k]) != fx[int(ids[k])] for k in checked)
-    info = plan.info()
-    plan.close()
-    dual = _dual_on(s3, torch, dev, data, ids, lens, offs, cfg, stream, gd, info) if cfg == "c3" else None
-    del data, out
-    torch.cuda.empty_cache()
     part_bytes = float(lens.sum())
     algo = part_bytes + 32 * len(lens)
-    res = {"workload": name, "kernel": info["kernel"], "grid": info["grid"],
-            "solo_workgroups": info["solo"], "steps": steps,
+    kernels = {}
+    gd = info = None
+    for kern in (("auto",) if cfg == "c3" else ("auto", "skewp")):
+        plan = s3.Plan(offs, lens, device=dev.index, kernel=kern)
+        kinfo = plan.info()
+        out = torch.zeros((len(lens), 8), dtype=torch.int32, device=dev)
+        plan.launch(data, out, stream)
+        torch.cuda.synchronize(dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        with power_sampler(ident) as pw:
+            t0 = time.perf_counter()
+            for a, b in ev:
+                a.record(stream)
+                plan.launch(data, out, stream)
+                b.record(stream)
+            torch.cuda.synchronize(dev)
+            wall = (time.perf_counter() - t0) / steps
+        plan.status(stream)  # device error word clear (raises otherwise)
+        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        probe = clock_probe(torch, plan, kinfo, data, out, stream, dev)
+        kd = out.cpu().numpy().view(np.uint32)
+        checked = [k for k, p in enumerate(ids) if int(p) in fx]
+        bad = sum(s3_hex(kd[k]) != fx[int(ids[k])] for k in checked)
+        plan.close()
+        del out
+        iss = issue_model(kinfo["kernel"], len(lens), kern_ms, kinfo, probe)
+        kernels[kinfo["kernel"]] = {
             "GiBps": round(part_bytes / 2**30 / wall, 3), "ms_per_step": round(1e3 * wall, 3),
-            "kernel_ms": round(kern_ms, 3),
+            "kernel_ms": round(kern_ms, 3), "grid": kinfo["grid"],
             "hbm_roofline_frac": round(algo / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5),
-            "bound": "the longest part's chain" if cfg == "c3" else "per-wave issue of 8,192 chains",
+            "clock_GHz": probe["clock_GHz"] if probe else None,
+            "cycles_per_block": probe["cycles_per_block"] if probe else None,
+            "chain_instr_per_block": iss["chain_instr_per_block"],
+            "issue_frac": iss["frac"] if probe else None,
+            "power": pw.summary(),
             "parity": {"fixtures_checked": len(checked), "mismatches": int(bad)}}
+        if kern == "auto":
+            gd, info = kd, kinfo
+        elif not np.array_equal(kd, gd):
+            kernels[kinfo["kernel"]]["digests_match_auto"] = False
+    dual = _dual_on(s3, torch, dev, data, ids, lens, offs, cfg, stream, gd, info) if cfg == "c3" else None
+    del data
+    torch.cuda.empty_cache()
+    auto = kernels[info["kernel"]]
+    res = {"workload": name, "kernel": info["kernel"], "grid": info["grid"],
+           "solo_workgroups": info["solo"], "steps": steps,
+           **{k: auto[k] for k in ("GiBps", "ms_per_step", "kernel_ms", "hbm_roofline_frac",
+                                   "clock_GHz", "cycles_per_block", "issue_frac", "power")},
+           "bound": "the longest part's chain" if cfg == "c3" else "per-wave issue of 8,192 chains",
+           "parity": auto["parity"]}
+    if len(kernels) > 1:
+        res["kernels"] = kernels
     if dual:
         res["sha256_md5"] = dual
     return res
@@ -725,13 +945,15 @@ def s3_hex(words) -> str:
     return np.ascontiguousarray(words, dtype=np.uint32).tobytes().hex()
 
 
-def c4_shard(args, s3, torch, dist, dev, rank, world, local, steps: int = 3):
+def c4_shard(args, s3, torch, dist, dev, rank, world, local, ident, ph, steps: int = 3):
     """BASELINE config 4 beside the C2 headline of a multi-GPU run: 8,192 x 8 MiB per GPU,
     global part p on rank p % N (65,536 parts = 512 GiB at N = 8), no collective on the data
     path.  The AUTO kernel (skews: producers on their consumers' SIMDs, ~1.4 kW per board) and
-    skewp (~0.7 kW) are timed on the same parts, each with the clock probe, so the node's power
-    envelope decides between them on measured numbers; per-GPU and aggregate GiB/s over the
-    max-over-ranks time, fixture parity on every rank (four own-shard fixtures per rank)."""
+    skewp (~0.7 kW) are timed on the same parts, each with the clock probe and the board power
+    (amdsmi) per GPU, so the node's power envelope decides between them on measured numbers;
+    per-GPU and aggregate GiB/s over the max-over-ranks time, fixture parity on every rank
+    (four own-shard fixtures per rank).  A device fault on any rank raises DeviceFault on
+    every rank together (status_all)."""
     from s3client_amd.shard import shard_ids
     per, L = 8192, 8 * MIB
     ids = shard_ids(per * world, rank, world)
@@ -745,27 +967,30 @@ def c4_shard(args, s3, torch, dist, dev, rank, world, local, steps: int = 3):
     algo = per * (L + 32)  # bytes read once + digests written, per GPU per launch
     res = {"workload": f"C4: {per} x 8 MiB per GPU, {per * world} parts over {world} GPUs "
                        "(part p on rank p % N)", "steps": steps, "kernels": {}}
+    ph.mark("c4 generate")
     for kern in ("auto", "skewp"):
         plan = s3.Plan(offs, lens, device=local, kernel=kern)
         info = plan.info()
         out = torch.zeros((per, 8), dtype=torch.int32, device=dev)
         plan.launch(data, out, stream)
-        plan.status(stream)
+        status_all(dist, world, lambda: plan.status(stream))
         dist.barrier()
         torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            plan.launch(data, out, stream)
-        torch.cuda.synchronize(dev)
-        mine = time.perf_counter() - t0
-        dist.barrier()
-        wall = time.perf_counter() - t0
-        plan.status(stream)
+        with power_sampler(ident) as pw:
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                plan.launch(data, out, stream)
+            torch.cuda.synchronize(dev)
+            mine = time.perf_counter() - t0
+            dist.barrier()
+            wall = time.perf_counter() - t0
+        status_all(dist, world, lambda: plan.status(stream))
         probe = clock_probe(torch, plan, info, data, out, stream, dev) or {}
         gd = out.cpu().numpy().view(np.uint32)
         chk = [k for k, p in enumerate(ids) if int(p) in fx]
         bad = sum(s3.hash_to_text(gd[k]) != fx[int(ids[k])] for k in chk)
         plan.close()
+        pws = gather_obj(dist, world, pw.summary())
         # per rank: time (us), wall (us), fixtures checked, mismatches, clock (MHz), cycles/block
         r = per_rank(dist, world, [int(mine * 1e6), int(wall * 1e6), len(chk), int(bad),
                                    int(probe.get("clock_GHz", 0) * 1e3),
@@ -779,10 +1004,13 @@ def c4_shard(args, s3, torch, dist, dev, rank, world, local, steps: int = 3):
                                           for t in t_rank],
             "clock_GHz_per_gpu": [x[4] / 1e3 for x in r],
             "cycles_per_block_per_gpu": [x[5] for x in r],
+            "board_W_busy_mean_per_gpu": [p.get("busy_mean_W") for p in pws],
+            "board_W_max_per_gpu": [p.get("max_W") for p in pws],
             "parity": {"fixtures_checked": sum(x[2] for x in r), "mismatches": sum(x[3] for x in r),
                        "fixtures_checked_per_rank": [x[2] for x in r]}}
         if kern == "auto":
             res["kernel"] = info["kernel"]
+        ph.mark(f"c4 {info['kernel']}")
     del data
     torch.cuda.empty_cache()
     auto = res["kernels"][res["kernel"]]
@@ -792,31 +1020,35 @@ def c4_shard(args, s3, torch, dist, dev, rank, world, local, steps: int = 3):
     return res
 
 
-def host_resident_multi(s3, torch, dev, world: int, per: int = 1024, reps: int = 3):
-    """Rank 0 of an N-GPU run: the C2 weak-scaling job's parts (1,024 x 8 MiB per GPU, global
-    ids 0..1024N-1) starting and ending in HOST memory, through
-    s3h_sha256_batch_host(..., ndevices=N) -- part i on device i % N, the device-resident
-    line's split -- with every H2D copy inside the timed region.  The parts are generated on
-    this GPU and copied into one pinned buffer beforehand (setup_s, untimed)."""
+def host_resident_multi(s3, torch, dev, world: int, ph, per: int = 1024, reps: int = 3):
+    """Rank 0 of an N-GPU run: the C2 weak-scaling job (1,024 x 8 MiB per GPU) starting and
+    ending in HOST memory, through s3h_sha256_batch_host(..., ndevices=N) -- part i on device
+    i % N, one host thread per device -- with every H2D copy inside the timed region.
+
+    Bounded host memory: ONE pinned buffer of 1,024 parts (8 GiB, C2 ids 0..1023) whatever N,
+    and global part i is buffer part i // N, so every device hashes all 1,024 buffer parts
+    (the same per-device work as the device-resident line) and the host DRAM is read N times
+    over, as an uploader staging N devices' parts would.  Parity: every device's digest of
+    buffer part j equals every other's, and the C2 fixtures pin parts 0..15, 511, 1022, 1023."""
     L = 8 * MIB
-    n = per * world
+    ndev = min(world, torch.cuda.device_count())
+    n = per * ndev
     t_setup = time.perf_counter()
     try:
-        host = torch.empty(n * L, dtype=torch.uint8, pin_memory=True)
+        host = torch.empty(per * L, dtype=torch.uint8, pin_memory=True)
     except RuntimeError as e:
-        return {"error": f"pinned host buffer of {n * L / 2**30:.0f} GiB: {e}"}
+        return {"error": f"pinned host buffer of {per * L / 2**30:.0f} GiB: {e}"}
     buf = torch.empty(per * L, dtype=torch.uint8, device=dev)
     lens = np.full(per, L, dtype=np.uint64)
     offs = np.arange(per, dtype=np.uint64) * np.uint64(L)
-    for c in range(world):
-        s3.generate_parts(buf, offs, lens, np.arange(c * per, (c + 1) * per), SEED)
-        host[c * per * L:(c + 1) * per * L].copy_(buf)
+    s3.generate_parts(buf, offs, lens, np.arange(per), SEED)
+    host.copy_(buf)
     del buf
     torch.cuda.empty_cache()
     h = host.numpy()
-    views = [h[i * L:(i + 1) * L] for i in range(n)]
+    views = [h[(i // ndev) * L:(i // ndev + 1) * L] for i in range(n)]
     setup = time.perf_counter() - t_setup
-    ndev = min(world, torch.cuda.device_count())
+    ph.mark("host_resident setup (8 GiB pinned)")
     out = s3.sha256_batch_host(views, ndevices=ndev)  # warm: a cached context per device
     times = []
     for _ in range(reps):
@@ -824,8 +1056,9 @@ def host_resident_multi(s3, torch, dev, world: int, per: int = 1024, reps: int =
         out = s3.sha256_batch_host(views, ndevices=ndev)
         times.append(time.perf_counter() - t0)
     fx = golden_fixtures("c2", "sha256")
-    chk = [p for p in range(n) if p in fx]
-    bad = sum(s3.hash_to_text(out[p]) != fx[p] for p in chk)
+    chk = [j for j in range(per) if j in fx]
+    bad = sum(s3.hash_to_text(out[j * ndev]) != fx[j] for j in chk)
+    same = bool((out.reshape(per, ndev, 8) == out.reshape(per, ndev, 8)[:, :1]).all())
     threads, cpus = s3.host_threads(ndev)
     gib = n * L / 2**30
     del host, h, views
@@ -833,13 +1066,16 @@ def host_resident_multi(s3, torch, dev, world: int, per: int = 1024, reps: int =
     return {"metric": f"host-resident (H2D-inclusive) SHA-256 GiB/s over {ndev} GPU(s)",
             "value": round(gib / float(np.mean(times)), 3), "best": round(gib / min(times), 3),
             "per_gpu": round(gib / float(np.mean(times)) / ndev, 3), "unit": "GiB/s",
-            "devices": ndev, "parts": n, "reps": reps,
+            "devices": ndev, "parts": n, "parts_per_device": per, "reps": reps,
+            "pinned_host_GiB": per * L / 2**30,
             "ms_per_batch": round(1e3 * float(np.mean(times)), 2), "setup_s": round(setup, 2),
             "path": "pinned host parts -> per-device 3-slot HBM ring (one 2-D H2D copy per "
                     "256 KiB slice) -> skew kernel per slice -> digests D2H "
-                    "(s3h_sha256_batch_host, one host thread per device)",
+                    "(s3h_sha256_batch_host, one host thread per device); one 8 GiB pinned "
+                    "buffer read by every device",
             "host_cpus": cpus, "staging_threads_per_device": threads,
-            "fixtures_checked": len(chk), "fixture_mismatches": int(bad)}
+            "fixtures_checked": len(chk), "fixture_mismatches": int(bad),
+            "digests_match_across_devices": same}
 
 
 def host_mode(args, s3, torch, dist, data, ids, lens, offs, world, rank, name):

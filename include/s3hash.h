@@ -75,6 +75,10 @@ int s3h_trim(void);
 int s3h_host_threads(int ndevices, int *cpus);
 /* Number of visible HIP devices; S3H_ENODEV (and *count = 0) when there is none. */
 int s3h_device_count(int *count);
+/* PCI address of HIP device `device` as "dddd:bb:dd.f" (lowercase, NUL-terminated; len >= 13):
+ * which physical GPU a device index names, so a multi-GPU run can show that its N ranks
+ * hashed on N distinct devices.  S3H_ENODEV / S3H_EINVAL as s3h_plan_create. */
+int s3h_device_pci_bus_id(int device, char *out, int len);
 
 /* ---------------------------------------------------------------- device-resident path
  * A plan captures the part geometry (byte offsets relative to a base pointer, lengths) of

@@ -37,7 +37,7 @@ C_ABI_SYMBOLS = (
     "s3h_sha256_md5_batch_host", "s3h_sha256_md5_batch_device", "s3h_trim",
     "s3h_sha256_file_parts", "s3h_sha256_batch_host_on", "s3h_plan_groups",
     "s3h_sha256_md5_file_parts", "s3h_plan_status", "s3h_stream_status", "s3h_host_threads",
-    "s3h_plan_dual_solo",
+    "s3h_plan_dual_solo", "s3h_device_pci_bus_id",
 )
 ALGO_SHA256, ALGO_MD5 = 0, 1
 ALGO_IDS = {"sha256": ALGO_SHA256, "md5": ALGO_MD5}
@@ -82,6 +82,7 @@ def lib() -> ctypes.CDLL:
             L = ctypes.CDLL(LIB_PATH)
             L.s3h_last_error.restype = ctypes.c_char_p
             L.s3h_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+            L.s3h_device_pci_bus_id.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
             L.s3h_plan_create.argtypes = [ctypes.c_int, u64p, u64p, ctypes.c_uint64, ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_void_p)]
             L.s3h_plan_create_ex.argtypes = [ctypes.c_int, ctypes.c_int, u64p, u64p,

@@ -11,6 +11,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <cctype>
 #include <cerrno>
 
 #include <algorithm>
@@ -1415,6 +1416,15 @@ int s3h_device_count(int* count) {
   int c = 0;
   if (hipGetDeviceCount(&c) != hipSuccess || c <= 0) return fail(S3H_ENODEV, "no HIP device visible");
   *count = c;
+  return S3H_OK;
+}
+
+int s3h_device_pci_bus_id(int device, char* out, int len) {
+  if (!out || len < 13) return fail(S3H_EINVAL, "need a buffer of at least 13 bytes");
+  out[0] = 0;
+  if (int rc = check_device(device)) return rc;
+  HIP_TRY(hipDeviceGetPCIBusId(out, len, device));
+  for (char* c = out; *c; ++c) *c = char(tolower(*c));
   return S3H_OK;
 }
 

@@ -42,6 +42,13 @@ def device_count() -> int:
     return c.value if rc == 0 else 0
 
 
+def device_pci_bus_id(device: int) -> str:
+    """PCI address "dddd:bb:dd.f" of HIP device ``device`` (s3h_device_pci_bus_id)."""
+    buf = ctypes.create_string_buffer(64)
+    check(lib().s3h_device_pci_bus_id(device, buf, len(buf)))
+    return buf.value.decode()
+
+
 def nblocks(length: int) -> int:
     """64-byte compressions SHA-256 performs on a message of ``length`` bytes."""
     return (int(length) + 72) // 64

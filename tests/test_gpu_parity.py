@@ -290,6 +290,28 @@ def test_md5_host_path_transfer_etag(torch_cuda, golden):
         assert s3.multipart_etag(d) == golden["md5"]["transfer_etag"]
 
 
+def test_md5_beyond_one_workgroup_per_cu(torch_cuda, oracle):
+    """MD5 batches whose grid has more workgroups than the GPU has CUs (> 64 x CUs parts: 20,000
+    here) run md5_pc_kernel<1> (1-block steps, 32 KiB of LDS, several workgroups per CU;
+    capi.hip launch): ragged, misaligned parts incl. empty ones, device-resident and through
+    the host path with slices of an odd number of blocks, bit-exact vs the oracle."""
+    rng = np.random.default_rng(2020)
+    n = 20000
+    lens = rng.integers(0, 40000, n)
+    lens[:6] = [0, 1, 55, 56, 64, 119]
+    offs = np.concatenate([[0], np.cumsum(lens + rng.integers(0, 9, n))[:-1]])
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    cus = torch_cuda.cuda.get_device_properties(0).multi_processor_count
+    with s3.Plan(offs, lens, algo="md5") as plan:
+        assert plan.info()["grid"] == (n + 63) // 64 > cus
+    want = oracle.md5_batch(host, offs, lens, threads=16)
+    got = s3.md5_batch_device(_dev_buffer(torch_cuda, host), offs, lens).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want)
+    views = [host[int(o):int(o) + int(L)] for o, L in zip(offs, lens)]
+    for sl in (37 * 64, 101 * 64, 0):
+        assert np.array_equal(s3.md5_batch_host(views, slice_bytes=sl), want), sl
+
+
 @pytest.mark.parametrize("n", [2100, 3000, 6000])
 def test_dual_mixed_grid_ragged(torch_cuda, oracle, n):
     """SHA-256 + MD5 of a ragged batch in the skewp-group range (C3-like lengths, scaled):

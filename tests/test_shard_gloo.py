@@ -4,6 +4,7 @@ Each rank takes parts p % world == rank, digests them locally (CPU drop-in here;
 path on the box), and the digest table is reassembled only for verification.  Checks: the
 shards partition the batch, the reassembled table equals the oracle's, and bench.py's
 workload() uses the same partition."""
+import json
 import os
 import socket
 import subprocess
@@ -139,8 +140,104 @@ def test_bench_gloo_init_keeps_stdout_clean():
 
 
 def test_bench_guard_reports_a_failed_sub_measurement():
-    """A sub-measurement that raises becomes {"error": ...} in the line; the metric survives."""
+    """A sub-measurement that raises becomes {"error": ...} in the line AND an entry of the
+    line's top-level errors (bench then exits non-zero); the metric survives."""
     import bench
-    assert bench._guard(lambda a, b: a + b, 2, 3) == 5
-    got = bench._guard(lambda: 1 / 0)
+    from s3client_amd import S3HashError
+    errors = []
+    assert bench._guard(errors, "x", lambda a, b: a + b, 2, 3) == 5 and errors == []
+    got = bench._guard(errors, "y", lambda: 1 / 0)
     assert got == {"error": "ZeroDivisionError: division by zero"}
+
+    def fault():
+        raise S3HashError(-3, "synchronisation timeout")
+    bench._guard(errors, "z", fault)
+    assert [e["where"] for e in errors] == ["y", "z"]
+    assert [e["device_fault"] for e in errors] == [False, True]
+
+
+def test_bench_parity_failures_scan_the_whole_line():
+    import bench
+    line = {"parity": {"mismatches": 0, "per_rank": [{"mismatches": 0}, {"mismatches": 2}]},
+            "configs": {"c4": {"kernels": {"skewp": {"parity": {"mismatches": 1}},
+                                           "skews": {"digests_match_auto": True}}},
+                        "c3": {"sha256_md5": {"sha256_equals_sha256_only_run": False}}},
+            "host_resident": {"fixture_mismatches": 0, "digests_match_device_run": False}}
+    got = sorted(e["where"] for e in bench.parity_failures(line))
+    assert got == ["configs.c3.sha256_md5.sha256_equals_sha256_only_run",
+                   "configs.c4.kernels.skewp.parity.mismatches",
+                   "host_resident.digests_match_device_run", "parity.per_rank[1].mismatches"]
+    assert bench.parity_failures({"parity": {"mismatches": 0}}) == []
+
+
+def test_bench_launcher_command_touches_no_gpu():
+    """`python bench.py --gpus N` with no launcher: the parent builds one torch.distributed.run
+    child (N ranks, rendezvous on 127.0.0.1, the same arguments) without importing torch --
+    no GPU call can precede the child."""
+    import bench
+    cmd, env = bench.launch_command(8, ["--gpus", "8", "--steps", "3"], 29999)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29999" in cmd
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"] and cmd[-5].endswith("bench.py")
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and env["S3H_BENCH_LAUNCHED"] == "1"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4", "--no-c4",
+                        "--print-launch"], capture_output=True, text=True, timeout=120,
+                       env={k: v for k, v in os.environ.items() if k != "WORLD_SIZE"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = json.loads(r.stdout)
+    assert got["torch_imported"] is False
+    assert "--nproc-per-node=4" in got["cmd"]
+    assert got["cmd"][-4:] == ["--gpus", "4", "--no-c4", "--print-launch"]
+
+
+def test_bench_self_launch_runs_n_ranks_on_cpu():
+    """The whole self-launch on a CPU host: `bench.py --gpus 2 --rank-dry-run` starts the child
+    launcher, both ranks join gloo, and the parent's stdout carries ONE line from rank 0 that
+    lists two distinct processes started by the bench's launcher."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--rank-dry-run"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1, r.stdout
+    got = json.loads(lines[0])
+    assert got["n_gpus"] == 2 and [x["rank"] for x in got["ranks"]] == [0, 1]
+    assert len({x["pid"] for x in got["ranks"]}) == 2
+    assert all(x["launched_by_bench"] for x in got["ranks"])
+
+
+def _status_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+
+    def check():
+        if rank == 1:
+            raise RuntimeError("s3hash error -3: synchronisation timeout")
+    try:
+        bench.status_all(dist, world, check)
+        q.put((rank, "no raise"))
+    except bench.DeviceFault as e:
+        q.put((rank, str(e)))
+    dist.barrier()  # every rank still reaches the next collective
+    dist.destroy_process_group()
+
+
+def test_bench_status_fault_on_one_rank_fails_every_rank():
+    """A device fault reported on rank 1 raises on rank 0 too (gathered first), so no rank is
+    left blocked in a collective (world size 2, gloo)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_status_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0] == got[1] == "rank 1: RuntimeError: s3hash error -3: synchronisation timeout"

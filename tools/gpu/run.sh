@@ -14,6 +14,8 @@
 #   pmc[:CTRS[:ARGS]]    rocprofv3 --pmc CTRS (one pass, e.g. FETCH_SIZE) of bench.py ARGS (240 s)
 #   n2[:ARGS]            2-rank torch.distributed.run rehearsal of bench.py on the one GPU
 #                        (S3H_BENCH_SHARE_GPU=1, gloo collectives, as the driver's N>1 runs) (600 s)
+#   selfn:N[:ARGS]       `python bench.py --gpus N ARGS` with NO launcher (bench.py starts the N
+#                        ranks itself) on the one GPU, S3H_BENCH_SHARE_GPU=1          (600 s)
 #   py:SCRIPT[:ARGS]     python SCRIPT ARGS                                  (600 s)
 #   exe:PROGRAM ARGS     a built tool, e.g. tools/ubench_dep                  (300 s)
 set -o pipefail
@@ -50,6 +52,10 @@ for step in "$@"; do
     n2)
       S3H_BENCH_SHARE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 $rest > $out.jsonl 2> $out.err; rc=$?
+      [ $rc -eq 0 ] && python3 tools/gpu/summary.py $out.jsonl ;;
+    selfn)
+      nr=${rest%%:*}; args=""; [ "$rest" != "$nr" ] && args=${rest#*:}
+      S3H_BENCH_SHARE_GPU=1 timeout -k 10 600 python bench.py --gpus $nr $args > $out.jsonl 2> $out.err; rc=$?
       [ $rc -eq 0 ] && python3 tools/gpu/summary.py $out.jsonl ;;
     exe)  # exe:PROGRAM [ARGS] -- a built tool (e.g. tools/ubench_dep), output to .log
       timeout -k 10 300 $rest > $out.log 2>&1; rc=$?

@@ -20,4 +20,8 @@ if isinstance(line.get("configs"), dict):
 if isinstance(line.get("c4"), dict):
     c4 = line["c4"]
     out.append(f"c4 agg {c4.get('aggregate_GiBps')} parity {c4.get('parity')}")
+if "distinct_devices" in line:
+    out.append(f"n_gpus {line.get('n_gpus')} distinct_devices {line['distinct_devices']}")
+if line.get("errors"):
+    out.append(f"ERRORS {line['errors']}")
 print(" | ".join(out))
