@@ -44,7 +44,9 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cctype>
 #include <chrono>
+#include <mutex>
 #include <csignal>
 #include <future>
 #include <random>
@@ -86,13 +88,34 @@ std::vector<Part> geometry(uint64_t size, int jobs, int parts_per_job) {
   return out;
 }
 
+// Value of response header `name` (case-insensitive, up to the first blank: the reference's
+// HTTPHeader regex "name\\s*:\\s*([^\\s]+)", response_parser.cpp:104-112) with its quotes
+// trimmed as TrimETag does (response_parser.cpp:51-62); "" when absent.
+std::string header_value(const std::string& head, const std::string& name) {
+  std::string lower(head);
+  for (char& c : lower) c = char(std::tolower(static_cast<unsigned char>(c)));
+  std::string key = "\r\n" + name + ":";
+  for (char& c : key) c = char(std::tolower(static_cast<unsigned char>(c)));
+  const size_t k = lower.find(key);
+  if (k == std::string::npos) return "";
+  size_t b = k + key.size();
+  while (b < head.size() && (head[b] == ' ' || head[b] == '\t')) ++b;
+  size_t e = b;
+  while (e < head.size() && !std::isspace(static_cast<unsigned char>(head[e]))) ++e;
+  std::string v = head.substr(b, e - b);
+  if (v.size() >= 2 && v.front() == '"') v = v.substr(1, v.size() - 2);
+  else if (v.rfind("&#34;", 0) == 0 && v.size() >= 10) v = v.substr(5, v.size() - 10);
+  return v;
+}
+
 // One UploadPart request over plain HTTP/1.1 (Connection: close): the signed headers, then
 // the body from memory or, for file parts, by sendfile from the open file (what libcurl's
 // read callback does in WebClient::UploadFile, webclient.cpp:331-355).  Returns the HTTP
-// status, or -1 on a socket error.
+// status, or -1 on a socket error; *etag receives the response's ETag (quotes trimmed), which
+// S3Api::UploadFilePart / UploadPart return (multipart_upload.cpp:101-105, 138-143).
 int put_part(const std::string& host, const std::string& port, const std::string& target,
              const s3h::sigv4::Map& headers, const uint8_t* mem, int fd, uint64_t off,
-             uint64_t size) {
+             uint64_t size, std::string* etag) {
   addrinfo hints{}, *ai = nullptr;
   hints.ai_family = AF_UNSPEC;
   hints.ai_socktype = SOCK_STREAM;
@@ -128,14 +151,15 @@ int put_part(const std::string& host, const std::string& port, const std::string
       if (ok) left -= uint64_t(w);
     }
   }
-  std::string resp;
+  std::string resp;  // the status line and every header
   char buf[4096];
-  for (ssize_t r; ok && resp.find("\r\n") == std::string::npos &&
+  for (ssize_t r; ok && resp.find("\r\n\r\n") == std::string::npos &&
                   (r = recv(sock, buf, sizeof buf, 0)) > 0;)
     resp.append(buf, size_t(r));
   close(sock);
   int code = -1;
   if (ok && std::sscanf(resp.c_str(), "HTTP/%*d.%*d %d", &code) != 1) code = -1;
+  if (etag) *etag = header_value(resp.substr(0, resp.find("\r\n\r\n") + 2), "ETag");
   return code;
 }
 
@@ -286,6 +310,7 @@ int main(int argc, char** argv) {
   }
 
   std::vector<std::string> hex(parts.size()), md5b64(content_md5 ? parts.size() : 0);
+  std::vector<uint32_t> md5w(content_md5 ? 4 * parts.size() : 0);  // GPU MD5s: ETag check
   // GPU runtime start-up (device discovery, code-object load) happens once per process in a
   // real uploader: do it before the timed hash stage with a one-part warm-up batch.
   double init_s = 0;
@@ -335,19 +360,41 @@ int main(int argc, char** argv) {
     hostport.emplace_back(send_parts ? ep.substr(h0 + 3, c - h0 - 3) : "", send_parts ? ep.substr(c + 1) : "");
   }
   std::atomic<int> put_failed{0}, retries{0};
+  std::mutex fail_mu;
+  std::vector<std::string> failures;  // "part N: why", for every part that failed for good
   // Part i to endpoint e, signed afresh (new x-amz-date) on every attempt; a failed attempt
-  // is repeated while the shared retry budget lasts (retriesG, upload.cpp:55-69).
+  // is repeated while the shared retry budget lasts (retriesG, upload.cpp:55-69).  As
+  // DoUploadFilePart / DoUploadPart (multipart_upload.cpp:101-105, 138-143) a 200 without an
+  // ETag fails the attempt; with --content-md5 the ETag must also equal the part's MD5 from
+  // the GPU (S3 returns the body's MD5 as a part's ETag), else the attempt fails.
   auto put = [&](size_t i, size_t e) {
     const uint8_t* mem = source == "file" ? nullptr : ptrs[i];
+    std::string why;
     for (;;) {
       const s3h::sigv4::SignConfig c = part_config(i, endpoints[e]);
       const std::string target = "/" + bucket + "/" + key + "?" + s3h::sigv4::UrlEncode(c.parameters);
-      if (put_part(hostport[e].first, hostport[e].second, target, s3h::sigv4::SignHeaders(c), mem,
-                   fd, offs[i], lens[i]) == 200)
+      std::string etag;
+      const int code = put_part(hostport[e].first, hostport[e].second, target,
+                                s3h::sigv4::SignHeaders(c), mem, fd, offs[i], lens[i], &etag);
+      if (code == 200 && etag.empty()) {
+        why = "no ETag found in the HTTP header";
+      } else if (code == 200 && content_md5) {
+        char want[33];
+        md5::hash_to_text(&md5w[4 * i], want);
+        std::string got(etag);
+        for (char& ch : got) ch = char(std::tolower(static_cast<unsigned char>(ch)));
+        if (got == want) return;
+        why = "ETag \"" + etag + "\" != the part's MD5 " + want;
+      } else if (code == 200) {
         return;
+      } else {
+        why = "HTTP status " + std::to_string(code);
+      }
       if (retries++ >= max_retries) break;
     }
     ++put_failed;
+    std::lock_guard<std::mutex> lk(fail_mu);
+    failures.push_back("part " + std::to_string(parts[i].number + 1) + ": " + why);
   };
   std::mt19937 rng{std::random_device{}()};
   std::vector<std::vector<size_t>> job_parts(jobs);
@@ -359,7 +406,7 @@ int main(int argc, char** argv) {
     sha256::hash_to_text(h, t);
     hex[i] = t;
     if (content_md5) {
-      uint32_t m[4];
+      uint32_t* m = &md5w[4 * i];
       md5::md5(ptrs[i], lens[i], m);
       md5b64[i] = base64(reinterpret_cast<const uint8_t*>(m), 16);
     }
@@ -382,6 +429,7 @@ int main(int argc, char** argv) {
         sha256::hash_to_text(const_cast<uint32_t*>(&d.sha256[8 * k]), t);
         hex[idx[k]] = t;
         md5b64[idx[k]] = base64(reinterpret_cast<const uint8_t*>(&d.md5[4 * k]), 16);
+        std::copy(&d.md5[4 * k], &d.md5[4 * k] + 4, &md5w[4 * idx[k]]);
       }
       return;
     }
@@ -521,6 +569,15 @@ int main(int argc, char** argv) {
   if (repeat > 1) std::fprintf(stderr, " (pass %d of %d; first pass %.3f s)", repeat, repeat, first);
   if (!cpu) std::fprintf(stderr, " (GPU runtime start-up before it: %.3f s)", init_s);
   std::fprintf(stderr, "\n");
+  for (const std::string& f : failures) std::fprintf(stderr, "upload failed: %s\n", f.c_str());
+  if (content_md5) {  // the ETag CompleteMultipartUpload would return, from the GPU MD5s
+    try {
+      std::fprintf(stderr, "multipart etag: %s\n", md5::multipart_etag(md5w).c_str());
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "multipart etag: %s\n", e.what());
+      return 1;
+    }
+  }
   if (send_parts && get_verify)
     std::fprintf(stderr, "download verify: %zu parts, %d GETs failed, %llu mismatches (GET %.3f s, %s check %.3f s)\n",
                  parts.size(), get_failed, (unsigned long long)down_bad, t_get, cpu ? "CPU" : "GPU",

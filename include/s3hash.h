@@ -266,6 +266,13 @@ void s3h_cpu_hmac256(const uint8_t *data, uint64_t length, const uint8_t *key,
                      uint64_t key_length, uint8_t mac[32]);
 /* MD5 drop-in (md5::md5, include/md5.h): hash[0..3], digest bytes = words in LE order. */
 void s3h_cpu_md5(const uint8_t *data, uint64_t length, uint32_t hash[4]);
+/* S3 multipart ETag of an object from its parts' MD5 digests (n x 4 words, as the MD5 batch
+ * entry points return them, in part order): lowercase hex of MD5(the n 16-byte digests
+ * concatenated) + "-" + n, NUL-terminated, into out (out_len >= S3H_ETAG_MAX).  This is the
+ * ETag CompleteMultipartUpload returns (lib/src/api/multipart_upload.cpp:162-183); an
+ * uploader compares it with the server's.  CPU (16 B per part).  S3H_EINVAL for n == 0. */
+#define S3H_ETAG_MAX 56
+int s3h_multipart_etag(const uint32_t *md5_digests, uint64_t n, char *out, uint64_t out_len);
 /* lowercase hex of the 32 digest bytes + NUL (sha256::hash_to_text). */
 void s3h_hash_to_text(const uint32_t hash[8], char text[65]);
 /* "sha-ni" or "scalar": which compression the CPU drop-in dispatched to. */

@@ -189,3 +189,18 @@ class stream_batch {
 };
 
 }  // namespace sha256
+
+namespace md5 {
+
+// The multipart ETag an S3 endpoint returns from CompleteMultipartUpload
+// (lib/src/api/multipart_upload.cpp:162-183), from the parts' MD5 digests in part order
+// (4 words per part, as DualDigests::md5 / s3h_md5_batch_* return them): s3h_multipart_etag.
+inline std::string multipart_etag(const std::vector<uint32_t>& part_md5s) {
+  if (part_md5s.empty() || part_md5s.size() % 4)
+    throw std::invalid_argument("multipart_etag: need 4 words per part and at least one part");
+  char out[S3H_ETAG_MAX];
+  sha256::batch_check(s3h_multipart_etag(part_md5s.data(), part_md5s.size() / 4, out, sizeof out));
+  return out;
+}
+
+}  // namespace md5

@@ -37,7 +37,7 @@ C_ABI_SYMBOLS = (
     "s3h_sha256_md5_batch_host", "s3h_sha256_md5_batch_device", "s3h_trim",
     "s3h_sha256_file_parts", "s3h_sha256_batch_host_on", "s3h_plan_groups",
     "s3h_sha256_md5_file_parts", "s3h_plan_status", "s3h_stream_status", "s3h_host_threads",
-    "s3h_plan_dual_solo", "s3h_device_pci_bus_id",
+    "s3h_plan_dual_solo", "s3h_device_pci_bus_id", "s3h_multipart_etag",
 )
 ALGO_SHA256, ALGO_MD5 = 0, 1
 ALGO_IDS = {"sha256": ALGO_SHA256, "md5": ALGO_MD5}
@@ -146,6 +146,8 @@ def lib() -> ctypes.CDLL:
             L.s3h_cpu_backend.restype = ctypes.c_char_p
             L.s3h_cpu_md5.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
             L.s3h_cpu_md5.restype = None
+            L.s3h_multipart_etag.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p,
+                                             ctypes.c_uint64]
             L.s3h_stream_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                             ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
             L.s3h_stream_update_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, u64p, u64p,

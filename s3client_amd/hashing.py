@@ -268,10 +268,12 @@ def verify_batch_device(data, offsets, lengths, expected, algo: str = "sha256", 
 
 
 def multipart_etag(part_md5s) -> str:
-    """S3 multipart ETag: hex(MD5(concatenated binary part MD5s)) + "-" + part count.
-    The outer MD5 (16 B per part) runs on the lib/hash MD5 drop-in."""
+    """S3 multipart ETag: hex(MD5(concatenated binary part MD5s)) + "-" + part count
+    (s3h_multipart_etag; the outer MD5, 16 B per part, runs on the lib/hash MD5 drop-in)."""
     w = np.ascontiguousarray(part_md5s, dtype=np.uint32).reshape(-1, 4)
-    return md5(w.tobytes()).tobytes().hex() + f"-{w.shape[0]}"
+    out = ctypes.create_string_buffer(56)
+    check(lib().s3h_multipart_etag(w.ctypes.data, w.shape[0], out, len(out)))
+    return out.value.decode()
 
 
 class Stream:

@@ -19,7 +19,9 @@ With `--store` the parts are kept and a signed `GET /{bucket}/{key}` with `Range
 returns that range of the parts concatenated in part-number order (the ranged GETs of
 lib/src/download.cpp:72-103); `--corrupt-get K` flips one byte of the K-th GET's body.
 `--fail-every K` answers every K-th PUT with 503 SlowDown after reading it (to exercise the
-uploader's retries, upload.cpp:55-87).  `GET /stats` returns JSON counts.  Run: `s3_mock_server.py --port 0 --port-file F` (prints
+uploader's retries, upload.cpp:55-87).  `--wrong-etag-part N` answers part N's PUTs with an
+ETag that is not the body's MD5 (a server-side corruption the uploader's ETag check must
+catch).  `GET /stats` returns JSON counts.  Run: `s3_mock_server.py --port 0 --port-file F` (prints
 the bound port).  Nothing is stored."""
 import argparse
 import base64
@@ -68,6 +70,7 @@ class Handler(BaseHTTPRequestHandler):
     fail_every = 0
     store = False
     corrupt_get = 0
+    wrong_etag_part = 0
     objects = {}  # "/bucket/key" -> {part number: bytes}
     gets = 0
     lock = threading.Lock()
@@ -158,14 +161,18 @@ class Handler(BaseHTTPRequestHandler):
             with self.lock:
                 self.stats["bad_signature"] += 1
             return self._reply(403, b"SignatureDoesNotMatch")
+        path, _, query = self.path.partition("?")
+        pn = int(dict(urllib.parse.parse_qsl(query)).get("partNumber", "0"))
+        etag = hashlib.md5(body).hexdigest()
         with self.lock:
             self.stats["parts"] += 1
             self.stats["bytes"] += n
             if self.store:
-                path, _, query = self.path.partition("?")
-                pn = int(dict(urllib.parse.parse_qsl(query)).get("partNumber", "0"))
                 self.objects.setdefault(path, {})[pn] = body
-        self._reply(200, etag=hashlib.md5(body).hexdigest())
+            if pn == self.wrong_etag_part:
+                self.stats["wrong_etags"] = self.stats.get("wrong_etags", 0) + 1
+                etag = hashlib.md5(body + b"x").hexdigest()
+        self._reply(200, etag=etag)
 
 
 def main():
@@ -176,7 +183,9 @@ def main():
     ap.add_argument("--fail-every", type=int, default=0)
     ap.add_argument("--store", action="store_true")
     ap.add_argument("--corrupt-get", type=int, default=0)
+    ap.add_argument("--wrong-etag-part", type=int, default=0)
     a = ap.parse_args()
+    Handler.wrong_etag_part = a.wrong_etag_part
     Handler.secret = a.secret
     Handler.fail_every = a.fail_every
     Handler.store = a.store

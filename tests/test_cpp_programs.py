@@ -238,6 +238,45 @@ def test_upload_send_content_md5_gpu(programs, tmp_path, golden, s3_mock, source
     assert s["parts"] == 6 and s["md5_checked"] == 6 and s["bad_md5"] == 0, s
 
 
+def _etag_round(args, tmp_path, golden):
+    """--content-md5 upload of the transfer geometry to a correct endpoint and to one that
+    returns a wrong ETag for part 4: the first succeeds and prints the multipart ETag (the
+    compiled reference's md5 golden), the second fails naming part 4, retries included."""
+    want = golden["md5"]["transfer_etag"]
+    proc, url, stats = _start_mock()
+    try:
+        r, _ = _upload(args + ["--content-md5"], url, tmp_path, golden)
+        assert r.returncode == 0, r.stderr
+        assert f"multipart etag: {want}" in r.stderr, r.stderr
+    finally:
+        proc.kill()
+        proc.wait()
+    proc, url, stats = _start_mock("--wrong-etag-part", "4")
+    try:
+        r, _ = _upload(args + ["--content-md5", "--retries", "2"], url, tmp_path, golden)
+        assert r.returncode == 1, r.stderr
+        assert "1 of 6 PUTs not 200" in r.stderr and "upload failed: part 4: ETag" in r.stderr, r.stderr
+        assert "upload failed: part" not in r.stderr.replace("upload failed: part 4:", ""), r.stderr
+        assert stats()["wrong_etags"] == 3  # the first attempt and both retries
+    finally:
+        proc.kill()
+        proc.wait()
+
+
+def test_upload_etag_check_cpu(programs, tmp_path, golden):
+    """UploadPart's ETag (multipart_upload.cpp:101-105, 138-143) checked against each part's MD5."""
+    _etag_round(["--cpu"], tmp_path, golden)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("source", ["file", "memory"])
+def test_upload_etag_check_gpu(programs, tmp_path, golden, source):
+    """The same with both digests from the GPU's dual pass: every returned ETag compared with
+    the part's GPU MD5, a wrong one fails its part (named), the multipart ETag from the GPU
+    MD5s equals the reference's."""
+    _etag_round(["--source", source], tmp_path, golden)
+
+
 def test_upload_then_download_verify_cpu(programs, tmp_path, golden):
     """--get-verify: after the upload each job GETs its parts back by byte range (download.cpp
     geometry) from the storing endpoint and every part is checked against the digest it was

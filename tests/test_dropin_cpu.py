@@ -97,7 +97,9 @@ def test_cpu_md5_golden(golden, oracle):
 
 def test_multipart_etag_golden(golden):
     words = [np.frombuffer(bytes.fromhex(p["digest"]), dtype=np.uint32) for p in golden["md5"]["transfer"]]
-    assert s3.multipart_etag(np.stack(words)) == golden["md5"]["transfer_etag"]
+    assert s3.multipart_etag(np.stack(words)) == golden["md5"]["transfer_etag"]  # s3h_multipart_etag
+    with pytest.raises(s3.S3HashError):
+        s3.multipart_etag(np.zeros((0, 4), dtype=np.uint32))
 
 
 def test_kernel_isa_counts_match_the_built_code_object(tmp_path):
