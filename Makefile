@@ -20,7 +20,7 @@ all: $(LIB) oracle cpptests
 # error-word check are read from the gfx950 code object the linked library ships
 # (tools/isa_counts.py -> s3client_amd/kernel_isa_counts.json; disassembly in build/isa).
 ISA_DIS := build/isa/libs3hash_gfx950.dis
-KSRC := $(CSRC)/capi.hip $(CSRC)/sha256_kernels.hip $(CSRC)/sha256_device.hpp $(CSRC)/sha256_skew_rounds.inc $(CSRC)/sha256_producer_simple.inc $(CSRC)/md5_step_asm.inc include/s3hash.h
+KSRC := $(CSRC)/capi.hip $(CSRC)/route.hpp $(CSRC)/sha256_kernels.hip $(CSRC)/sha256_device.hpp $(CSRC)/sha256_skew_rounds.inc $(CSRC)/sha256_producer_simple.inc $(CSRC)/md5_step_asm.inc include/s3hash.h
 $(LIBDIR)/capi.o: $(KSRC)
 	@mkdir -p $(LIBDIR) build/isa
 	cd build/isa && $(HIPCC) $(HIPFLAGS) -save-temps -c -o ../../$@ ../../$<

@@ -28,10 +28,13 @@
 //                    is forwarded into the signature as DoUploadFilePart does (:81-86).
 //   --per-job        one batch call per job thread at the same time (std::async per job, as
 //                    upload.cpp:136-140 runs UploadParts), instead of one call for all parts.
+//   --route R        gpu (default) | cpu | auto: where the SHA-256 batch call runs
+//                    (s3h_sha256_*_routed: auto = whichever the measured model says finishes
+//                    first -- a few large parts go to the CPU drop-in, hundreds to the GPU).
 //
 //   s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory] [--per-job]
 //                  [--cpu] [--verify] [--print-headers] [--send] [--get-verify] [--retries N]
-//                  [--content-md5]
+//                  [--content-md5] [--route gpu|cpu|auto]
 //                  [--devices N]
 //                  [--repeat R] [--endpoint URL[,URL...] --bucket B --key K --access A
 //                  --secret S --upload-id ID]
@@ -230,7 +233,7 @@ void usage() {
   std::fprintf(stderr,
                "usage: s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory]\n"
                "       [--per-job] [--cpu] [--verify] [--print-headers] [--send] [--get-verify]\n"
-               "       [--retries N] [--content-md5]\n"
+               "       [--retries N] [--content-md5] [--route gpu|cpu|auto]\n"
                "       [--endpoint URL[,URL...] --bucket B --key K --access A --secret S --upload-id ID]\n"
                "       [--devices N] [--repeat R]\n");
 }
@@ -241,6 +244,7 @@ int main(int argc, char** argv) {
   std::string file, endpoint = "http://127.0.0.1:9000", bucket = "bucket1", key = "key1";
   std::string access = "ACCESS", secret = "SECRET", upload_id = "UPLOAD-ID";
   std::string source = "file";
+  std::string route_name = "gpu";
   int jobs = 1, ppj = 1, devices = 0, repeat = 1, max_retries = 0;
   bool cpu = false, verify = false, print_headers = false, per_job = false, send_parts = false;
   bool content_md5 = false;  // also send Content-MD5: both digests from one pass
@@ -271,11 +275,17 @@ int main(int argc, char** argv) {
     else if (a == "--repeat") repeat = std::atoi(next().c_str());
     else if (a == "--source") source = next();
     else if (a == "--per-job") per_job = true;
+    else if (a == "--route") route_name = next();
     else { usage(); return 2; }
   }
   std::signal(SIGPIPE, SIG_IGN);  // a closed connection fails its PUT (sendfile has no MSG_NOSIGNAL)
   if (file.empty() || jobs < 1 || ppj < 1 || repeat < 1 ||
-      (source != "file" && source != "mmap" && source != "memory")) { usage(); return 2; }
+      (source != "file" && source != "mmap" && source != "memory") ||
+      (route_name != "gpu" && route_name != "cpu" && route_name != "auto")) { usage(); return 2; }
+  const sha256::Route route = route_name == "cpu"    ? sha256::Route::cpu
+                              : route_name == "auto" ? sha256::Route::automatic
+                                                     : sha256::Route::gpu;
+  sha256::Route route_taken = route;
 
   const int fd = open(file.c_str(), O_RDONLY);
   if (fd < 0) { std::perror(file.c_str()); return 1; }
@@ -433,9 +443,9 @@ int main(int argc, char** argv) {
       }
       return;
     }
-    const std::vector<std::string> h = source == "file"
-                                           ? sha256::file_part_hashes(file, o, l, devices)
-                                           : sha256::payload_hashes(p, l, devices);
+    const std::vector<std::string> h =
+        source == "file" ? sha256::file_part_hashes(file, o, l, devices, route, &route_taken)
+                         : sha256::payload_hashes(p, l, devices, route, &route_taken);
     for (size_t k = 0; k < idx.size(); ++k) hex[idx[k]] = h[k];
   };
   // One pass over all parts.  Job threads as upload.cpp:136-140 runs them: the CPU drop-in
@@ -558,7 +568,10 @@ int main(int argc, char** argv) {
         std::printf("# part %d %s: %s\n", parts[i].number, kv.first.c_str(), kv.second.c_str());
   std::string what = cpu ? std::string("cpu lib/hash drop-in")
                          : "gpu batch (H2D included, source " + source +
-                               (per_job ? ", one call per job" : ", one call") + ")";
+                               (per_job ? ", one call per job" : ", one call") +
+                               (route == sha256::Route::gpu ? std::string()
+                                : std::string(", route ") + route_name + " -> " +
+                                      (route_taken == sha256::Route::cpu ? "cpu" : "gpu")) + ")";
   if (send_parts) what = "upload (hash + PUT to " + endpoint + ", " + std::to_string(jobs) + " jobs), " + what;
   std::fprintf(stderr, "%s: %zu parts, %.3f GiB in %.3f s = %.3f GiB/s%s", what.c_str(), parts.size(),
                double(size) / (1 << 30), dt, double(size) / (1 << 30) / dt,

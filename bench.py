@@ -891,7 +891,9 @@ def c5_loopback(data, offs, lens, gd, nparts: int = 128, jobs: int = 16, repeat:
     tests/s3_mock_server.py, which re-hashes every body (hashlib) and verifies every SigV4
     signature.  Wall-clock of the whole pass (hash + upload; --repeat: the last pass) for the
     GPU batch (one call, and one call per job: merged on the device), the CPU SHA-NI drop-in
-    and its scalar loop (lib/hash-like cost), plus the GPU hash alone."""
+    and its scalar loop (lib/hash-like cost), the size-aware route (--route auto: the measured
+    model picks the GPU or the CPU drop-in for the batch; `auto_route` says which), plus the
+    GPU hash alone."""
     import re
     import subprocess
     import tempfile
@@ -918,6 +920,7 @@ def c5_loopback(data, offs, lens, gd, nparts: int = 128, jobs: int = 16, repeat:
                                      ("gpu_per_job", ["--send", "--per-job"], {}),
                                      ("cpu_shani", ["--send", "--cpu"], {}),
                                      ("cpu_scalar", ["--send", "--cpu"], {"S3H_CPU_SCALAR": "1"}),
+                                     ("auto", ["--send", "--route", "auto"], {}),
                                      ("gpu_hash_only", [], {})):
                 r = subprocess.run([app, "-f", path, "-j", str(jobs), "-n", str(nparts // jobs),
                                     "--endpoint", url, "--repeat", str(repeat), *extra],
@@ -929,6 +932,9 @@ def c5_loopback(data, offs, lens, gd, nparts: int = 128, jobs: int = 16, repeat:
                     res["error"] = f"{name}: rc {r.returncode}, digests match {got == want}"
                     break
                 res["seconds"][name] = float(m.group(1))
+                if name == "auto":
+                    ra = re.search(r"route auto -> (\w+)", r.stderr)
+                    res["auto_route"] = ra.group(1) if ra else None
             with urllib.request.urlopen(url + "/stats", timeout=10) as f:
                 res["server"] = json.loads(f.read())
         except (OSError, ValueError, subprocess.SubprocessError) as e:

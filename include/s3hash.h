@@ -208,6 +208,41 @@ int s3h_sha256_md5_batch_device(int device, const void *d_base, const uint64_t *
                                 const uint64_t *lengths, uint64_t n, uint32_t *d_sha256,
                                 uint32_t *d_md5, void *stream);
 
+/* ---------------------------------------------------------------- size-aware routing
+ * One part's chain runs at ~69 MB/s on the GPU and ~1.5 GB/s on one SHA-NI core, so a batch
+ * of a few large parts -- the per-job batches of lib/src/upload.cpp:89-110, 136-140 -- is
+ * faster on the CPU drop-in, and a batch of hundreds is faster on the GPU.  The routed entry
+ * points take a route: S3H_ROUTE_GPU = s3h_sha256_batch_host / s3h_sha256_file_parts
+ * unchanged (the default everywhere); S3H_ROUTE_CPU = the lib/hash drop-in (sha256::sha256)
+ * on s3h_host_threads' CPU count, parts longest first; S3H_ROUTE_AUTO = whichever the model
+ * below estimates to finish first.  The model's rates are measured once per process on the
+ * first AUTO call (~0.1 s: a lone GPU chain, a pinned 32 MiB H2D copy, a one-block host call,
+ * 4 MiB on the drop-in).  AUTO needs a visible GPU (S3H_ENODEV otherwise): it chooses
+ * between two paths with identical digests and is never a fallback for a missing device.
+ * *taken (if non-null) receives the route that ran (S3H_ROUTE_GPU or S3H_ROUTE_CPU).
+ *   gpu_s = call_s + max(longest part / chain rate, bytes per device / H2D rate)
+ *   cpu_s = max(bytes / (threads x per-thread rate), longest part / per-thread rate) */
+enum s3h_route { S3H_ROUTE_GPU = 0, S3H_ROUTE_CPU = 1, S3H_ROUTE_AUTO = 2 };
+typedef struct {
+  double cpu_bytes_per_s;   /* one host thread on the lib/hash drop-in (s3h_cpu_backend) */
+  double chain_bytes_per_s; /* one part's chain on the GPU (the skew kernel, a lone part) */
+  double h2d_bytes_per_s;   /* pinned host -> device copy, one device */
+  double call_s;            /* fixed cost of one host-path GPU call (setup, launch, sync) */
+  int cpu_threads;          /* host threads of the CPU route (affinity and cgroup quota) */
+  int devices;              /* visible HIP devices */
+} s3h_route_model_t;
+/* The measured model (measures it on first use).  S3H_ENODEV without a GPU (cpu fields set). */
+int s3h_route_model(s3h_route_model_t *m);
+/* AUTO's choice for `lengths` under model *m (any model, e.g. a recorded one; pure host
+ * arithmetic): returns S3H_ROUTE_GPU or S3H_ROUTE_CPU and both time estimates in seconds. */
+int s3h_route_estimate(const s3h_route_model_t *m, const uint64_t *lengths, uint64_t n,
+                       int ndevices, double *gpu_s, double *cpu_s);
+int s3h_sha256_batch_routed(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
+                            uint32_t *digests, int ndevices, int route, int *taken);
+int s3h_sha256_file_parts_routed(const char *path, const uint64_t *offsets,
+                                 const uint64_t *lengths, uint64_t n, uint32_t *digests,
+                                 int ndevices, int route, int *taken);
+
 /* ---------------------------------------------------------------- verification
  * Download-side check of parts against known digests (ranged GETs of
  * lib/src/download.cpp:88-103; expected = the uploader's x-amz-content-sha256 / Content-MD5).

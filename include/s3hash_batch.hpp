@@ -1,7 +1,8 @@
 // include/s3hash_batch.hpp -- C++ convenience layer over the C-ABI (include/s3hash.h) in the
 // same `namespace sha256` as the lib/hash drop-in, for C++ callers such as the parallel
 // upload (the reference's lib/src/upload.cpp:89-110 insertion point).  Header-only; every
-// call goes to the GPU through libs3hash.so and throws on error (no CPU fallback).
+// call goes to the GPU through libs3hash.so and throws on error (no CPU fallback) -- unless
+// the caller passes Route::cpu or Route::automatic to payload_hashes / file_part_hashes.
 #pragma once
 #include <cstdint>
 #include <stdexcept>
@@ -44,14 +45,14 @@ inline void sha256_batch_device(int device, const void* d_base,
                                       offsets.size(), d_digests, stream));
 }
 
-// 64-char lowercase hex per part: the `payloadHash` strings S3Api::UploadFilePart takes
-// (lib/include/s3-api.h:447-452).
-inline std::vector<std::string> payload_hashes(const std::vector<const uint8_t*>& parts,
-                                               const std::vector<uint64_t>& lengths,
-                                               int ndevices = 0) {
-  const std::vector<uint32_t> d = sha256_batch(parts, lengths, ndevices);
-  std::vector<std::string> out(parts.size());
-  for (size_t i = 0; i < parts.size(); ++i) {
+// Where a host batch is hashed (include/s3hash.h "size-aware routing"): gpu = the batched GPU
+// path (default), cpu = the lib/hash drop-in on host threads, automatic = whichever a model
+// measured once per process estimates to finish first (needs a GPU; never a fallback).
+enum class Route { gpu = S3H_ROUTE_GPU, cpu = S3H_ROUTE_CPU, automatic = S3H_ROUTE_AUTO };
+
+inline std::vector<std::string> to_hex(const std::vector<uint32_t>& d) {
+  std::vector<std::string> out(d.size() / 8);
+  for (size_t i = 0; i < out.size(); ++i) {
     char t[65];
     hash_to_text(const_cast<uint32_t*>(&d[8 * i]), t);
     out[i] = t;
@@ -59,24 +60,44 @@ inline std::vector<std::string> payload_hashes(const std::vector<const uint8_t*>
   return out;
 }
 
+// 64-char lowercase hex per part: the `payloadHash` strings S3Api::UploadFilePart takes
+// (lib/include/s3-api.h:447-452).  *taken (if non-null) receives the route that ran.
+inline std::vector<std::string> payload_hashes(const std::vector<const uint8_t*>& parts,
+                                               const std::vector<uint64_t>& lengths,
+                                               int ndevices = 0, Route route = Route::gpu,
+                                               Route* taken = nullptr) {
+  if (parts.size() != lengths.size()) throw std::invalid_argument("parts/lengths size mismatch");
+  if (route == Route::gpu) {
+    if (taken) *taken = Route::gpu;
+    return to_hex(sha256_batch(parts, lengths, ndevices));
+  }
+  std::vector<uint32_t> d(8 * parts.size());
+  int t = S3H_ROUTE_GPU;
+  if (!parts.empty())
+    batch_check(s3h_sha256_batch_routed(parts.data(), lengths.data(), parts.size(), d.data(),
+                                        ndevices, int(route), &t));
+  if (taken) *taken = Route(t);
+  return to_hex(d);
+}
+
 // Digests of byte ranges of a file -- the (file, offset, size) parts UploadFilePart sends --
 // read by host threads straight into pinned staging (s3h_sha256_file_parts), as hex.
 inline std::vector<std::string> file_part_hashes(const std::string& path,
                                                  const std::vector<uint64_t>& offsets,
                                                  const std::vector<uint64_t>& lengths,
-                                                 int ndevices = 0) {
+                                                 int ndevices = 0, Route route = Route::gpu,
+                                                 Route* taken = nullptr) {
   if (offsets.size() != lengths.size()) throw std::invalid_argument("offsets/lengths size mismatch");
   std::vector<uint32_t> d(8 * offsets.size());
-  if (!offsets.empty())
+  int t = S3H_ROUTE_GPU;
+  if (!offsets.empty() && route == Route::gpu)
     batch_check(s3h_sha256_file_parts(path.c_str(), offsets.data(), lengths.data(), offsets.size(),
                                       d.data(), ndevices, 0));
-  std::vector<std::string> out(offsets.size());
-  for (size_t i = 0; i < offsets.size(); ++i) {
-    char t[65];
-    hash_to_text(&d[8 * i], t);
-    out[i] = t;
-  }
-  return out;
+  else if (!offsets.empty())
+    batch_check(s3h_sha256_file_parts_routed(path.c_str(), offsets.data(), lengths.data(),
+                                             offsets.size(), d.data(), ndevices, int(route), &t));
+  if (taken) *taken = Route(t);
+  return to_hex(d);
 }
 
 // Release the host path's cached per-device buffers (s3h_trim).

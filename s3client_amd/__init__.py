@@ -8,7 +8,9 @@ from .hashing import (Plan, device_count, digests_to_text, generate_parts, hash_
                       verify_batch_device, verify_batch_host, Stream,
                       sha256_md5_batch_device, sha256_md5_batch_host, sha256_file_parts,
                       sha256_md5_file_parts,
-                      trim, sha256_batch_host_on, host_threads, device_pci_bus_id)
+                      trim, sha256_batch_host_on, host_threads, device_pci_bus_id,
+                      route_model, route_estimate, sha256_batch_routed,
+                      sha256_file_parts_routed)
 from .upload import upload_parts_geometry, UploadPart
 from ._native import S3HashError, LIB_PATH
 
@@ -18,5 +20,6 @@ __all__ = ["Plan", "device_count", "digests_to_text", "generate_parts", "hash_to
            "verify_batch_device", "verify_batch_host", "Stream",
            "sha256_md5_batch_device", "sha256_md5_batch_host", "sha256_file_parts",
            "sha256_md5_file_parts", "trim", "sha256_batch_host_on", "host_threads",
-           "device_pci_bus_id",
+           "device_pci_bus_id", "route_model", "route_estimate", "sha256_batch_routed",
+           "sha256_file_parts_routed",
            "upload_parts_geometry", "UploadPart", "S3HashError", "LIB_PATH"]

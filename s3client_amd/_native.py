@@ -38,7 +38,21 @@ C_ABI_SYMBOLS = (
     "s3h_sha256_file_parts", "s3h_sha256_batch_host_on", "s3h_plan_groups",
     "s3h_sha256_md5_file_parts", "s3h_plan_status", "s3h_stream_status", "s3h_host_threads",
     "s3h_plan_dual_solo", "s3h_device_pci_bus_id", "s3h_multipart_etag",
+    "s3h_route_model", "s3h_route_estimate", "s3h_sha256_batch_routed",
+    "s3h_sha256_file_parts_routed",
 )
+ROUTE_GPU, ROUTE_CPU, ROUTE_AUTO = 0, 1, 2
+ROUTE_IDS = {"gpu": ROUTE_GPU, "cpu": ROUTE_CPU, "auto": ROUTE_AUTO}
+ROUTE_NAMES = {v: k for k, v in ROUTE_IDS.items()}
+
+
+class RouteModel(ctypes.Structure):
+    """s3h_route_model_t (include/s3hash.h)."""
+    _fields_ = [("cpu_bytes_per_s", ctypes.c_double), ("chain_bytes_per_s", ctypes.c_double),
+                ("h2d_bytes_per_s", ctypes.c_double), ("call_s", ctypes.c_double),
+                ("cpu_threads", ctypes.c_int), ("devices", ctypes.c_int)]
+
+
 ALGO_SHA256, ALGO_MD5 = 0, 1
 ALGO_IDS = {"sha256": ALGO_SHA256, "md5": ALGO_MD5}
 DIGEST_WORDS = {ALGO_SHA256: 8, ALGO_MD5: 4}
@@ -146,6 +160,17 @@ def lib() -> ctypes.CDLL:
             L.s3h_cpu_backend.restype = ctypes.c_char_p
             L.s3h_cpu_md5.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
             L.s3h_cpu_md5.restype = None
+            L.s3h_route_model.argtypes = [ctypes.POINTER(RouteModel)]
+            L.s3h_route_estimate.argtypes = [ctypes.POINTER(RouteModel), u64p, ctypes.c_uint64,
+                                             ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                             ctypes.POINTER(ctypes.c_double)]
+            L.s3h_sha256_batch_routed.argtypes = [ctypes.POINTER(ctypes.c_void_p), u64p,
+                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
+                                                  ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+            L.s3h_sha256_file_parts_routed.argtypes = [ctypes.c_char_p, u64p, u64p,
+                                                       ctypes.c_uint64, ctypes.c_void_p,
+                                                       ctypes.c_int, ctypes.c_int,
+                                                       ctypes.POINTER(ctypes.c_int)]
             L.s3h_multipart_etag.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p,
                                              ctypes.c_uint64]
             L.s3h_stream_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64,

@@ -1950,3 +1950,5 @@ int s3h_stream_destroy(s3h_stream_t S) {
 }
 
 }  // extern "C"
+
+#include "route.hpp"

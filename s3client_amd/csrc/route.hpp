@@ -1,0 +1,292 @@
+// route.hpp -- size-aware routing of host-resident batches (included at the end of capi.hip).
+//
+// One part's SHA-256 is one sequential chain: on the GPU it runs at ~69 MB/s (the skew
+// kernel's per-wave issue bound), on one EPYC core with SHA-NI at ~1.5 GB/s.
+// The GPU wins only when a batch has enough parts to fill its lanes -- and the reference's
+// callers are per-job batches of a few parts (lib/src/upload.cpp:89-110, 136-140), exactly the
+// shape where it loses (128 x 8 MiB took 0.123 s on the GPU against 0.045 s on 16
+// SHA-NI threads).  S3H_ROUTE_AUTO sends each batch where a measured model says it finishes
+// first:
+//   gpu_s = call_s + max(longest part / chain rate, bytes per device / H2D rate)
+//   cpu_s = max(bytes / (threads x per-thread rate), longest part / per-thread rate)
+// The four rates are measured ONCE per process (route_model, ~0.1 s on the first AUTO call)
+// on this host and device, and s3h_route_model reports them.  AUTO needs a visible GPU
+// (S3H_ENODEV otherwise): it is a routing choice between two equal-result paths, never a
+// fallback for a missing device.  S3H_ROUTE_GPU (the default everywhere, and the only route
+// the bench metric uses) is s3h_sha256_batch_host / s3h_sha256_file_parts unchanged.
+
+#include "../../include/sha256.h"
+
+namespace {
+
+// CPU route: the lib/hash drop-in (sha256::sha256, SHA-NI when CPUID has it) on host threads,
+// parts handed out longest first.  File ranges are pread in 4 MiB chunks and streamed through
+// sha256_stream, the last chunk padded with the part's total length (sha256_next's contract).
+int cpu_batch(const uint8_t* const* parts, int fd, const uint64_t* offsets,
+              const uint64_t* lengths, uint64_t n, uint32_t* digests, unsigned threads) {
+  std::vector<uint64_t> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(),
+                   [&](uint64_t a, uint64_t b) { return lengths[a] > lengths[b]; });
+  std::atomic<uint64_t> next{0};
+  std::atomic<int> io_error{0};
+  auto work = [&] {
+    constexpr uint64_t kChunk = 4ull << 20;
+    std::vector<uint8_t> buf(fd >= 0 ? kChunk : 0);
+    for (uint64_t k; (k = next.fetch_add(1)) < n && !io_error.load();) {
+      const uint64_t i = order[k];
+      uint32_t* h = digests + 8 * i;
+      if (fd < 0 || lengths[i] == 0) {  // (sha256_next pads only when total_length > 0)
+        sha256::sha256(fd < 0 ? parts[i] : buf.data(), lengths[i], h);
+        continue;
+      }
+      sha256::init_hash(h);
+      uint64_t done = 0;
+      do {
+        const uint64_t want = std::min(kChunk, lengths[i] - done);
+        for (uint64_t got = 0; got < want;) {
+          const ssize_t r = pread(fd, buf.data() + got, want - got, off_t(offsets[i] + done + got));
+          if (r <= 0) {
+            io_error = 1;
+            return;
+          }
+          got += uint64_t(r);
+        }
+        if (done + want < lengths[i]) sha256::sha256_stream(h, buf.data(), want);
+        else sha256::sha256_next(buf.data(), uint32_t(want), h, lengths[i], nullptr);
+        done += want;
+      } while (done < lengths[i]);
+      sha256::to_little(h);
+    }
+  };
+  const unsigned t = unsigned(std::min<uint64_t>(std::max(1u, threads), n));
+  std::vector<std::thread> pool;
+  for (unsigned k = 1; k < t; ++k) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+  if (io_error) return fail(S3H_EINVAL, "cpu route: reading a file range failed");
+  return S3H_OK;
+}
+
+struct RouteModel {
+  s3h_route_model_t m{};
+  int rc = S3H_OK;
+  std::string err;
+};
+
+double seconds_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// Measures the model's rates on this host and device 0 (once per process).
+RouteModel measure_route_model() {
+  RouteModel R;
+  s3h_route_model_t& m = R.m;
+  m.cpu_threads = int(host_cpus());
+  {  // one host thread on the drop-in: best of 3 over 4 MiB
+    std::vector<uint8_t> buf(4u << 20, 0x5a);
+    uint32_t h[8];
+    double best = 1e30;
+    for (int r = 0; r < 3; ++r) {
+      const auto t0 = std::chrono::steady_clock::now();
+      sha256::sha256(buf.data(), buf.size(), h);
+      best = std::min(best, seconds_since(t0));
+    }
+    m.cpu_bytes_per_s = double(buf.size()) / best;
+  }
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+    R.rc = S3H_ENODEV;
+    R.err = "no HIP device visible (S3H_ROUTE_AUTO chooses between the GPU and the CPU drop-in; "
+            "it is not a fallback)";
+    return R;
+  }
+  m.devices = count;
+  DeviceGuard g(0);
+  auto hip_fail = [&](const char* what, hipError_t e) {
+    R.rc = S3H_EHIP;
+    R.err = std::string("route model: ") + what + ": " + hipGetErrorString(e);
+    return R;
+  };
+  hipStream_t s = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  uint8_t *d = nullptr, *hp = nullptr;
+  uint32_t* dd = nullptr;
+  constexpr uint64_t kChain = 1ull << 20, kCopy = 32ull << 20;
+  hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&e0);
+  if (e == hipSuccess) e = hipEventCreate(&e1);
+  if (e == hipSuccess) e = hipMalloc(&d, kCopy);
+  if (e == hipSuccess) e = hipMalloc(&dd, 32);
+  if (e == hipSuccess) e = hipHostMalloc(&hp, kCopy, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipMemsetAsync(d, 0, kCopy, s);
+  if (e == hipSuccess) std::memset(hp, 0x5a, kCopy);
+  float ms = 0;
+  // one lone chain (the skew kernel, 1 MiB = 16K blocks, ~15 ms): chain rate
+  s3h_plan_s* P = nullptr;
+  const uint64_t off = 0, len = kChain;
+  if (e == hipSuccess) {
+    if (int rc = plan_build(0, S3H_ALGO_SHA256, &off, &len, 1, S3H_KERNEL_AUTO, &P)) {
+      R.rc = rc;
+      R.err = g_err;
+    }
+  }
+  if (e == hipSuccess && P) {  // best of launches 2-3 (the first ramps the clock up)
+    double best = 1e30;
+    for (int r = 0; r < 3 && e == hipSuccess; ++r) {
+      e = hipEventRecord(e0, s);
+      if (e == hipSuccess && s3h_plan_launch(P, d, dd, s) != S3H_OK) e = hipErrorLaunchFailure;
+      if (e == hipSuccess) e = hipEventRecord(e1, s);
+      if (e == hipSuccess) e = hipEventSynchronize(e1);
+      if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+      if (e == hipSuccess && r > 0) best = std::min(best, double(ms) * 1e-3);
+    }
+    if (e == hipSuccess) m.chain_bytes_per_s = double(kChain) / best;
+    if (e == hipSuccess && s3h_plan_status(P, s) != S3H_OK) e = hipErrorLaunchFailure;
+  }
+  // pinned host -> device copy: best of 3 over 32 MiB
+  if (e == hipSuccess) {
+    double best = 1e30;
+    for (int r = 0; r < 4 && e == hipSuccess; ++r) {
+      e = hipEventRecord(e0, s);
+      if (e == hipSuccess) e = hipMemcpyAsync(d, hp, kCopy, hipMemcpyHostToDevice, s);
+      if (e == hipSuccess) e = hipEventRecord(e1, s);
+      if (e == hipSuccess) e = hipEventSynchronize(e1);
+      if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+      if (e == hipSuccess && r > 0) best = std::min(best, double(ms) * 1e-3);
+    }
+    if (e == hipSuccess) m.h2d_bytes_per_s = double(kCopy) / best;
+  }
+  if (P) s3h_plan_destroy(P);
+  (void)hipHostFree(hp);
+  (void)hipFree(d);
+  (void)hipFree(dd);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (s) (void)hipStreamDestroy(s);
+  if (R.rc) return R;
+  if (e != hipSuccess) return hip_fail("rate probe", e);
+  // fixed cost of one host-path call: a one-block part, timed on its second call (the first
+  // builds the device's cached host context)
+  static const uint8_t tiny[64] = {};
+  const uint8_t* tp = tiny;
+  const uint64_t tl = sizeof tiny;
+  uint32_t th[8];
+  double best = 1e30;
+  for (int r = 0; r < 3; ++r) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (int rc = s3h_sha256_batch_host(&tp, &tl, 1, th, 1, 0)) {
+      R.rc = rc;
+      R.err = g_err;
+      return R;
+    }
+    if (r > 0) best = std::min(best, seconds_since(t0));
+  }
+  m.call_s = best;
+  return R;
+}
+
+const RouteModel& route_model() {
+  static const RouteModel R = measure_route_model();
+  return R;
+}
+
+// AUTO's decision for a batch (S3H_ROUTE_GPU or S3H_ROUTE_CPU) and both estimates.
+int route_choose(const s3h_route_model_t& m, const uint64_t* lengths, uint64_t n, int ndevices,
+                 double* gpu_s, double* cpu_s) {
+  uint64_t total = 0, longest = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    total += lengths[i];
+    longest = std::max(longest, lengths[i]);
+  }
+  const int devs = std::max(1, int(std::min<uint64_t>(n, uint64_t(ndevices > 0 ? std::min(ndevices, m.devices) : m.devices))));
+  const double g = m.call_s + std::max(double(longest) / m.chain_bytes_per_s,
+                                       double(total) / devs / m.h2d_bytes_per_s);
+  const double threads = double(std::min<uint64_t>(n, uint64_t(std::max(1, m.cpu_threads))));
+  const double c = std::max(double(total) / (threads * m.cpu_bytes_per_s),
+                            double(longest) / m.cpu_bytes_per_s);
+  if (gpu_s) *gpu_s = g;
+  if (cpu_s) *cpu_s = c;
+  return c < g ? S3H_ROUTE_CPU : S3H_ROUTE_GPU;
+}
+
+bool trace_route() {
+  static const bool on = std::getenv("S3H_TRACE_ROUTE") != nullptr;
+  return on;
+}
+
+// The routed entry points: parts (fd < 0) or file ranges (fd >= 0, `path` for the GPU form).
+int routed(const uint8_t* const* parts, const char* path, const uint64_t* offsets,
+           const uint64_t* lengths, uint64_t n, uint32_t* digests, int ndevices, int route,
+           int* taken) {
+  if (taken) *taken = -1;
+  if (!lengths || !digests || n == 0 || (!path && !parts) || (path && !offsets))
+    return fail(S3H_EINVAL, "routed batch: null argument or n == 0");
+  if (route != S3H_ROUTE_GPU && route != S3H_ROUTE_CPU && route != S3H_ROUTE_AUTO)
+    return fail(S3H_EINVAL, "routed batch: unknown route %d", route);
+  int use = route;
+  if (route == S3H_ROUTE_AUTO) {
+    const RouteModel& R = route_model();
+    if (R.rc) return fail(R.rc, "%s", R.err.c_str());
+    double g = 0, c = 0;
+    use = route_choose(R.m, lengths, n, ndevices, &g, &c);
+    if (trace_route())
+      std::fprintf(stderr, "[s3h route] %llu parts: gpu %.4f s, cpu %.4f s (%d threads) -> %s\n",
+                   (unsigned long long)n, g, c, R.m.cpu_threads, use == S3H_ROUTE_CPU ? "cpu" : "gpu");
+  }
+  int rc;
+  if (use == S3H_ROUTE_GPU) {
+    rc = path ? s3h_sha256_file_parts(path, offsets, lengths, n, digests, ndevices, 0)
+              : s3h_sha256_batch_host(parts, lengths, n, digests, ndevices, 0);
+  } else if (path) {
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return fail(S3H_EINVAL, "cpu route: cannot open %s", path);
+    struct stat st {};
+    rc = fstat(fd, &st) == 0 ? S3H_OK : fail(S3H_EINVAL, "cpu route: cannot stat %s", path);
+    for (uint64_t i = 0; rc == S3H_OK && i < n; ++i)
+      if (offsets[i] + lengths[i] > uint64_t(st.st_size))
+        rc = fail(S3H_EINVAL, "cpu route: part %llu ends past the end of %s",
+                  (unsigned long long)i, path);
+    if (rc == S3H_OK) rc = cpu_batch(nullptr, fd, offsets, lengths, n, digests, host_cpus());
+    close(fd);
+  } else {
+    for (uint64_t i = 0; i < n; ++i)
+      if (!parts[i] && lengths[i]) return fail(S3H_EINVAL, "cpu route: part %llu is null", (unsigned long long)i);
+    rc = cpu_batch(parts, -1, nullptr, lengths, n, digests, host_cpus());
+  }
+  if (rc == S3H_OK && taken) *taken = use;
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int s3h_route_model(s3h_route_model_t* m) {
+  if (!m) return fail(S3H_EINVAL, "route model: null argument");
+  const RouteModel& R = route_model();
+  *m = R.m;
+  return R.rc ? fail(R.rc, "%s", R.err.c_str()) : S3H_OK;
+}
+
+int s3h_route_estimate(const s3h_route_model_t* m, const uint64_t* lengths, uint64_t n,
+                       int ndevices, double* gpu_s, double* cpu_s) {
+  if (!m || !lengths || n == 0) return fail(S3H_EINVAL, "route estimate: bad argument");
+  if (!(m->cpu_bytes_per_s > 0 && m->chain_bytes_per_s > 0 && m->h2d_bytes_per_s > 0))
+    return fail(S3H_EINVAL, "route estimate: the model's rates must be positive");
+  return route_choose(*m, lengths, n, ndevices, gpu_s, cpu_s);
+}
+
+int s3h_sha256_batch_routed(const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
+                            uint32_t* digests, int ndevices, int route, int* taken) {
+  return routed(parts, nullptr, nullptr, lengths, n, digests, ndevices, route, taken);
+}
+
+int s3h_sha256_file_parts_routed(const char* path, const uint64_t* offsets,
+                                 const uint64_t* lengths, uint64_t n, uint32_t* digests,
+                                 int ndevices, int route, int* taken) {
+  if (!path) return fail(S3H_EINVAL, "routed file parts: null path");
+  return routed(nullptr, path, offsets, lengths, n, digests, ndevices, route, taken);
+}
+
+}  // extern "C"

@@ -398,6 +398,54 @@ def sha256_md5_file_parts(path: str, offsets, lengths, ndevices: int = 0,
     return sha, m5
 
 
+def route_model() -> dict:
+    """The size-aware routing model's rates, measured once per process on this host and GPU
+    (s3h_route_model): per-thread CPU drop-in rate, one GPU chain's rate, pinned H2D rate,
+    fixed GPU call cost, CPU threads, devices.  Raises S3HashError without a GPU."""
+    m = _native.RouteModel()
+    check(lib().s3h_route_model(ctypes.byref(m)))
+    return {f: getattr(m, f) for f, _ in m._fields_}
+
+
+def route_estimate(lengths, model: dict, ndevices: int = 0) -> tuple[str, float, float]:
+    """AUTO's choice for a batch of parts of ``lengths`` under ``model`` (any dict with
+    route_model()'s fields; pure host arithmetic, s3h_route_estimate): (route, gpu_s, cpu_s)."""
+    m = _native.RouteModel(**model)
+    lens = _u64(lengths)
+    g, c = ctypes.c_double(), ctypes.c_double()
+    r = lib().s3h_route_estimate(ctypes.byref(m), _p64(lens), lens.size, ndevices,
+                                 ctypes.byref(g), ctypes.byref(c))
+    if r < 0:
+        check(r)
+    return _native.ROUTE_NAMES[r], g.value, c.value
+
+
+def sha256_batch_routed(parts: Sequence, ndevices: int = 0, route: str = "auto") -> tuple[np.ndarray, str]:
+    """Host-resident parts hashed on the route given -- "gpu" (= sha256_batch_host), "cpu" (the
+    lib/hash drop-in on host threads) or "auto" (whichever the measured model says finishes
+    first; needs a GPU) -- s3h_sha256_batch_routed.  Returns ((n, 8) uint32, route taken)."""
+    arrs, ptrs, lens = _host_parts(parts)
+    out = np.zeros((len(arrs), DIGEST_WORDS), dtype=np.uint32)
+    taken = ctypes.c_int(-1)
+    check(lib().s3h_sha256_batch_routed(ptrs, _p64(lens), len(arrs), out.ctypes.data, ndevices,
+                                        _native.ROUTE_IDS[route], ctypes.byref(taken)))
+    return out, _native.ROUTE_NAMES[taken.value]
+
+
+def sha256_file_parts_routed(path: str, offsets, lengths, ndevices: int = 0,
+                             route: str = "auto") -> tuple[np.ndarray, str]:
+    """File ranges on the route given (s3h_sha256_file_parts_routed): ((n, 8) uint32, taken)."""
+    offs, lens = _u64(offsets), _u64(lengths)
+    if offs.shape != lens.shape or offs.ndim != 1 or offs.size == 0:
+        raise ValueError("offsets and lengths must be 1-D, equal length and non-empty")
+    out = np.zeros((offs.size, DIGEST_WORDS), dtype=np.uint32)
+    taken = ctypes.c_int(-1)
+    check(lib().s3h_sha256_file_parts_routed(os.fsencode(path), _p64(offs), _p64(lens), offs.size,
+                                             out.ctypes.data, ndevices, _native.ROUTE_IDS[route],
+                                             ctypes.byref(taken)))
+    return out, _native.ROUTE_NAMES[taken.value]
+
+
 def host_threads(ndevices: int = 1) -> tuple[int, int]:
     """(staging threads per device when ``ndevices`` device shards run at once, CPUs this
     process may use: affinity capped by the cgroup quota) -- s3h_host_threads."""

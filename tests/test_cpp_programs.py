@@ -277,6 +277,20 @@ def test_upload_etag_check_gpu(programs, tmp_path, golden, source):
     _etag_round(["--source", source], tmp_path, golden)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("route", ["cpu", "auto"])
+def test_upload_send_routed_gpu(programs, tmp_path, golden, s3_mock, route):
+    """--route: the transfer test's 6 small parts hashed on the chosen route (auto: the
+    measured model sends a batch this small to the CPU drop-in) and PUT to the verifying
+    endpoint; the digests are the lib/hash goldens either way."""
+    url, stats = s3_mock
+    r, t = _upload(["--route", route, "--source", "file"], url, tmp_path, golden)
+    assert r.returncode == 0, r.stderr
+    assert f"route {route} -> cpu" in r.stderr, r.stderr
+    assert [x[4] for x in _parse_parts(r.stdout)] == [p["digest"] for p in t["parts"]]
+    assert stats()["parts"] == 6
+
+
 def test_upload_then_download_verify_cpu(programs, tmp_path, golden):
     """--get-verify: after the upload each job GETs its parts back by byte range (download.cpp
     geometry) from the storing endpoint and every part is checked against the digest it was

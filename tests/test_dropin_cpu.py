@@ -121,3 +121,71 @@ def test_kernel_isa_counts_match_the_built_code_object(tmp_path):
     # the shared-SIMD kernel's consumer is the flag-synchronised skew consumer (the producer
     # beside it runs on the same SIMD and is not in this loop)
     assert abs(k["skews"]["instr_per_block"] - k["skew_nc2"]["instr_per_block"]) < 1.0
+
+
+# ------------------------------------------------------------------ size-aware routing
+_MODEL = dict(cpu_bytes_per_s=1.5e9, chain_bytes_per_s=69e6, h2d_bytes_per_s=50e9, call_s=2e-4,
+              cpu_threads=16, devices=1)
+
+
+def test_route_estimate_crossover():
+    """AUTO's model (s3h_route_estimate): a few 8 MiB parts finish first on 16 SHA-NI threads
+    (one GPU chain needs 8 MiB / 69 MB/s = 0.12 s), 1,024 of them on the GPU (PCIe-bound
+    0.17 s vs 0.36 s on the CPU); one thread per part at most; bad models are rejected."""
+    r, g, c = s3.route_estimate([8 << 20] * 128, _MODEL)
+    assert r == "cpu" and abs(g - (2e-4 + (8 << 20) / 69e6)) < 1e-9 and c < g
+    r, g, c = s3.route_estimate([8 << 20] * 1024, _MODEL)
+    assert r == "gpu" and abs(g - (2e-4 + 1024 * (8 << 20) / 50e9)) < 1e-9 and c > g
+    _, _, c1 = s3.route_estimate([8 << 20] * 2, _MODEL)
+    assert abs(c1 - (8 << 20) / 1.5e9) < 1e-12  # two parts: two threads, not sixteen
+    _, g2, _ = s3.route_estimate([8 << 20] * 1024, {**_MODEL, "devices": 2}, ndevices=0)
+    assert abs(g2 - (2e-4 + max((8 << 20) / 69e6, 512 * (8 << 20) / 50e9))) < 1e-9  # per device
+    with pytest.raises(s3.S3HashError):
+        s3.route_estimate([1], {**_MODEL, "chain_bytes_per_s": 0.0})
+
+
+def test_cpu_route_batch_vs_oracle(oracle):
+    """S3H_ROUTE_CPU: the lib/hash drop-in on host threads, longest part first, bit-exact vs
+    the oracle (empty parts, every tail length)."""
+    rng = np.random.default_rng(77)
+    lens = np.concatenate([[0, 1, 55, 56, 63, 64, 65, 119, 120, (4 << 20) + 1, 9 << 20],
+                           rng.integers(0, 300000, 40)])
+    data = [rng.integers(0, 256, int(L), dtype=np.uint8) for L in lens]
+    got, taken = s3.sha256_batch_routed(data, route="cpu")
+    assert taken == "cpu"
+    assert np.array_equal(got, np.stack([oracle.sha256(d.tobytes()) for d in data]))
+
+
+def test_cpu_route_file_parts_vs_oracle(oracle, tmp_path):
+    """The same for (file, offset, size) ranges: pread in 4 MiB chunks, streamed, the last chunk
+    padded with the part's total length -- ranges straddling chunk edges, empty, misaligned."""
+    rng = np.random.default_rng(78)
+    blob = rng.integers(0, 256, (13 << 20) + 333, dtype=np.uint8)
+    path = tmp_path / "object.bin"
+    blob.tofile(path)
+    ranges = [(0, 0), (0, 4 << 20), (1, (4 << 20) + 1), (3, (8 << 20) - 1), (7, (12 << 20) + 64),
+              (blob.size - 1, 1), (12345, 55), (777, 0), (5, blob.size - 5)]
+    offs = [o for o, _ in ranges]
+    lens = [L for _, L in ranges]
+    got, taken = s3.sha256_file_parts_routed(str(path), offs, lens, route="cpu")
+    assert taken == "cpu"
+    want = np.stack([oracle.sha256(blob[o:o + L].tobytes()) for o, L in ranges])
+    assert np.array_equal(got, want)
+    with pytest.raises(s3.S3HashError):  # a range past the end of the file
+        s3.sha256_file_parts_routed(str(path), [blob.size - 10], [11], route="cpu")
+    with pytest.raises(s3.S3HashError):
+        s3.sha256_file_parts_routed(str(tmp_path / "missing"), [0], [1], route="cpu")
+
+
+def test_route_auto_is_not_a_fallback():
+    """AUTO chooses between the GPU and the CPU drop-in; with no GPU it fails (S3H_ENODEV)
+    instead of running everything on the CPU.  An unknown route is rejected."""
+    with pytest.raises(s3.S3HashError) as e:
+        s3.sha256_batch_routed([b"abc"], route="auto")
+    assert e.value.code == -2
+    with pytest.raises(s3.S3HashError) as e:
+        s3.route_model()
+    assert e.value.code == -2
+    from s3client_amd import _native
+    rc = _native.lib().s3h_sha256_batch_routed(None, None, 0, None, 0, 7, None)
+    assert rc == -1

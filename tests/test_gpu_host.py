@@ -441,3 +441,46 @@ def test_device_queue_soak_mixed_calls(torch_cuda, tmp_path):
     for x in th:
         x.join()
     assert not errors, errors
+
+
+def test_route_auto_by_batch_shape(torch_cuda, oracle, golden, tmp_path):
+    """S3H_ROUTE_AUTO on a real GPU: the measured model is sane; 1,024 x 8 MiB C2 parts (pinned,
+    the bench metric's shape) go to the GPU and 8 x 8 MiB parts (a per-job batch of
+    upload.cpp:89-110) go wherever the model estimates -- on a host with a few SHA-NI cores,
+    the CPU.  Every digest equals the GPU-forced path's and the lib/hash fixtures."""
+    torch = torch_cuda
+    m = s3.route_model()
+    assert 20e6 < m["chain_bytes_per_s"] < 200e6, m   # one skew chain: ~69 MB/s at 2.4 GHz
+    assert m["h2d_bytes_per_s"] > 5e9 and m["cpu_bytes_per_s"] > 50e6, m
+    assert 0 < m["call_s"] < 0.05 and m["cpu_threads"] >= 1 and m["devices"] >= 1, m
+    n, L = 1024, 8 * MIB
+    lens = np.full(n, L, dtype=np.uint64)
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(L)
+    dev = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    s3.generate_parts(dev, offs, lens, np.arange(n), 20241008)
+    host = torch.empty(n * L, dtype=torch.uint8, pin_memory=True)
+    host.copy_(dev)
+    del dev
+    _free(torch)
+    h = host.numpy()
+    views = [h[i * L:(i + 1) * L] for i in range(n)]
+    fx = {e["p"]: e["digest"] for e in golden["c2_parts"]}
+    want_route, g, c = s3.route_estimate([L] * n, m)
+    assert want_route == "gpu", (g, c, m)
+    got, taken = s3.sha256_batch_routed(views, route="auto")
+    assert taken == "gpu"
+    assert all(s3.hash_to_text(got[p]) == d for p, d in fx.items())
+    small = views[:8]
+    want_route, g, c = s3.route_estimate([L] * 8, m)
+    got8, taken = s3.sha256_batch_routed(small, route="auto")
+    assert taken == want_route, (g, c)
+    assert np.array_equal(got8, got[:8])
+    gpu8, taken = s3.sha256_batch_routed(small, route="gpu")
+    assert taken == "gpu" and np.array_equal(gpu8, got[:8])
+    # file ranges: the same eight parts from a file, both routes
+    path = tmp_path / "parts.bin"
+    h[:8 * L].tofile(path)
+    for route in ("auto", "cpu", "gpu"):
+        f8, taken = s3.sha256_file_parts_routed(str(path), offs[:8], lens[:8], route=route)
+        assert np.array_equal(f8, got[:8]), route
+    del host, h, views
