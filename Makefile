@@ -20,7 +20,7 @@ all: $(LIB) oracle cpptests
 # error-word check are read from the gfx950 code object the linked library ships
 # (tools/isa_counts.py -> s3client_amd/kernel_isa_counts.json; disassembly in build/isa).
 ISA_DIS := build/isa/libs3hash_gfx950.dis
-KSRC := $(CSRC)/capi.hip $(CSRC)/route.hpp $(CSRC)/sha256_kernels.hip $(CSRC)/sha256_device.hpp $(CSRC)/sha256_skew_rounds.inc $(CSRC)/sha256_producer_simple.inc $(CSRC)/md5_step_asm.inc include/s3hash.h
+KSRC := $(CSRC)/capi.hip $(CSRC)/route.hpp $(CSRC)/exp_config.hpp $(CSRC)/sha256_kernels.hip $(CSRC)/sha256_device.hpp $(CSRC)/sha256_skew_rounds.inc $(CSRC)/sha256_producer_simple.inc $(CSRC)/md5_step_asm.inc include/s3hash.h
 $(LIBDIR)/capi.o: $(KSRC)
 	@mkdir -p $(LIBDIR) build/isa
 	cd build/isa && $(HIPCC) $(HIPFLAGS) -save-temps -c -o ../../$@ ../../$<
@@ -44,7 +44,7 @@ $(LIB): $(LIBDIR)/capi.o $(LIBDIR)/lib_hash.o $(LIBDIR)/lib_md5.o tools/isa_coun
 STALL := tests/cpp/build/libs3hash_stall.so
 $(STALL): $(KSRC) $(LIBDIR)/lib_hash.o $(LIBDIR)/lib_md5.o
 	@mkdir -p tests/cpp/build
-	$(HIPCC) $(HIPFLAGS) -DS3H_EXP_STALL_PRODUCER=1 -DS3H_EXP_SPIN_LIMIT=4096 -c -o tests/cpp/build/capi_stall.o $(CSRC)/capi.hip
+	$(HIPCC) $(HIPFLAGS) -DS3H_EXPERIMENT_BUILD -DS3H_EXP_STALL_PRODUCER=1 -DS3H_EXP_SPIN_LIMIT=4096 -c -o tests/cpp/build/capi_stall.o $(CSRC)/capi.hip
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ tests/cpp/build/capi_stall.o $(LIBDIR)/lib_hash.o $(LIBDIR)/lib_md5.o -lpthread
 
 oracle: $(LIB)
@@ -76,7 +76,7 @@ stall: $(STALL)
 # -> tools/exp/libs3hash_<TAG>.so, loaded with S3H_LIBRARY=... python bench.py ...
 exp: $(LIBDIR)/lib_hash.o $(LIBDIR)/lib_md5.o
 	@mkdir -p tools/exp
-	$(HIPCC) $(HIPFLAGS) $(EXPFLAGS) -c -o tools/exp/capi_$(TAG).o $(CSRC)/capi.hip
+	$(HIPCC) $(HIPFLAGS) -DS3H_EXPERIMENT_BUILD $(EXPFLAGS) -c -o tools/exp/capi_$(TAG).o $(CSRC)/capi.hip
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o tools/exp/libs3hash_$(TAG).so tools/exp/capi_$(TAG).o $^ -lpthread
 
 clean:

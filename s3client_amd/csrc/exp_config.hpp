@@ -1,0 +1,65 @@
+// exp_config.hpp -- every compile-time experiment switch of the kernels and the host plan, in
+// one place, with the values the PRODUCT build uses.
+//
+// Experiment builds (`make exp TAG=... EXPFLAGS="-DS3H_EXP_..."`, timing studies under
+// tools/exp/, never shipped) and the test-only forced-fault build (`make stall`) define
+// S3H_EXPERIMENT_BUILD and may override anything below.  Without it -- the build of
+// s3client_amd/lib/libs3hash.so -- every value switch must hold its default and no flag switch
+// may be defined: the static_asserts and #errors below stop a product build that was
+// compiled with an experiment's flags, so the shipped kernels are exactly the ones the
+// measurements in DESIGN.md and the code hashes in kernel_isa_counts.json describe.
+#pragma once
+
+// ---- value switches: product defaults
+#ifndef S3H_EXP_SKEW_BLK_PAD
+#define S3H_EXP_SKEW_BLK_PAD 0  // skew layout: uint4 of LDS padding per block (SkewGeom)
+#endif
+#ifndef S3H_EXP_SKEW_BPS_NC2
+#define S3H_EXP_SKEW_BPS_NC2 8  // skew NC=2: blocks per producer step
+#endif
+#ifndef S3H_EXP_PRODUCER_ROLLED
+#define S3H_EXP_PRODUCER_ROLLED 0  // 1: skew producer loops over its items without unrolling
+#endif
+#ifndef S3H_EXP_MD5_SELF_DEPTH
+#define S3H_EXP_MD5_SELF_DEPTH 4  // self-fed MD5: blocks fetched ahead
+#endif
+#ifndef S3H_EXP_MD5_BPS
+#define S3H_EXP_MD5_BPS 4  // MD5 producer/consumer kernel: blocks per producer step
+#endif
+#ifndef S3H_EXP_MD5_ROLL
+#define S3H_EXP_MD5_ROLL 1  // MD5 consumer: the rolling fused step (0: the chunked one)
+#endif
+#ifndef S3H_EXP_MD5_PSETS
+#define S3H_EXP_MD5_PSETS 2  // MD5 producer: raw-block register sets (3: loads two steps ahead)
+#endif
+#ifndef S3H_EXP_SPIN_LIMIT
+#define S3H_EXP_SPIN_LIMIT (1u << 24)  // flag waits: s_sleep 1 polls before a wait times out
+#endif
+#ifndef S3H_EXP_STALL_PRODUCER
+// 1: flag-synchronised producers stop publishing after their first step, so every consumer
+// wait times out (the forced-fault build `make stall`, tests/test_gpu_errors.py)
+#define S3H_EXP_STALL_PRODUCER 0
+#endif
+
+#ifndef S3H_EXPERIMENT_BUILD
+static_assert(S3H_EXP_SKEW_BLK_PAD == 0, "product build: S3H_EXP_SKEW_BLK_PAD must be 0");
+static_assert(S3H_EXP_SKEW_BPS_NC2 == 8, "product build: S3H_EXP_SKEW_BPS_NC2 must be 8");
+static_assert(S3H_EXP_PRODUCER_ROLLED == 0, "product build: unrolled skew producer");
+static_assert(S3H_EXP_MD5_SELF_DEPTH == 4, "product build: self-fed MD5 loads 4 blocks ahead");
+static_assert(S3H_EXP_MD5_BPS == 4, "product build: MD5 kernel with 4-block producer steps");
+static_assert(S3H_EXP_MD5_ROLL == 1, "product build: rolling MD5 row reads");
+static_assert(S3H_EXP_MD5_PSETS == 2, "product build: two MD5 producer register sets");
+static_assert(S3H_EXP_SPIN_LIMIT == (1u << 24), "product build: flag waits give up after 2^24 polls");
+static_assert(S3H_EXP_STALL_PRODUCER == 0, "product build: producers publish every step");
+
+// ---- flag switches: experiments only (each changes a kernel's code or the plan's choices)
+#if defined(S3H_EXP_FORCE_NC) || defined(S3H_EXP_SOLO) || defined(S3H_EXP_GROUP_SKEW) ||      \
+    defined(S3H_EXP_NO_SPLIT) || defined(S3H_EXP_NO_GROUP_NC2) ||                            \
+    defined(S3H_EXP_NO_DUAL_MIXED) || defined(S3H_EXP_PRODUCER_INC) ||                       \
+    defined(S3H_EXP_PROD_ROWS) || defined(S3H_EXP_LONE_CONSUMER) ||                          \
+    defined(S3H_EXP_MD5_INC) || defined(S3H_MD5_VMEM) || defined(S3H_EXP_MD5_NOSYNC) ||      \
+    defined(S3H_EXP_MD5_NOPROD) || defined(S3H_EXP_MD5_NOFUSE) ||                            \
+    defined(S3H_EXP_GROUP_ONLY) || defined(S3H_EXP_NONTEMPORAL_FETCH)
+#error "an experiment switch is defined in a product build (define S3H_EXPERIMENT_BUILD: make exp)"
+#endif
+#endif  // S3H_EXPERIMENT_BUILD

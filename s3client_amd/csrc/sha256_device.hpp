@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "exp_config.hpp"
+
 namespace s3h {
 
 struct Slot {        // one upload part in a plan, slots sorted by block count (descending)

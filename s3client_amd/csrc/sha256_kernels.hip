@@ -1,27 +1,38 @@
-// sha256_kernels.hip -- batched many-message SHA-256 kernels for MI355X (gfx950).
+// sha256_kernels.hip -- batched many-message SHA-256 (and MD5) kernels for MI355X (gfx950).
 //
-// Why one part per LANE (not per workgroup): SHA-256 of one part is a strictly sequential
-// Merkle-Damgard chain (lib/hash/sha256.cpp:88-143: block i needs the state of block i-1),
-// so the only parallelism is across parts.  A wave64 VALU instruction costs the SIMD the
-// same issue slot whether 1 or 64 lanes are active, so each lane carries its own part and
-// the workgroup is the staging / scheduling unit.
+// Why one part per chain of lanes, never per workgroup: SHA-256 of one part is a strictly
+// sequential Merkle-Damgard chain (lib/hash/sha256.cpp:88-143: block i needs the state of
+// block i-1), so the only parallelism is across parts, and BASELINE's batches (C2: 1,024
+// parts, C4: 8,192 per GPU) fill at most 1.6-12.5 % of the chip's 65,536 lanes.  What sets
+// the time is how fast ONE chain runs: a wave issues at most one instruction per ~4 cycles
+// whatever its type (4.05 measured on an aligned lone-wave stream,
+// profiles/r01_ubench_alignment.txt), so every design choice below removes instructions from
+// the chain's wave.
 //
-// Kernels (AUTO picks by part count, capi.hip):
-//   sha256_quad_kernel (<= 4,096 parts) -- each chain on 8 lanes: half-states on lane quads,
-//       one rotation per lane + quad_perm xor_dpp -> 9 VALU per round; NC consumer waves and
-//       one producer wave per workgroup.  Fastest per chain: the C2 metric kernel.
-//   sha256_pair_kernel (<= 32,768) -- each chain on a lane pair, 10 VALU per round, 32 chains
-//       per consumer wave: 3.6x less issue per chain than quad once the SIMDs fill.
-//   sha256_pc_kernel   (<= 65,536) -- one lane per chain, ~14 VALU per round.  In all three
-//       the producer wave streams each lane's 64-byte blocks from HBM, decodes them
-//       (alignment + big-endian in one v_perm per word), synthesises the padding, expands
-//       the message schedule and writes W[t]+K[t] into an LDS double buffer; the consumer
-//       wave runs only the 64-round chain.
-//   sha256_lane_kernel (fused) -- one lane does schedule + rounds; no LDS, 8 waves/SIMD.
-//       Used when parts are plentiful enough to saturate every SIMD (> 65,536 parts).
-//   md5_pc_kernel -- MD5 in the producer/consumer shape.
-// A wave issues ~1 VALU per 4.7-5 cycles whatever the op (profiles/r01_ubench_*), so per-chain
-// speed = 1 / (chain VALU per block): every design choice above removes chain instructions.
+// Kernels and what AUTO (capi.hip resolve_kernel) picks, by part count n on 256 CUs:
+//   sha256_skew_kernel<1>       n <= 2,048   the C2 metric kernel: each chain on 8 lanes (an
+//       e-quad and an a-quad), the a-quad two rounds behind -> 8 VALU per round; one consumer
+//       wave (8 chains) + one producer wave per workgroup.  543.9 instructions per block in
+//       the shipped code object (kernel_isa_counts.json); measured 2,205 cycles per block =
+//       4.06 cycles per instruction = 98.6 % of the issue floor.
+//   sha256_skew_pairs_kernel    n <= 4,096   two flag-synchronised skew groups per
+//       workgroup; the longest parts' groups run solo (capi.hip plan_solo).
+//   sha256_skew_shared_kernel   n <= 32 x CUs (8,192)  "skews": four skew groups per
+//       workgroup, each producer on its consumer's SIMD in simple-class instructions
+//       (sha256_producer_simple.inc) -- the C4 shard kernel.
+//   sha256_skew_kernel<1, PAIR> n <= 28,672  "skewp": the skewed schedule on lane pairs,
+//       9 VALU per round, 32 chains per consumer wave.
+//   sha256_pair_kernel          n <= 32,768  each chain on a lane pair.
+//   sha256_pc_kernel            n <= 65,536  one lane per chain, producer/consumer.
+//   sha256_lane_kernel          above        fused: one lane loads, schedules and compresses.
+//   sha256_quad_kernel<NC>      explicit, and skew ranges of >= 2^31 blocks (64-bit counters).
+//   md5_pc_kernel<4 | 1>        MD5 (Content-MD5 / ETag): 4-block producer steps
+//       while the grid fits one workgroup per CU, 1-block steps (32 KiB LDS) beyond.
+//   sha256_md5_*_kernel         both digests of every part from one grid (capi.hip dual).
+// In the producer/consumer kernels the producer wave streams each part's 64-byte blocks from
+// HBM (cached loads), aligns and byte-swaps them (one v_perm per word), synthesises the
+// padding, expands the message schedule and writes W[t]+K[t] into an LDS double buffer; the
+// consumer wave runs only the 64-round chain.
 //
 // All kernels are resumable: a launch processes blocks [blk_begin, blk_end) of every part,
 // loading/saving the 8-word chaining state in `state` (message order) between launches.  The
@@ -30,37 +41,7 @@
 // (kNoPad | kResume) and a final padded launch with each message's total bit length.
 #include "sha256_device.hpp"
 
-// Compile-time experiment parameters (tools/ builds only: `make exp`; the product build uses
-// these defaults).
-#ifndef S3H_EXP_SKEW_BLK_PAD
-#define S3H_EXP_SKEW_BLK_PAD 0  // skew layout: uint4 of LDS padding per block (SkewGeom)
-#endif
-#ifndef S3H_EXP_SKEW_BPS_NC2
-#define S3H_EXP_SKEW_BPS_NC2 8  // skew NC=2: blocks per producer step
-#endif
-#ifndef S3H_EXP_PRODUCER_ROLLED
-#define S3H_EXP_PRODUCER_ROLLED 0  // 1: skew producer loops over its items without unrolling
-#endif
-#ifndef S3H_EXP_MD5_SELF_DEPTH
-#define S3H_EXP_MD5_SELF_DEPTH 4  // self-fed MD5: blocks fetched ahead
-#endif
-#ifndef S3H_EXP_MD5_BPS
-#define S3H_EXP_MD5_BPS 4  // MD5 producer/consumer kernel: blocks per producer step
-#endif
-#ifndef S3H_EXP_MD5_ROLL
-#define S3H_EXP_MD5_ROLL 1  // MD5 consumer: the rolling fused step (0: the chunked one)
-#endif
-#ifndef S3H_EXP_MD5_PSETS
-#define S3H_EXP_MD5_PSETS 2  // MD5 producer: raw-block register sets (3: loads two steps ahead)
-#endif
-#ifndef S3H_EXP_SPIN_LIMIT
-#define S3H_EXP_SPIN_LIMIT (1u << 24)  // flag waits: s_sleep 1 polls before a wait times out
-#endif
-#ifndef S3H_EXP_STALL_PRODUCER
-// 1: flag-synchronised producers stop publishing after their first step, so every consumer
-// wait times out (the forced-fault build `make stall`, tests/test_gpu_errors.py)
-#define S3H_EXP_STALL_PRODUCER 0
-#endif
+// Experiment switches and their product values: exp_config.hpp (included by sha256_device.hpp).
 #if S3H_EXP_PRODUCER_ROLLED
 #define S3H_PROD_UNROLL _Pragma("unroll 1")
 #else

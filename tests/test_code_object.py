@@ -138,3 +138,21 @@ def test_no_kernel_uses_scratch():
     for sym, m in md.items():
         assert m["private_segment_fixed_size"] == 0, (sym, m)
         assert m["vgpr_spill_count"] == 0, (sym, m)
+
+
+@pytest.mark.parametrize("flags,ok", [([], True), (["-DS3H_EXP_SOLO=3"], False),
+                                      (["-DS3H_EXP_MD5_BPS=2"], False),
+                                      (["-DS3H_EXP_NONTEMPORAL_FETCH"], False),
+                                      (["-DS3H_EXPERIMENT_BUILD", "-DS3H_EXP_SOLO=3",
+                                        "-DS3H_EXP_MD5_BPS=2"], True)])
+def test_product_build_refuses_experiment_switches(tmp_path, flags, ok):
+    """exp_config.hpp: a build without S3H_EXPERIMENT_BUILD (the shipped libs3hash.so) must keep
+    every experiment switch at its product value -- the kernels measured in DESIGN.md and
+    hashed in kernel_isa_counts.json; `make exp` / `make stall` builds opt out explicitly."""
+    import subprocess
+    src = tmp_path / "t.cpp"
+    src.write_text('#include "exp_config.hpp"\nint main() { return S3H_EXP_MD5_BPS; }\n')
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only",
+                        "-I" + os.path.join(ROOT, "s3client_amd", "csrc"), *flags, str(src)],
+                       capture_output=True, text=True)
+    assert (r.returncode == 0) == ok, r.stderr[-1500:]
