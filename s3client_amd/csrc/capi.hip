@@ -1190,11 +1190,18 @@ int stream_update(s3h_stream_s* S, const uint8_t* base, const uint64_t* offsets,
 }
 
 // The error words of the stream's three plans (head / body / final launches), once `s` has
-// run everything before: plan_check.
+// run everything before: plan_check.  Every plan's word is read and cleared (a fault of one
+// must not be reported again by a later check), then the first failure is returned.
 int stream_check(s3h_stream_s* S, hipStream_t s) {
+  int first = S3H_OK;
+  std::string msg;
   for (s3h_plan_s* P : {S->head, S->body, S->fin})
-    if (int rc = plan_check(P, s)) return rc;
-  return S3H_OK;
+    if (int rc = plan_check(P, s); rc && !first) {
+      first = rc;
+      msg = g_err;
+    }
+  if (first) g_err = msg;
+  return first;
 }
 
 int stream_final(s3h_stream_s* S, uint32_t* d_digests, hipStream_t s) {
