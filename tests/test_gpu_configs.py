@@ -55,6 +55,39 @@ def _oracle_whole(torch, oracle, data, offs, lens, md5=False, chunk=8 << 30, thr
     return sha, m5
 
 
+def _hashlib_whole(torch, data, offs, lens, chunk=8 << 30, threads=16):
+    """SHA-256 of EVERY part of the device buffer by Python's hashlib (OpenSSL: an independent
+    implementation, pinned to lib/hash by the golden tests; it releases the GIL, so 16 threads
+    hash in parallel) -- for the multi-shard checks whose volume (512 GiB for BASELINE config 4
+    whole) the scalar oracle would take minutes over.  Same chunked pinned copy-back as
+    _oracle_whole.  -> (n, 8) uint32."""
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
+    n = len(lens)
+    offs = np.asarray(offs, dtype=np.uint64)
+    lens = np.asarray(lens, dtype=np.uint64)
+    ends = offs + lens
+    host = torch.empty(chunk, dtype=torch.uint8, pin_memory=True)
+    out = np.zeros((n, 8), dtype=np.uint32)
+    with ThreadPoolExecutor(threads) as pool:
+        i = 0
+        while i < n:
+            j = i + 1
+            while j < n and int(ends[j]) - int(offs[i]) <= chunk:
+                j += 1
+            a, b = int(offs[i]), int(ends[j - 1])
+            host[:b - a].copy_(data[a:b])
+            mv = memoryview(host.numpy())
+
+            def one(k, a=a, mv=mv):
+                o = int(offs[k]) - a
+                out[k] = np.frombuffer(hashlib.sha256(mv[o:o + int(lens[k])]).digest(), dtype=np.uint32)
+            list(pool.map(one, range(i, j)))
+            i = j
+    del host
+    return out
+
+
 def _release(torch):
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -147,7 +180,7 @@ def test_other_rank_shards(torch_cuda, oracle, golden, cfg, world, rank):
     global part p on rank p % N): BASELINE configs[3]'s rank 7 of 8, the C2 weak-scaling job's
     rank 3 of 4, and two more -- run here on the one GPU, checked against that rank's own
     lib/hash fixtures (gen_golden.py 4c: four slots per rank, plus any other fixture whose id
-    falls in the shard) and the oracle on 64 random parts."""
+    falls in the shard), the oracle on 64 random parts and hashlib on every part."""
     torch = torch_cuda
     from s3client_amd.shard import shard_ids
     per = 8192 if cfg == "c4" else 1024
@@ -178,6 +211,8 @@ def test_other_rank_shards(torch_cuda, oracle, golden, cfg, world, rank):
         rng = np.random.default_rng(1000 * world + rank)
         slots = np.sort(rng.choice(per, 64, replace=False))
         assert np.array_equal(got[slots], _oracle_sample(torch, oracle, data, offs, lens, slots))
+        bad = np.flatnonzero((got != _hashlib_whole(torch, data, offs, lens)).any(axis=1))
+        assert bad.size == 0, f"{bad.size} of {per} digests differ, e.g. slots {bad[:8]}"
     finally:
         del data
         _release(torch)
@@ -188,8 +223,9 @@ def test_every_rank_of_eight_on_one_gpu(torch_cuda, oracle, golden, cfg):
     """BASELINE configs[3] whole: all 65,536 x 8 MiB parts (512 GiB) hashed shard by shard on
     the one GPU, each shard exactly as rank r of an 8-GPU run holds it (global part p on rank
     p % 8, slot p // 8), and the same for the C2 weak-scaling job at N = 8 (8,192 parts).  Every
-    shard checked against its own lib/hash fixtures and the oracle on 16 random parts; the
-    multi-GPU run itself adds only concurrency on separate devices (no data-path exchange)."""
+    shard checked against its own lib/hash fixtures, the oracle on 16 random parts, and EVERY
+    part against hashlib (all 65,536 digests of config 4); the multi-GPU run itself adds only
+    concurrency on separate devices (no data-path exchange)."""
     torch = torch_cuda
     from s3client_amd.shard import shard_ids
     world, per, L = 8, (8192 if cfg == "c4" else 1024), 8 * MIB
@@ -214,8 +250,10 @@ def test_every_rank_of_eight_on_one_gpu(torch_cuda, oracle, golden, cfg):
                 checked += len(mine)
                 rng = np.random.default_rng(700 + rank)
                 slots = np.sort(rng.choice(per, 16, replace=False))
-                got = out.cpu().numpy().view(np.uint32)[slots]
-                assert np.array_equal(got, _oracle_sample(torch, oracle, data, offs, lens, slots)), rank
+                allgot = out.cpu().numpy().view(np.uint32)
+                assert np.array_equal(allgot[slots], _oracle_sample(torch, oracle, data, offs, lens, slots)), rank
+                bad = np.flatnonzero((allgot != _hashlib_whole(torch, data, offs, lens)).any(axis=1))
+                assert bad.size == 0, f"rank {rank}: {bad.size} of {per} digests differ, e.g. {bad[:8]}"
         assert checked >= 4 * world
     finally:
         del data, out
