@@ -156,3 +156,18 @@ def test_product_build_refuses_experiment_switches(tmp_path, flags, ok):
                         "-I" + os.path.join(ROOT, "s3client_amd", "csrc"), *flags, str(src)],
                        capture_output=True, text=True)
     assert (r.returncode == 0) == ok, r.stderr[-1500:]
+
+
+def test_power_sampler_reports_instead_of_failing():
+    """tools/power.py (bench's board-power sample): on a host without that GPU it reports an
+    error in its summary instead of raising, and summarises samples as documented."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from power import PowerSampler
+    with PowerSampler("0000:ff:1f.7", period=0.01) as ps:
+        pass
+    assert "error" in ps.summary()
+    ps = PowerSampler("x")
+    ps.samples = [(0.0, 300.0, 150.0), (0.1, 1300.0, 2300.0), (0.2, 1340.0, 2320.0)]
+    s = ps.summary()
+    assert s["samples"] == 3 and s["max_W"] == 1340.0 and s["busy_mean_W"] == 1320.0
+    assert s["busy_clock_MHz_mean"] == 2310.0
