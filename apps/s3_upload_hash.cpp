@@ -28,9 +28,10 @@
 //                    is forwarded into the signature as DoUploadFilePart does (:81-86).
 //   --per-job        one batch call per job thread at the same time (std::async per job, as
 //                    upload.cpp:136-140 runs UploadParts), instead of one call for all parts.
-//   --route R        gpu (default) | cpu | auto: where the SHA-256 batch call runs
-//                    (s3h_sha256_*_routed: auto = whichever the measured model says finishes
-//                    first -- a few large parts go to the CPU drop-in, hundreds to the GPU).
+//   --route R        gpu (default) | cpu | auto: where the SHA-256 hashing runs.  auto decides
+//                    once for the whole upload with the measured model (sha256::choose_route:
+//                    a few large parts go to the CPU drop-in, hundreds to the GPU); a CPU
+//                    decision hashes per job as --cpu does, overlapped with the PUTs.
 //
 //   s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory] [--per-job]
 //                  [--cpu] [--verify] [--print-headers] [--send] [--get-verify] [--retries N]
@@ -335,6 +336,23 @@ int main(int argc, char** argv) {
     }
     init_s = now() - ti;
   }
+  // --route: ONE decision for the whole upload, made here before the timed passes (the first
+  // decision measures the model, once per process, like the runtime start-up above).  A CPU
+  // decision hashes exactly as --cpu does -- each job thread hashes its own parts with the
+  // drop-in and PUTs them as it goes, so hashing overlaps the uploads -- and a GPU decision as
+  // the default GPU path.
+  double est_gpu = 0, est_cpu = 0;
+  if (!cpu && route != sha256::Route::gpu) {
+    try {
+      route_taken = route == sha256::Route::cpu
+                        ? sha256::Route::cpu
+                        : sha256::choose_route(lens, devices, &est_gpu, &est_cpu);
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "%s\n", e.what());
+      return 1;
+    }
+  }
+  const bool cpu_hash_mode = cpu || route_taken == sha256::Route::cpu;
   // Signed UploadPart headers of part i: its digest in x-amz-content-sha256 instead of
   // UNSIGNED-PAYLOAD (aws_sign.cpp:236-237); the memory path forwards it too, where the
   // reference's DoUploadPart drops it (multipart_upload.cpp:131-136).
@@ -443,9 +461,9 @@ int main(int argc, char** argv) {
       }
       return;
     }
-    const std::vector<std::string> h =
-        source == "file" ? sha256::file_part_hashes(file, o, l, devices, route, &route_taken)
-                         : sha256::payload_hashes(p, l, devices, route, &route_taken);
+    const std::vector<std::string> h = source == "file"
+                                           ? sha256::file_part_hashes(file, o, l, devices)
+                                           : sha256::payload_hashes(p, l, devices);
     for (size_t k = 0; k < idx.size(); ++k) hex[idx[k]] = h[k];
   };
   // One pass over all parts.  Job threads as upload.cpp:136-140 runs them: the CPU drop-in
@@ -454,7 +472,7 @@ int main(int argc, char** argv) {
   // job, each job then PUTting its own parts.
   auto hash_pass = [&]() -> bool {
     try {
-      if (!cpu && !per_job) {
+      if (!cpu_hash_mode && !per_job) {
         std::vector<size_t> all(parts.size());
         for (size_t i = 0; i < all.size(); ++i) all[i] = i;
         gpu(all);
@@ -466,9 +484,9 @@ int main(int argc, char** argv) {
         // RandomIndex(0, cfg.endpoints.size() - 1) per job (upload.cpp:94-95)
         const size_t ep = std::uniform_int_distribution<size_t>(0, endpoints.size() - 1)(rng);
         fut.push_back(std::async(std::launch::async, [&, j, ep] {
-          if (!cpu && per_job) gpu(job_parts[j]);
+          if (!cpu_hash_mode && per_job) gpu(job_parts[j]);
           for (size_t i : job_parts[j]) {
-            if (cpu) cpu_hash(i);
+            if (cpu_hash_mode) cpu_hash(i);
             if (send_parts) put(i, ep);
           }
         }));
@@ -571,7 +589,11 @@ int main(int argc, char** argv) {
                                (per_job ? ", one call per job" : ", one call") +
                                (route == sha256::Route::gpu ? std::string()
                                 : std::string(", route ") + route_name + " -> " +
-                                      (route_taken == sha256::Route::cpu ? "cpu" : "gpu")) + ")";
+                                      (route_taken == sha256::Route::cpu ? "cpu" : "gpu")) +
+                               (route == sha256::Route::automatic
+                                    ? " (model: gpu " + std::to_string(est_gpu) + " s, cpu " +
+                                          std::to_string(est_cpu) + " s)"
+                                    : std::string()) + ")";
   if (send_parts) what = "upload (hash + PUT to " + endpoint + ", " + std::to_string(jobs) + " jobs), " + what;
   std::fprintf(stderr, "%s: %zu parts, %.3f GiB in %.3f s = %.3f GiB/s%s", what.c_str(), parts.size(),
                double(size) / (1 << 30), dt, double(size) / (1 << 30) / dt,

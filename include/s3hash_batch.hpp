@@ -60,6 +60,20 @@ inline std::vector<std::string> to_hex(const std::vector<uint32_t>& d) {
   return out;
 }
 
+// AUTO's decision for a batch of parts of `lengths` without running it (s3h_route_model, measured
+// once per process, + s3h_route_estimate): Route::gpu or Route::cpu, and both estimates.  An
+// uploader that hashes per job decides once for the whole upload with this, then hashes each
+// job's parts on that route.
+inline Route choose_route(const std::vector<uint64_t>& lengths, int ndevices = 0,
+                          double* gpu_s = nullptr, double* cpu_s = nullptr) {
+  if (lengths.empty()) throw std::invalid_argument("choose_route: no parts");
+  s3h_route_model_t m;
+  batch_check(s3h_route_model(&m));
+  const int r = s3h_route_estimate(&m, lengths.data(), lengths.size(), ndevices, gpu_s, cpu_s);
+  if (r < 0) batch_check(r);
+  return Route(r);
+}
+
 // 64-char lowercase hex per part: the `payloadHash` strings S3Api::UploadFilePart takes
 // (lib/include/s3-api.h:447-452).  *taken (if non-null) receives the route that ran.
 inline std::vector<std::string> payload_hashes(const std::vector<const uint8_t*>& parts,

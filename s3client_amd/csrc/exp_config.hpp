@@ -30,7 +30,10 @@
 #define S3H_EXP_MD5_ROLL 1  // MD5 consumer: the rolling fused step (0: the chunked one)
 #endif
 #ifndef S3H_EXP_MD5_PSETS
-#define S3H_EXP_MD5_PSETS 2  // MD5 producer: raw-block register sets (3: loads two steps ahead)
+#define S3H_EXP_MD5_PSETS 2  // MD5 producer, 4-block steps: raw-block register sets (3: two steps ahead)
+#endif
+#ifndef S3H_EXP_MD5_PSETS1
+#define S3H_EXP_MD5_PSETS1 3  // the same for md5_pc_kernel<1> (1-block steps): two blocks ahead
 #endif
 #ifndef S3H_EXP_SPIN_LIMIT
 #define S3H_EXP_SPIN_LIMIT (1u << 24)  // flag waits: s_sleep 1 polls before a wait times out
@@ -49,6 +52,7 @@ static_assert(S3H_EXP_MD5_SELF_DEPTH == 4, "product build: self-fed MD5 loads 4 
 static_assert(S3H_EXP_MD5_BPS == 4, "product build: MD5 kernel with 4-block producer steps");
 static_assert(S3H_EXP_MD5_ROLL == 1, "product build: rolling MD5 row reads");
 static_assert(S3H_EXP_MD5_PSETS == 2, "product build: two MD5 producer register sets");
+static_assert(S3H_EXP_MD5_PSETS1 == 3, "product build: three sets for 1-block MD5 steps");
 static_assert(S3H_EXP_SPIN_LIMIT == (1u << 24), "product build: flag waits give up after 2^24 polls");
 static_assert(S3H_EXP_STALL_PRODUCER == 0, "product build: producers publish every step");
 

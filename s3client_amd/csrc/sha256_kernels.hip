@@ -1650,11 +1650,15 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
     const uint32_t lastv = (slot0 + 64u <= A.n ? slot0 + 64u : A.n) - 1;
     const uint64_t fabs = A.slots[lastv].len >> 6 < A.blk_end ? A.slots[lastv].len >> 6 : A.blk_end;
     const uint64_t full_steps = fabs > b0 ? (fabs - b0) / kBps : 0;
-#if S3H_EXP_MD5_PSETS == 3
-    // Experiment (S3H_EXP_MD5_PSETS=3): three register sets, loads two steps (~4 us of chain
-    // time) ahead of their decode.  Measured no faster (C2 114.2-114.6 vs 114.4-114.7 GiB/s,
-    // C4 shard 811 vs 815; profiles/r03_exp_md5_roll.jsonl): one step of lead already hides
-    // the loads, and the producer's loop (118 instructions per block) has slack.
+    // Register sets of raw blocks in flight: with 4-block steps (md5_pc_kernel<4>) two sets --
+    // loads one step (~2 us of chain time) ahead -- hide the loads: three measured no faster
+    // (C2 114.2-114.6 vs 114.4-114.7 GiB/s, C4 shard 811 vs 815; r03_exp_md5_roll.jsonl).
+    // With 1-block steps (md5_pc_kernel<1>, grids beyond one workgroup per CU) one step of
+    // lead is one block (~0.5 us), less than an HBM miss under load: three sets (two blocks
+    // ahead) ran 20,480 x 256 KiB at 1,615.5 GiB/s against 1,435.0 with two
+    // (profiles/r04_exp_md5_psets.jsonl).
+    constexpr int kSets = kBps == 1 ? S3H_EXP_MD5_PSETS1 : S3H_EXP_MD5_PSETS;
+    if constexpr (kSets == 3) {
     RawBlock rc[kBps];
     S3H_MD5_FETCH(ra, 0)
     S3H_MD5_FETCH(rb, 1)
@@ -1695,7 +1699,7 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
       S3H_MD5_SYNC();
       if (k + 3 > nsteps) break;
     }
-#else
+    } else {
     S3H_MD5_FETCH(ra, 0)
     S3H_MD5_FETCH(rb, 1)
     S3H_MD5_MAKE(ra, 0)
@@ -1723,7 +1727,7 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
       S3H_MD5_SYNC();
       if (k + 2 > nsteps) break;
     }
-#endif
+    }
 #undef S3H_MD5_FETCH
 #undef S3H_MD5_MAKE
 #undef S3H_MD5_MAKE_T
