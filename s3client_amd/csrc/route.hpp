@@ -186,8 +186,19 @@ RouteModel measure_route_model() {
   return R;
 }
 
-const RouteModel& route_model() {
-  static const RouteModel R = measure_route_model();
+// The measured model, kept once it measured successfully; a failed measurement (no device, a
+// transient HIP error) is returned to its caller and tried again on the next call.
+RouteModel route_model() {
+  static std::mutex mu;
+  static bool have = false;
+  static RouteModel cached;
+  std::lock_guard<std::mutex> lk(mu);
+  if (have) return cached;
+  RouteModel R = measure_route_model();
+  if (R.rc == S3H_OK) {
+    cached = R;
+    have = true;
+  }
   return R;
 }
 
