@@ -479,6 +479,9 @@ DualMode dual_mode(const s3h_plan_s* S, const s3h_plan_s* M, uint64_t b0, uint64
 #ifndef S3H_EXP_NO_DUAL_MIXED  // tools/ experiment builds only: round-2/3 behaviour
   if (group_ok && S->dual_solo > 0) return kDualGroupMixed;
 #endif
+#ifdef S3H_EXP_GROUP_ANY  // tools/ experiment builds only: the group kernel at any grid size
+  if (group_ok || S->kernel == S3H_KERNEL_PAIR || S->kernel == S3H_KERNEL_PC) return kDualGroup;
+#endif
   if (group_ok && (S->n + 31) / 32 <= cus) return kDualGroup;
   return kDualNone;
 }
