@@ -613,7 +613,10 @@ def status_all(dist, world: int, check) -> None:
 
 
 def power_sampler(ident: dict):
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    """Board power + GFX clock of this rank's device over a timed region (tools/power.py)."""
+    tools = os.path.join(ROOT, "tools")
+    if tools not in sys.path:
+        sys.path.insert(0, tools)
     from power import PowerSampler
     return PowerSampler(ident["pci_bus_id"])
 
