@@ -1029,6 +1029,13 @@ def c4_shard(args, s3, torch, dist, dev, rank, world, local, ident, ph, steps: i
     return res
 
 
+def shared_buffer_views(h: np.ndarray, per: int, ndev: int, L: int) -> list:
+    """host_resident_multi's parts: global part i = buffer part i // ndev, so the host path's
+    split (part i on device i % ndev) gives every device buffer parts 0..per-1 in order, at the
+    buffer's constant stride L (its 2-D copy form)."""
+    return [h[(i // ndev) * L:(i // ndev + 1) * L] for i in range(per * ndev)]
+
+
 def host_resident_multi(s3, torch, dev, world: int, ph, per: int = 1024, reps: int = 3):
     """Rank 0 of an N-GPU run: the C2 weak-scaling job (1,024 x 8 MiB per GPU) starting and
     ending in HOST memory, through s3h_sha256_batch_host(..., ndevices=N) -- part i on device
@@ -1054,8 +1061,7 @@ def host_resident_multi(s3, torch, dev, world: int, ph, per: int = 1024, reps: i
     host.copy_(buf)
     del buf
     torch.cuda.empty_cache()
-    h = host.numpy()
-    views = [h[(i // ndev) * L:(i // ndev + 1) * L] for i in range(n)]
+    views = shared_buffer_views(host.numpy(), per, ndev, L)
     setup = time.perf_counter() - t_setup
     ph.mark("host_resident setup (8 GiB pinned)")
     out = s3.sha256_batch_host(views, ndevices=ndev)  # warm: a cached context per device
@@ -1070,7 +1076,7 @@ def host_resident_multi(s3, torch, dev, world: int, ph, per: int = 1024, reps: i
     same = bool((out.reshape(per, ndev, 8) == out.reshape(per, ndev, 8)[:, :1]).all())
     threads, cpus = s3.host_threads(ndev)
     gib = n * L / 2**30
-    del host, h, views
+    del host, views
     s3.trim()
     return {"metric": f"host-resident (H2D-inclusive) SHA-256 GiB/s over {ndev} GPU(s)",
             "value": round(gib / float(np.mean(times)), 3), "best": round(gib / min(times), 3),

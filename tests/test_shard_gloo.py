@@ -241,3 +241,19 @@ def test_bench_status_fault_on_one_rank_fails_every_rank():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got[0] == got[1] == "rank 1: RuntimeError: s3hash error -3: synchronisation timeout"
+
+
+def test_host_resident_multi_views_give_every_device_the_whole_buffer():
+    """bench.host_resident_multi over N devices reads ONE bounded pinned buffer: with the host
+    path's split (part i on device i % N) device k gets buffer parts 0..per-1 in order, at a
+    constant stride (the 2-D copy form), whatever N."""
+    import bench
+    per, L = 16, 64
+    h = np.arange(per * L, dtype=np.uint8)
+    for ndev in (1, 2, 3, 8):
+        views = bench.shared_buffer_views(h, per, ndev, L)
+        assert len(views) == per * ndev
+        for k in range(ndev):
+            mine = views[k::ndev]
+            assert [v.ctypes.data - h.ctypes.data for v in mine] == [j * L for j in range(per)]
+            assert all(v.size == L for v in mine)
