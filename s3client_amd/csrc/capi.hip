@@ -1732,6 +1732,13 @@ int s3h_sha256_md5_batch_device(int device, const void* d_base, const uint64_t* 
     HIP_TRY(hipStreamSynchronize(main_s));
     return plan_check(P[0], main_s);  // the one grid reports into S's word
   }
+#ifdef S3H_EXP_DUAL_SERIAL  // tools/ experiment builds only: both kernels one after the other
+  if (int rc = plan_launch(P[0], d_base, d_sha256, 0, P[0]->max_blocks, 0, main_s, false)) return rc;
+  if (int rc = plan_launch(P[1], d_base, d_md5, 0, P[1]->max_blocks, 0, main_s, false)) return rc;
+  HIP_TRY(hipStreamSynchronize(main_s));
+  if (int rc = plan_check(P[0], main_s)) return rc;
+  return plan_check(P[1], main_s);
+#endif
   // Otherwise MD5 runs on a side stream forked from and joined back into the caller's: the two
   // kernels occupy different CUs, so both digests take about the SHA-256 time.
   HIP_TRY(hipStreamCreateWithFlags(&C.side, hipStreamNonBlocking));
