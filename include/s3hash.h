@@ -192,7 +192,8 @@ int s3h_sha256_file_parts(const char *path, const uint64_t *offsets, const uint6
  * md5::md5 call per part (lib/hash/sha256.cpp:147-160, lib/hash/md5.cpp:71-180).
  * Both forms launch ONE grid whose workgroups run either the SHA-256 or the MD5 chain
  * (sha256_md5_dual_kernel) while it fits one workgroup per CU, so both digests take the
- * SHA-256 time; larger batches run the two kernels on two streams.  Host form: each slice
+ * SHA-256 time; larger batches (> 32 x CUs parts, where each kernel fills the chip) run the
+ * two kernels one after the other.  Host form: each slice
  * crosses PCIe ONCE for both digests (the host path is PCIe-bound).  Blocking.
  * sha256_digests: n x 8 words (lib/hash layout); md5_digests: n x 4 words (memory order). */
 int s3h_sha256_md5_batch_host(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,

@@ -439,7 +439,8 @@ int plan_launch(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint64_t
 
 // SHA-256 (plan S) and MD5 (plan M, same parts) in ONE grid (sha256_md5_dual_kernel) when S
 // runs a 128-thread skew body; returns S3H_EINVAL without launching otherwise (the caller
-// then launches the two plans on two streams).
+// then launches the two plans itself: one after the other on the device-resident path, on the
+// two hash streams of a slice on the host path).
 // The fused grid must fit one workgroup per CU: beyond that its MD5 workgroups (the grid's
 // tail) would only start as SHA-256 ones retire, i.e. run after them.
 
@@ -447,7 +448,7 @@ int plan_launch(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint64_t
 // the same order): kDualSplit = sha256_md5_dual_kernel (skew with one consumer per workgroup:
 // S's workgroups then M's, all within one workgroup per CU); kDualGroup =
 // sha256_md5_group_kernel (skewp: each workgroup runs a SHA-256 group and a self-fed MD5 wave
-// over the same 32 parts, S->grid <= one per CU); kDualNone = two launches on two streams.
+// over the same 32 parts, S->grid <= one per CU); kDualNone = two separate launches.
 // kDualGroupMixed = sha256_md5_group_mixed_kernel (ragged 2,049-8,192 parts: the longest
 // parts in skew groups, the rest as kDualGroup; S->dual_solo skew workgroups).
 enum DualMode { kDualNone = 0, kDualSplit = 1, kDualGroup = 2, kDualGroupSkew = 3, kDualGroupMixed = 4 };
@@ -1710,13 +1711,7 @@ int s3h_sha256_md5_batch_device(int device, const void* d_base, const uint64_t* 
   s3h_plan_s* P[2] = {};
   struct Cleanup {
     s3h_plan_s** P;
-    hipStream_t side = nullptr;
-    hipEvent_t ev[2] = {};
     ~Cleanup() {
-      if (side) (void)hipStreamSynchronize(side);
-      for (hipEvent_t e : ev)
-        if (e) (void)hipEventDestroy(e);
-      if (side) (void)hipStreamDestroy(side);
       s3h_plan_destroy(P[0]);
       s3h_plan_destroy(P[1]);
     }
@@ -1732,24 +1727,14 @@ int s3h_sha256_md5_batch_device(int device, const void* d_base, const uint64_t* 
     HIP_TRY(hipStreamSynchronize(main_s));
     return plan_check(P[0], main_s);  // the one grid reports into S's word
   }
-#ifdef S3H_EXP_DUAL_SERIAL  // tools/ experiment builds only: both kernels one after the other
+  // Otherwise (more parts than the one-grid forms hold: > 32 x CUs) both kernels fill the chip
+  // on their own, and run one after the other on the caller's stream.  Round 1-3 ran MD5 on a
+  // side stream beside SHA-256; measured on one box (256 KiB parts, both digests, GiB/s):
+  // 9,000 parts 294 two streams -> 315 in order, 12,288 397 -> 420, 16,384 515 -> 543,
+  // 32,768 523 -> 609, 65,536 692 -> 796 (profiles/r04_exp_dual_serial.jsonl): concurrent
+  // grids only contend for the same SIMDs.
   if (int rc = plan_launch(P[0], d_base, d_sha256, 0, P[0]->max_blocks, 0, main_s, false)) return rc;
   if (int rc = plan_launch(P[1], d_base, d_md5, 0, P[1]->max_blocks, 0, main_s, false)) return rc;
-  HIP_TRY(hipStreamSynchronize(main_s));
-  if (int rc = plan_check(P[0], main_s)) return rc;
-  return plan_check(P[1], main_s);
-#endif
-  // Otherwise MD5 runs on a side stream forked from and joined back into the caller's: the two
-  // kernels occupy different CUs, so both digests take about the SHA-256 time.
-  HIP_TRY(hipStreamCreateWithFlags(&C.side, hipStreamNonBlocking));
-  HIP_TRY(hipEventCreateWithFlags(&C.ev[0], hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&C.ev[1], hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(C.ev[0], main_s));
-  HIP_TRY(hipStreamWaitEvent(C.side, C.ev[0], 0));
-  if (int rc = plan_launch(P[1], d_base, d_md5, 0, P[1]->max_blocks, 0, C.side, false)) return rc;
-  if (int rc = plan_launch(P[0], d_base, d_sha256, 0, P[0]->max_blocks, 0, main_s, false)) return rc;
-  HIP_TRY(hipEventRecord(C.ev[1], C.side));
-  HIP_TRY(hipStreamWaitEvent(main_s, C.ev[1], 0));
   HIP_TRY(hipStreamSynchronize(main_s));
   if (int rc = plan_check(P[0], main_s)) return rc;
   return plan_check(P[1], main_s);

@@ -433,10 +433,12 @@ def test_dual_digest_device_c2_subset(torch_cuda, oracle, golden):
 def test_dual_digest_device_fallback_and_fused_ragged(torch_cuda, oracle):
     """Ragged batches on the dual-digest routes: 300 parts (split grid: skew workgroups then MD5
     workgroups), 2,000 parts (the split grid would not fit one workgroup per CU: skew groups
-    each with a self-fed MD5 wave) and 2,500 parts (two-group skew range: the group kernel's
-    skewp geometry), each vs the oracle."""
+    each with a self-fed MD5 wave), 2,500 parts (two-group skew range: the group kernel's
+    skewp geometry), and 9,000 / 33,000 parts (beyond every one-grid form: the SHA-256 and MD5
+    kernels one after the other on the caller's stream -- skewp / pc with md5_pc_kernel<1>),
+    each vs the oracle."""
     rng = np.random.default_rng(33)
-    for n in (300, 2000, 2500):
+    for n in (300, 2000, 2500, 9000, 33000):
         rl = rng.integers(0, 9000, n)
         ro = np.cumsum(rng.integers(0, 70, n) + np.concatenate([[0], rl[:-1]]))
         host = rng.integers(0, 256, int(ro[-1] + rl[-1]) + 8, dtype=np.uint8)
