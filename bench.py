@@ -347,6 +347,10 @@ def main():
     # has no collective at all, so RCCL would buy nothing, and the one-GPU rehearsal then runs
     # exactly the code of a real N-GPU run.
     share = os.environ.get("S3H_BENCH_SHARE_GPU") == "1"
+    if not share and local >= torch.cuda.device_count():
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {torch.cuda.device_count()} "
+                         "visible GPU(s): one process per GPU (S3H_BENCH_SHARE_GPU=1 to rehearse "
+                         "several ranks on one GPU)")
     gpu = local % torch.cuda.device_count() if share else local
     torch.cuda.set_device(gpu)
     if world > 1:
