@@ -963,7 +963,19 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
   int rc = S3H_OK;
   uint64_t k = 0;
   const double t_setup = wall_s();
-  for (uint64_t b0 = 0; b0 < max_blocks && rc == S3H_OK; b0 += bps, ++k) {
+  // Slices of bps blocks, except that the last ones halve down to bps/16: the copies set the
+  // pace (PCIe) and each slice's hash overlaps the next slice's copy, so only the LAST slice's
+  // hash is exposed -- ~3.8 ms of a 256 KiB slice of 1,024 parts, 2.4 % of a C2 call.
+  auto slice_blocks = [&](uint64_t b0) -> uint64_t {
+    const uint64_t left = max_blocks - b0;
+#ifndef S3H_EXP_NO_TAIL_RAMP  // tools/ experiment builds only: round-3 fixed slices
+    if (bps >= 256 && left < 2 * bps && left > bps / 16) return (left + 1) / 2;
+#endif
+    return std::min(left, bps);
+  };
+  for (uint64_t b0 = 0, step = 0; b0 < max_blocks && rc == S3H_OK; b0 += step, ++k) {
+    step = slice_blocks(b0);
+    const uint64_t sbytes = step * 64;  // bytes of each part this slice carries (<= slice)
     const int r = int(k % kHostRing);
     uint8_t* slot_base = C.ring + uint64_t(r) * slot_bytes;
     hipError_t e = hipSuccess;
@@ -979,15 +991,17 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
       std::atomic<bool> bad{false};
       pool->run(n, [&](uint64_t j) {
         const uint64_t len = lens[j];
-        if (byte0 < len && !src.fill(sh.parts[j], byte0, std::min(slice, len - byte0), hslot + j * slice))
+        if (byte0 < len && !src.fill(sh.parts[j], byte0, std::min(sbytes, len - byte0), hslot + j * slice))
           bad.store(true, std::memory_order_relaxed);
       });
       if (bad.load()) { rc = fail(S3H_EINVAL, "reading a part failed (file shorter than a part?)"); break; }
-      e = hipMemcpyAsync(slot_base, hslot, slot_bytes, hipMemcpyHostToDevice, C.copy_s);
+      e = step == bps ? hipMemcpyAsync(slot_base, hslot, slot_bytes, hipMemcpyHostToDevice, C.copy_s)
+                      : hipMemcpy2DAsync(slot_base, slice, hslot, slice, sbytes, n,
+                                         hipMemcpyHostToDevice, C.copy_s);
       if (e != hipSuccess) rc = fail(S3H_EHIP, "H2D staged: %s", hipGetErrorString(e));
     } else if (uniform) {
       if (byte0 < lens[0]) {
-        const uint64_t cnt = std::min(slice, lens[0] - byte0);
+        const uint64_t cnt = std::min(sbytes, lens[0] - byte0);
         e = hipMemcpy2DAsync(slot_base, slice, parts[sh.parts[0]] + byte0, stride, cnt, n,
                              hipMemcpyHostToDevice, C.copy_s);
         if (e != hipSuccess) rc = fail(S3H_EHIP, "H2D 2D: %s", hipGetErrorString(e));
@@ -996,7 +1010,7 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
       for (uint64_t j = 0; j < n && rc == S3H_OK; ++j) {
         const uint64_t len = lens[j];
         if (byte0 >= len) continue;
-        const uint64_t cnt = std::min(slice, len - byte0);
+        const uint64_t cnt = std::min(sbytes, len - byte0);
         e = hipMemcpyAsync(slot_base + j * slice, parts[sh.parts[j]] + byte0, cnt,
                            hipMemcpyHostToDevice, C.copy_s);
         if (e != hipSuccess) rc = fail(S3H_EHIP, "H2D: %s", hipGetErrorString(e));
@@ -1007,7 +1021,7 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
     if (fused) {  // both digests from one grid on one stream
       if (e == hipSuccess) e = hipStreamWaitEvent(C.hash_s[0], C.copied[r], 0);
       if (e != hipSuccess) { rc = fail(S3H_EHIP, "event: %s", hipGetErrorString(e)); break; }
-      rc = dual_launch(P0, P1, slot_base, C.d_dig[0], C.d_dig[1], b0, b0 + bps, b0, true,
+      rc = dual_launch(P0, P1, slot_base, C.d_dig[0], C.d_dig[1], b0, b0 + step, b0, true,
                        C.hash_s[0]);
       if (rc == S3H_OK) e = hipEventRecord(C.hashed[r][0], C.hash_s[0]);
       if (e == hipSuccess) e = hipEventRecord(C.hashed[r][1], C.hash_s[0]);
@@ -1016,7 +1030,7 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
       if (e == hipSuccess) e = hipStreamWaitEvent(C.hash_s[a], C.copied[r], 0);
       if (e != hipSuccess) { rc = fail(S3H_EHIP, "event: %s", hipGetErrorString(e)); break; }
       if (b0 < C.plan[a]->max_blocks)  // both pad 9 B, so equal block counts; guard anyway
-        rc = plan_launch(C.plan[a], slot_base, C.d_dig[a], b0, b0 + bps, b0, C.hash_s[a], true);
+        rc = plan_launch(C.plan[a], slot_base, C.d_dig[a], b0, b0 + step, b0, C.hash_s[a], true);
       if (rc == S3H_OK) e = hipEventRecord(C.hashed[r][a], C.hash_s[a]);
     }
     if (rc == S3H_OK && e != hipSuccess) rc = fail(S3H_EHIP, "event: %s", hipGetErrorString(e));
