@@ -38,7 +38,9 @@ def test_context_grows_keeps_small_ring_and_trims(torch_cuda, oracle):
     assert np.array_equal(s3.sha256_batch_host(larger),
                           np.stack([oracle.sha256(p.tobytes()) for p in larger]))
     kept = free0 - _free(torch)
-    assert 0 <= kept < 256 * MIB, kept           # small ring + plans stay cached
+    # small ring + plans stay cached (a few MiB below zero: allocations of earlier tests in this
+    # process that the runtime released meanwhile)
+    assert -64 * MIB <= kept < 256 * MIB, kept
     # pinned, non-uniform parts -> 2 MiB slices: ring = 3 x 200 x 2 MiB = 1.2 GiB > 1 GiB
     pinned = torch.empty(200 * (2 * MIB + 64), dtype=torch.uint8, pin_memory=True)
     h = pinned.numpy()
