@@ -238,8 +238,28 @@ int main(int argc, char** argv) {
         const auto fh = file_job.get();
         for (int i = 0; i < 6; ++i) cok &= fh[i] == want[i];
       }
-      std::remove(path.c_str());
       report("gpu concurrent jobs", cok);
+
+      // Size-aware routing through the C++ layer: one decision for the upload
+      // (choose_route), then each route explicitly, memory parts and file ranges alike --
+      // every route returns the reference's digests.
+      bool rok = true;
+      double g = 0, c = 0;
+      const sha256::Route pick = sha256::choose_route(lens, 0, &g, &c);
+      rok &= g > 0 && c > 0 && (pick == sha256::Route::cpu) == (c < g);
+      std::vector<const uint8_t*> parts;
+      for (uint64_t o : offs) parts.push_back(obj.data() + o);
+      for (sha256::Route r : {sha256::Route::gpu, sha256::Route::cpu, sha256::Route::automatic}) {
+        sha256::Route t1 = sha256::Route::automatic, t2 = sha256::Route::automatic;
+        const auto hm = sha256::payload_hashes(parts, lens, 0, r, &t1);
+        const auto hf = sha256::file_part_hashes(path, offs, lens, 0, r, &t2);
+        for (int i = 0; i < 6; ++i) rok &= hm[i] == want[i] && hf[i] == want[i];
+        rok &= t1 != sha256::Route::automatic && t2 != sha256::Route::automatic;
+        if (r == sha256::Route::automatic) rok &= t1 == pick && t2 == pick;
+        else rok &= t1 == r && t2 == r;
+      }
+      report("gpu routed payload_hashes", rok);
+      std::remove(path.c_str());
     }
     sha256::trim();
   }

@@ -40,6 +40,7 @@ def test_dropin_gpu_batch(programs):
     got = {r[1]: r[2] for r in rows}
     assert got["gpu batch payload_hashes"] == "1" and got["gpu stream_batch"] == "1", rows
     assert got["gpu sha256_md5_batch"] == "1" and got["gpu concurrent jobs"] == "1", rows
+    assert got["gpu routed payload_hashes"] == "1", rows
 
 
 def _xfer_file(tmp_path, golden):
