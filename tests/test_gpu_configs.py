@@ -169,6 +169,15 @@ def test_c4_rank0_shard(torch_cuda, oracle, golden):
         want, _ = _oracle_whole(torch, oracle, data, offs, lens)
         bad = np.flatnonzero((got != want).any(axis=1))
         assert bad.size == 0, f"{bad.size} of {per} C4-shard digests differ, e.g. slots {bad[:8]}"
+        # download verification at this size: the shard against its own
+        # digests, then with one byte flipped in one part -- exactly that part mismatches
+        n_bad, mask = s3.verify_batch_device(data, offs, lens, out)
+        assert n_bad == 0 and not bool(mask.any())
+        k = 5555
+        pos = int(offs[k]) + L // 2 + 3
+        data[pos] ^= 0x40
+        n_bad, mask = s3.verify_batch_device(data, offs, lens, out)
+        assert n_bad == 1 and np.flatnonzero(mask.cpu().numpy()).tolist() == [k]
     finally:
         del data
         _release(torch)
