@@ -115,19 +115,3 @@ void md5_file(const char *fname, uint32_t hash[4]) {
 extern "C" void s3h_cpu_md5(const uint8_t *data, uint64_t length, uint32_t hash[4]) {
   md5::md5(data, size_t(length), hash);
 }
-
-// S3 multipart ETag (what CompleteMultipartUpload returns, multipart_upload.cpp:162-183):
-// hex(MD5(binary part MD5s concatenated in part order)) + "-" + part count.  The outer MD5
-// covers 16 B per part, so it stays on the CPU drop-in.
-extern "C" int s3h_multipart_etag(const uint32_t *md5_digests, uint64_t n, char *out,
-                                  uint64_t out_len) {
-  if (!out || out_len < 56 || (n && !md5_digests) || n == 0) {
-    if (out && out_len) out[0] = '\0';
-    return -1;  // S3H_EINVAL
-  }
-  uint32_t h[4];
-  md5::md5(reinterpret_cast<const uint8_t *>(md5_digests), size_t(16 * n), h);
-  md5::hash_to_text(h, out);
-  std::snprintf(out + 32, size_t(out_len - 32), "-%llu", static_cast<unsigned long long>(n));
-  return 0;
-}

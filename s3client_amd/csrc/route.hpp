@@ -1,4 +1,5 @@
-// route.hpp -- size-aware routing of host-resident batches (included at the end of capi.hip).
+// route.hpp -- size-aware routing of host-resident batches, and the multipart-ETag helper
+// (host-side C-ABI entry points that need no kernel; included at the end of capi.hip).
 //
 // One part's SHA-256 is one sequential chain: on the GPU it runs at ~69 MB/s (the skew
 // kernel's per-wave issue bound), on one EPYC core with SHA-NI at ~1.5 GB/s.
@@ -15,6 +16,7 @@
 // fallback for a missing device.  S3H_ROUTE_GPU (the default everywhere, and the only route
 // the bench metric uses) is s3h_sha256_batch_host / s3h_sha256_file_parts unchanged.
 
+#include "../../include/md5.h"
 #include "../../include/sha256.h"
 
 namespace {
@@ -291,6 +293,20 @@ int s3h_route_estimate(const s3h_route_model_t* m, const uint64_t* lengths, uint
 int s3h_sha256_batch_routed(const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
                             uint32_t* digests, int ndevices, int route, int* taken) {
   return routed(parts, nullptr, nullptr, lengths, n, digests, ndevices, route, taken);
+}
+
+// S3 multipart ETag (what CompleteMultipartUpload returns, multipart_upload.cpp:162-183):
+// hex(MD5(binary part MD5s concatenated in part order)) + "-" + part count.  The outer MD5
+// covers 16 B per part, so it runs on the lib/hash MD5 drop-in.
+int s3h_multipart_etag(const uint32_t* md5_digests, uint64_t n, char* out, uint64_t out_len) {
+  if (out && out_len) out[0] = '\0';
+  if (!out || out_len < S3H_ETAG_MAX) return fail(S3H_EINVAL, "multipart etag: need %d output bytes", S3H_ETAG_MAX);
+  if (n == 0 || !md5_digests) return fail(S3H_EINVAL, "multipart etag: no part digests");
+  uint32_t h[4];
+  md5::md5(reinterpret_cast<const uint8_t*>(md5_digests), size_t(16 * n), h);
+  md5::hash_to_text(h, out);
+  std::snprintf(out + 32, size_t(out_len - 32), "-%llu", static_cast<unsigned long long>(n));
+  return S3H_OK;
 }
 
 int s3h_sha256_file_parts_routed(const char* path, const uint64_t* offsets,
