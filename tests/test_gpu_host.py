@@ -486,3 +486,32 @@ def test_route_auto_by_batch_shape(torch_cuda, oracle, golden, tmp_path):
         f8, taken = s3.sha256_file_parts_routed(str(path), offs[:8], lens[:8], route=route)
         assert np.array_equal(f8, got[:8]), route
     del host, h, views
+
+
+def test_dual_digest_host_beyond_one_grid(torch_cuda, oracle):
+    """SHA-256 + MD5 from host memory for more parts than any one-grid dual form holds (9,000
+    ragged pageable parts: the two plans per slice on the two hash streams) and, in another
+    call, pinned parts of one length at a constant stride (2-D copies, tail-ramp slices): every
+    digest of both algorithms vs the oracle."""
+    torch = torch_cuda
+    rng = np.random.default_rng(9000)
+    n = 9000
+    lens = rng.integers(0, 40000, n)
+    lens[:4] = [0, 1, 55, 64]
+    base = rng.integers(0, 256, int(lens.sum()) + 64, dtype=np.uint8)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    views = [base[int(o):int(o) + int(L)] for o, L in zip(offs, lens)]
+    sha, m5 = s3.sha256_md5_batch_host(views)
+    assert np.array_equal(sha, oracle.batch(base, offs, lens, threads=16))
+    assert np.array_equal(m5, oracle.md5_batch(base, offs, lens, threads=16))
+    L, stride = 300_000, 300_032
+    pinned = torch.empty(n * stride, dtype=torch.uint8, pin_memory=True)
+    h = pinned.numpy()
+    h[:] = rng.integers(0, 256, h.size, dtype=np.uint8)
+    po = np.arange(n) * stride
+    pv = [h[int(o):int(o) + L] for o in po]
+    sha, m5 = s3.sha256_md5_batch_host(pv)
+    pl = np.full(n, L)
+    assert np.array_equal(sha, oracle.batch(h, po, pl, threads=16))
+    assert np.array_equal(m5, oracle.md5_batch(h, po, pl, threads=16))
+    del pinned, h, pv
