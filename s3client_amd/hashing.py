@@ -205,8 +205,9 @@ def sha256_md5_batch_host(parts: Sequence, ndevices: int = 0,
 
 
 def sha256_md5_batch_device(data, offsets, lengths, device: int | None = None, stream=None):
-    """SHA-256 (n, 8) and MD5 (n, 4) int32 device tensors of device-resident parts; the MD5
-    kernel runs concurrently on a side stream (s3h_sha256_md5_batch_device)."""
+    """SHA-256 (n, 8) and MD5 (n, 4) int32 device tensors of device-resident parts
+    (s3h_sha256_md5_batch_device): one grid running both chains while the batch fits one
+    workgroup per CU, above that the two kernels one after the other on ``stream``."""
     import torch
     dev = data.device.index if device is None else device
     offs, lens = _u64(offsets), _u64(lengths)
