@@ -963,13 +963,19 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
   int rc = S3H_OK;
   uint64_t k = 0;
   const double t_setup = wall_s();
-  // Slices of bps blocks, except that the last ones halve down to bps/16: the copies set the
-  // pace (PCIe) and each slice's hash overlaps the next slice's copy, so only the LAST slice's
-  // hash is exposed -- ~3.8 ms of a 256 KiB slice of 1,024 parts, 2.4 % of a C2 call.
+  // Slices of bps blocks, then a geometric tail: the copies set the pace (PCIe; C2: a full
+  // slice copies in ~4.7 ms and hashes in ~3.8) and slice k's hash runs beside slice k+1's
+  // copy, so the hash keeps up only while hash(k) <= copy(k+1).  Once fewer than D slices are
+  // left each slice takes 1/D of the rest (sizes shrink by (D-1)/D >= the hash/copy ratio,
+  // ~0.81), down to bps/16, so the hash exposed after the last copy is one small slice's
+  // (~0.24 ms).  Halving (D = 2) broke the condition at the first tail slice: 3.8 ms of
+  // full-slice hash ran past the copies (tools/host_timeline.py trace).
   auto slice_blocks = [&](uint64_t b0) -> uint64_t {
     const uint64_t left = max_blocks - b0;
 #ifndef S3H_EXP_NO_TAIL_RAMP  // tools/ experiment builds only: round-3 fixed slices
-    if (bps >= 256 && left < 2 * bps && left > bps / 16) return (left + 1) / 2;
+    constexpr uint64_t D = S3H_EXP_TAIL_RAMP_DIV;
+    if (bps >= 256 && left < D * bps)
+      return std::min(left, std::max<uint64_t>(bps / 16, (left + D - 1) / D));
 #endif
     return std::min(left, bps);
   };

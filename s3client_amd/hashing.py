@@ -175,12 +175,29 @@ def md5_batch_device(data, offsets, lengths, device: int | None = None, stream=N
     return sha256_batch_device(data, offsets, lengths, device, "auto", stream, algo="md5")
 
 
+def _as_bytes(p) -> np.ndarray:
+    if type(p) is np.ndarray and p.dtype == np.uint8 and p.ndim == 1 and p.flags.c_contiguous:
+        return p
+    if isinstance(p, (bytes, bytearray, memoryview)):
+        return np.frombuffer(p, dtype=np.uint8)
+    return np.ascontiguousarray(p, dtype=np.uint8).reshape(-1)
+
+
+def _addr(a: np.ndarray) -> int:
+    # c_char.from_buffer is ~3x cheaper than a.ctypes.data / __array_interface__ (which build
+    # objects per part: ~2 ms of a 1,024-part call); it needs a writable, non-empty buffer
+    if not a.size:
+        return 0
+    if a.flags.writeable:
+        return ctypes.addressof(ctypes.c_char.from_buffer(a))
+    return a.__array_interface__["data"][0]
+
+
 def _host_parts(parts):
-    arrs = [np.frombuffer(p, dtype=np.uint8) if isinstance(p, (bytes, bytearray, memoryview))
-            else np.ascontiguousarray(p, dtype=np.uint8).reshape(-1) for p in parts]
+    arrs = [_as_bytes(p) for p in parts]
     n = len(arrs)
-    ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data if a.size else 0 for a in arrs])
-    return arrs, ptrs, _u64([a.size for a in arrs])
+    ptrs = (ctypes.c_void_p * n)(*[_addr(a) for a in arrs])
+    return arrs, ptrs, np.fromiter((a.size for a in arrs), dtype=np.uint64, count=n)
 
 
 def _host_batch(fn, words, parts, ndevices, slice_bytes):

@@ -17,6 +17,7 @@
 #   selfn:N[:ARGS]       `python bench.py --gpus N ARGS` with NO launcher (bench.py starts the N
 #                        ranks itself) on the one GPU, S3H_BENCH_SHARE_GPU=1          (600 s)
 #   py:SCRIPT[:ARGS]     python SCRIPT ARGS                                  (600 s)
+#   trace:SCRIPT         rocprofv3 --kernel-trace --memory-copy-trace of python3 SCRIPT (300 s)
 #   exe:PROGRAM ARGS     a built tool, e.g. tools/ubench_dep                  (300 s)
 set -o pipefail
 TAG=${1:?usage: run.sh TAG STEP...}; shift
@@ -60,6 +61,9 @@ for step in "$@"; do
     exe)  # exe:PROGRAM [ARGS] -- a built tool (e.g. tools/ubench_dep), output to .log
       timeout -k 10 300 $rest > $out.log 2>&1; rc=$?
       tail -12 $out.log ;;
+    trace)  # trace:SCRIPT -- kernel + memory-copy trace (no counters) of python3 SCRIPT
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d ${out}_prof -o run --output-format csv -- python3 $rest > $out.log 2> $out.err; rc=$?
+      [ $rc -eq 0 ] && tail -2 $out.log ;;
     py)
       script=${rest%%:*}; args=""; [ "$rest" != "$script" ] && args=${rest#*:}
       timeout -k 10 600 python -u $script $args > $out.log 2>&1; rc=$?
