@@ -315,10 +315,7 @@ class Stream:
     def update(self, chunks: Sequence) -> None:
         if len(chunks) != self.n:
             raise ValueError(f"need one chunk per message ({self.n})")
-        arrs = [np.frombuffer(c, dtype=np.uint8) if isinstance(c, (bytes, bytearray, memoryview))
-                else np.ascontiguousarray(c, dtype=np.uint8).reshape(-1) for c in chunks]
-        ptrs = (ctypes.c_void_p * self.n)(*[a.ctypes.data if a.size else 0 for a in arrs])
-        lens = _u64([a.size for a in arrs])
+        arrs, ptrs, lens = _host_parts(chunks)
         check(lib().s3h_stream_update_host(self._h, ptrs, _p64(lens)))
 
     def update_device(self, data, offsets, lengths, stream=None) -> None:

@@ -169,3 +169,31 @@ def test_concurrent_stream_objects(torch_cuda, oracle):
     for x in th:
         x.join()
     assert not errors, errors
+
+
+@pytest.mark.parametrize("algo", ["sha256", "md5"])
+def test_stream_messages_past_2_32_bits(torch_cuda, oracle, algo):
+    """Messages longer than 512 MiB (bit length > 2^32: the final block's 64-bit length field
+    uses its high word; sha256.cpp:147-160 / md5.cpp:132-180 padding) streamed from HBM in
+    ragged chunks of up to 64 MiB, with the carry crossing every chunk boundary: digests vs
+    the oracle over the same bytes."""
+    torch = torch_cuda
+    rng = np.random.default_rng(2 ** 32)
+    total = (512 << 20) + 4099  # past 2^32 bits, ragged last block
+    host = rng.integers(0, 256, total + 64, dtype=np.uint8)
+    data = torch.from_numpy(host).cuda()
+    n = 2  # message 1 is message 0 shifted by 7 bytes
+    starts = [0, 7]
+    pos = 0
+    with s3.Stream(n, algo=algo) as st:
+        while pos < total:
+            L = min(int(rng.integers(1, 64 << 20)), total - pos)
+            st.update_device(data, [starts[0] + pos, starts[1] + pos], [L, L])
+            pos += L
+        torch.cuda.synchronize()
+        assert st.total(0) == total and st.total(1) == total
+        got = st.final()
+    for i, s0 in enumerate(starts):
+        m = host[s0:s0 + total].tobytes()
+        want = oracle.sha256(m) if algo == "sha256" else oracle.md5(m)
+        assert np.array_equal(got[i], want), (algo, i)
