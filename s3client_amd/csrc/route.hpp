@@ -39,7 +39,8 @@ int cpu_batch(const uint8_t* const* parts, int fd, const uint64_t* offsets,
       const uint64_t i = order[k];
       uint32_t* h = digests + 8 * i;
       if (fd < 0 || lengths[i] == 0) {  // (sha256_next pads only when total_length > 0)
-        sha256::sha256(fd < 0 ? parts[i] : buf.data(), lengths[i], h);
+        static const uint8_t kEmpty[1] = {0};
+        sha256::sha256(lengths[i] == 0 ? kEmpty : fd < 0 ? parts[i] : buf.data(), lengths[i], h);
         continue;
       }
       sha256::init_hash(h);
@@ -257,7 +258,7 @@ int routed(const uint8_t* const* parts, const char* path, const uint64_t* offset
     struct stat st {};
     rc = fstat(fd, &st) == 0 ? S3H_OK : fail(S3H_EINVAL, "cpu route: cannot stat %s", path);
     for (uint64_t i = 0; rc == S3H_OK && i < n; ++i)
-      if (offsets[i] + lengths[i] > uint64_t(st.st_size))
+      if (lengths[i] > uint64_t(st.st_size) || offsets[i] > uint64_t(st.st_size) - lengths[i])
         rc = fail(S3H_EINVAL, "cpu route: part %llu ends past the end of %s",
                   (unsigned long long)i, path);
     if (rc == S3H_OK) rc = cpu_batch(nullptr, fd, offsets, lengths, n, digests, host_cpus());

@@ -175,6 +175,8 @@ def test_cpu_route_file_parts_vs_oracle(oracle, tmp_path):
     assert np.array_equal(got, want)
     with pytest.raises(s3.S3HashError):  # a range past the end of the file
         s3.sha256_file_parts_routed(str(path), [blob.size - 10], [11], route="cpu")
+    with pytest.raises(s3.S3HashError):  # offset + length wraps past 2^64
+        s3.sha256_file_parts_routed(str(path), [2**64 - 1], [2], route="cpu")
     with pytest.raises(s3.S3HashError):
         s3.sha256_file_parts_routed(str(tmp_path / "missing"), [0], [1], route="cpu")
 
