@@ -1121,12 +1121,23 @@ struct s3h_stream_s {
   uint8_t* d_stage = nullptr;  // host-form updates: chunks staged here
   uint64_t stage_cap = 0;
   uint32_t* d_dig = nullptr;   // host-form final
-  // pinned staging of one update / final (reused once `staged` has completed)
-  s3h::SpliceJob* h_jobs = nullptr;
-  s3h::Slot* h_slots[2] = {nullptr, nullptr};
-  uint32_t* h_order[2] = {nullptr, nullptr};
-  uint64_t* h_bits = nullptr;
-  hipEvent_t staged = nullptr;
+  // Pinned staging of an update / final in two sets used alternately: set b is rewritten
+  // only once the call that used it two calls ago has completed (staged[b]), so the host
+  // prepares update k+1 while update k's kernels run (one set made every update wait for the
+  // previous one's kernels: the GPU idled ~45 us per update, -4.7 % at 64 KiB chunks).
+  uint8_t* h_pin = nullptr;
+  s3h::SpliceJob* h_jobs[2] = {nullptr, nullptr};
+  s3h::Slot* h_slots[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  uint32_t* h_order[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  uint64_t* h_bits[2] = {nullptr, nullptr};
+  hipEvent_t staged[2] = {nullptr, nullptr};
+  hipEvent_t done = nullptr;  // end of the last update / final: the next call's stream waits on it
+  unsigned set = 0;
+  // What the head / body plans' device slots hold: an update whose lengths equal them and
+  // whose offsets are them plus one constant (equal chunks appended in place) reuses the
+  // slots with the launch base moved by that constant -- no re-sort, no copies.
+  std::vector<uint64_t> up_offs[2], up_lens[2];
+  bool up_valid[2] = {false, false};
   hipStream_t own = nullptr;
   std::vector<uint64_t> total;
   std::vector<uint32_t> carry;
@@ -1138,15 +1149,17 @@ namespace {
 void stream_free(s3h_stream_s* S) {
   DeviceGuard g(S->device);
   if (S->own) (void)hipStreamSynchronize(S->own);
-  if (S->staged) (void)hipEventSynchronize(S->staged);
+  for (hipEvent_t e : {S->staged[0], S->staged[1], S->done})
+    if (e) (void)hipEventSynchronize(e);
   s3h_plan_destroy(S->head);
   s3h_plan_destroy(S->body);
   s3h_plan_destroy(S->fin);
   for (void* p : {(void*)S->d_state, (void*)S->d_carry, (void*)S->d_head, (void*)S->d_jobs,
                   (void*)S->d_bits, (void*)S->d_stage, (void*)S->d_dig})
     (void)hipFree(p);
-  (void)hipHostFree(S->h_jobs);
-  if (S->staged) (void)hipEventDestroy(S->staged);
+  (void)hipHostFree(S->h_pin);
+  for (hipEvent_t e : {S->staged[0], S->staged[1], S->done})
+    if (e) (void)hipEventDestroy(e);
   if (S->own) (void)hipStreamDestroy(S->own);
   delete S;
 }
@@ -1160,10 +1173,61 @@ int stream_reset(s3h_stream_s* S, hipStream_t s) {
   return S3H_OK;
 }
 
+// Claims the next staging set for a call on stream `s`: waits (host) until the set's previous
+// use has completed, and orders `s` after the previous call's work on any stream.
+int stream_begin(s3h_stream_s* S, hipStream_t s, unsigned* b) {
+  *b = S->set;
+  S->set ^= 1u;
+  HIP_TRY(hipEventSynchronize(S->staged[*b]));
+  HIP_TRY(hipStreamWaitEvent(s, S->done, 0));
+  return S3H_OK;
+}
+
+int stream_end(s3h_stream_s* S, hipStream_t s, unsigned b) {
+  HIP_TRY(hipEventRecord(S->staged[b], s));
+  HIP_TRY(hipEventRecord(S->done, s));
+  return S3H_OK;
+}
+
+// Launch base of update plan `which` (0 head, 1 body) for these slots: the device's slots
+// moved by a constant when they fit (see up_offs), else after a refill from staging set b.
+int stream_plan_base(s3h_stream_s* S, int which, s3h_plan_s* P, const uint8_t* base,
+                     const std::vector<uint64_t>& offs, const std::vector<uint64_t>& lens,
+                     unsigned b, hipStream_t s, const uint8_t** launch_base) {
+  if (S->up_valid[which] && lens == S->up_lens[which]) {
+    bool same = true, have = false;
+    uint64_t delta = 0;
+    for (uint64_t i = 0; i < S->n && same; ++i) {
+      if (!lens[i]) continue;  // an empty slot is never read
+      const uint64_t d = offs[i] - S->up_offs[which][i];
+      if (!have) {
+        delta = d;
+        have = true;
+      } else {
+        same = d == delta;
+      }
+    }
+    if (same) {  // base + off_now == (base + delta) + off_uploaded, modulo 2^64 like the slots
+      *launch_base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(base) + delta);
+      return S3H_OK;
+    }
+  }
+  S->up_valid[which] = false;
+  if (int rc = plan_refill(P, offs.data(), lens.data(), true, S->h_slots[b][which], S->h_order[b][which], s))
+    return rc;
+  S->up_offs[which] = offs;
+  S->up_lens[which] = lens;
+  S->up_valid[which] = true;
+  *launch_base = base;
+  return S3H_OK;
+}
+
 int stream_update(s3h_stream_s* S, const uint8_t* base, const uint64_t* offsets,
                   const uint64_t* lengths, hipStream_t s) {
   const uint64_t n = S->n;
-  HIP_TRY(hipEventSynchronize(S->staged));  // the previous call's staging has been consumed
+  unsigned b = 0;
+  if (int rc = stream_begin(S, s, &b)) return rc;
+  s3h::SpliceJob* const h_jobs = S->h_jobs[b];
   bool any_splice = false, any_head = false, any_body = false;
   for (uint64_t i = 0; i < n; ++i) {
     const uint64_t L = lengths[i], off = L ? offsets[i] : 0;
@@ -1185,7 +1249,7 @@ int stream_update(s3h_stream_s* S, const uint8_t* base, const uint64_t* offsets,
       S->carry[i] = j.r;
     }
     S->total[i] += L;
-    S->h_jobs[i] = j;
+    h_jobs[i] = j;
     any_splice |= j.mode != 0;
     any_head |= (j.mode & s3h::kSpliceHead) != 0;
     any_body |= B != 0;
@@ -1195,22 +1259,23 @@ int stream_update(s3h_stream_s* S, const uint8_t* base, const uint64_t* offsets,
     S->lens2[i] = B;
   }
   if (any_splice) {
-    HIP_TRY(hipMemcpyAsync(S->d_jobs, S->h_jobs, n * sizeof(s3h::SpliceJob), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(S->d_jobs, h_jobs, n * sizeof(s3h::SpliceJob), hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(s3h::stream_splice_kernel, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, s,
                        base, S->d_jobs, S->d_carry, S->d_head, n);
     HIP_TRY(hipGetLastError());
   }
   constexpr uint32_t kAppend = s3h::kNoPad | s3h::kResume;
   if (any_head) {  // the blocks straddling the previous update and this one come first
-    if (int rc = plan_refill(S->head, S->offs.data(), S->lens.data(), true, S->h_slots[0], S->h_order[0], s)) return rc;
-    if (int rc = launch_args(S->head, S->d_head, nullptr, S->d_state, 0, 1, 0, kAppend, nullptr, s)) return rc;
+    const uint8_t* hb = nullptr;
+    if (int rc = stream_plan_base(S, 0, S->head, S->d_head, S->offs, S->lens, b, s, &hb)) return rc;
+    if (int rc = launch_args(S->head, hb, nullptr, S->d_state, 0, 1, 0, kAppend, nullptr, s)) return rc;
   }
   if (any_body) {
-    if (int rc = plan_refill(S->body, S->offs2.data(), S->lens2.data(), true, S->h_slots[1], S->h_order[1], s)) return rc;
-    if (int rc = launch_args(S->body, base, nullptr, S->d_state, 0, S->body->max_blocks, 0, kAppend, nullptr, s)) return rc;
+    const uint8_t* bb = nullptr;
+    if (int rc = stream_plan_base(S, 1, S->body, base, S->offs2, S->lens2, b, s, &bb)) return rc;
+    if (int rc = launch_args(S->body, bb, nullptr, S->d_state, 0, S->body->max_blocks, 0, kAppend, nullptr, s)) return rc;
   }
-  HIP_TRY(hipEventRecord(S->staged, s));
-  return S3H_OK;
+  return stream_end(S, s, b);
 }
 
 // The error words of the stream's three plans (head / body / final launches), once `s` has
@@ -1230,19 +1295,20 @@ int stream_check(s3h_stream_s* S, hipStream_t s) {
 
 int stream_final(s3h_stream_s* S, uint32_t* d_digests, hipStream_t s) {
   const uint64_t n = S->n;
-  HIP_TRY(hipEventSynchronize(S->staged));
+  unsigned b = 0;
+  if (int rc = stream_begin(S, s, &b)) return rc;
   for (uint64_t i = 0; i < n; ++i) {
     S->offs[i] = 64 * i;
     S->lens[i] = S->carry[i];
-    S->h_bits[i] = S->total[i] << 3;
+    S->h_bits[b][i] = S->total[i] << 3;
   }
-  HIP_TRY(hipMemcpyAsync(S->d_bits, S->h_bits, n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-  if (int rc = plan_refill(S->fin, S->offs.data(), S->lens.data(), false, S->h_slots[0], S->h_order[0], s)) return rc;
+  HIP_TRY(hipMemcpyAsync(S->d_bits, S->h_bits[b], n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  if (int rc = plan_refill(S->fin, S->offs.data(), S->lens.data(), false, S->h_slots[b][0], S->h_order[b][0], s)) return rc;
   // one or two padded blocks per message, starting from the appended state
   if (int rc = launch_args(S->fin, S->d_carry, d_digests, S->d_state, 0, S->fin->max_blocks, 0,
                            s3h::kResume, S->d_bits, s)) return rc;
-  HIP_TRY(hipEventRecord(S->staged, s));
-  return stream_reset(S, s);
+  if (int rc = stream_reset(S, s)) return rc;
+  return stream_end(S, s, b);
 }
 
 }  // namespace
@@ -1870,21 +1936,27 @@ int s3h_stream_create(int device, int algo, uint64_t n, int kernel, s3h_stream_t
   if (e == hipSuccess) e = hipMalloc(&S->d_head, n * 64);
   if (e == hipSuccess) e = hipMalloc(&S->d_jobs, n * sizeof(s3h::SpliceJob));
   if (e == hipSuccess) e = hipMalloc(&S->d_bits, n * 8);
-  const size_t per = sizeof(s3h::SpliceJob) + 2 * (sizeof(s3h::Slot) + 4) + 8;
-  uint8_t* pin = nullptr;
-  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&pin), n * per, hipHostMallocDefault);
-  if (e == hipSuccess) {
-    S->h_jobs = reinterpret_cast<s3h::SpliceJob*>(pin);
-    S->h_slots[0] = reinterpret_cast<s3h::Slot*>(pin + n * sizeof(s3h::SpliceJob));
-    S->h_slots[1] = S->h_slots[0] + n;
-    S->h_bits = reinterpret_cast<uint64_t*>(S->h_slots[1] + n);
-    S->h_order[0] = reinterpret_cast<uint32_t*>(S->h_bits + n);
-    S->h_order[1] = S->h_order[0] + n;
-    e = hipEventCreateWithFlags(&S->staged, hipEventDisableTiming);
+  // per message and set: a splice job, two slots, the bit length, two order entries (8-B
+  // aligned in this order)
+  const size_t per = sizeof(s3h::SpliceJob) + 2 * sizeof(s3h::Slot) + 8 + 2 * 4;
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&S->h_pin), 2 * n * per, hipHostMallocDefault);
+  for (int b = 0; b < 2 && e == hipSuccess; ++b) {
+    uint8_t* pin = S->h_pin + b * n * per;
+    S->h_jobs[b] = reinterpret_cast<s3h::SpliceJob*>(pin);
+    S->h_slots[b][0] = reinterpret_cast<s3h::Slot*>(pin + n * sizeof(s3h::SpliceJob));
+    S->h_slots[b][1] = S->h_slots[b][0] + n;
+    S->h_bits[b] = reinterpret_cast<uint64_t*>(S->h_slots[b][1] + n);
+    S->h_order[b][0] = reinterpret_cast<uint32_t*>(S->h_bits[b] + n);
+    S->h_order[b][1] = S->h_order[b][0] + n;
+    e = hipEventCreateWithFlags(&S->staged[b], hipEventDisableTiming);
   }
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&S->done, hipEventDisableTiming);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&S->own, hipStreamNonBlocking);
   if (e == hipSuccess) {
     rc = stream_reset(S, S->own);
+    // every event recorded once, so the first calls' waits have something to wait for
+    for (hipEvent_t ev : {S->staged[0], S->staged[1], S->done})
+      if (!rc && hipEventRecord(ev, S->own) != hipSuccess) rc = fail(S3H_EHIP, "stream: event record failed");
     if (!rc && hipStreamSynchronize(S->own) != hipSuccess) rc = fail(S3H_EHIP, "stream: init failed");
   } else {
     rc = fail(e == hipErrorOutOfMemory ? S3H_ENOMEM : S3H_EHIP, "stream: %s", hipGetErrorString(e));

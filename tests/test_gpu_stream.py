@@ -197,3 +197,30 @@ def test_stream_messages_past_2_32_bits(torch_cuda, oracle, algo):
         m = host[s0:s0 + total].tobytes()
         want = oracle.sha256(m) if algo == "sha256" else oracle.md5(m)
         assert np.array_equal(got[i], want), (algo, i)
+
+
+def test_stream_updates_on_alternating_streams(torch_cuda, oracle):
+    """Back-to-back device updates issued on two different HIP streams in turn, with no host
+    sync between them (the host prepares update k+1 while update k runs): every update is
+    ordered after the previous one on the device, so the digests equal the oracle's over the
+    concatenated chunks."""
+    torch = torch_cuda
+    rng = np.random.default_rng(91)
+    n, rounds = 300, 12
+    lens_r = _schedule(rng, n, rounds, 200000)
+    total = [int(sum(l[i] for l in lens_r)) for i in range(n)]
+    host = rng.integers(0, 256, sum(total) + 64, dtype=np.uint8)
+    data = torch.from_numpy(host).cuda()
+    starts = np.concatenate([[0], np.cumsum(total)[:-1]]).astype(np.int64)
+    pos = np.zeros(n, dtype=np.int64)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    out = torch.zeros((n, 8), dtype=torch.int32, device="cuda")
+    with s3.Stream(n) as st:
+        for k, lens in enumerate(lens_r):
+            st.update_device(data, (starts + pos).astype(np.uint64), lens, streams[k % 2])
+            pos += lens
+        st.final_device(out, streams[0])
+        torch.cuda.synchronize()
+        st.status(streams[0])
+    want = oracle.batch(host, starts, np.array(total), threads=16)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
