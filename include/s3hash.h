@@ -266,7 +266,8 @@ int s3h_verify_batch_host(int algo, const uint8_t *const *parts, const uint64_t 
  *           Whole 64-B blocks are compressed on the GPU; each message's < 64-B remainder is
  *           carried on the device into the next update.  Asynchronous on `stream`; the host
  *           arrays may be reused on return, the device chunks must stay valid until the
- *           stream reaches this point.
+ *           stream reaches this point.  An object's calls run on the device in call order,
+ *           whichever stream each is given (each waits for the previous call's work).
  *   final:  pads every message with its total length, writes n digests (words as in the
  *           batch API) and resets the object to n empty messages.
  * The chaining state, carries and total lengths live on the device (n x 104 B); one object
