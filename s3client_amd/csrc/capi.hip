@@ -94,6 +94,7 @@ struct s3h_plan_s {
   int quad_waves = 1;           // skew / quad kernels: consumer waves per workgroup (1-2)
   uint32_t solo = 0;            // two-group skew grid: leading one-group workgroups (plan_solo)
   uint32_t dual_solo = 0;       // SHA-256 + MD5 of a ragged batch: skew groups of the mixed grid
+  bool dual_apart = false;      // ... whose MD5 chains run on workgroups of their own
   uint64_t* d_clocks = nullptr; // clock probe buffer (caller-owned), see s3h_plan_set_clock_probe
   uint32_t* d_err = nullptr;    // device error word (s3h::kErr* bits), read by plan_check
 };
@@ -190,28 +191,38 @@ uint32_t plan_solo(const s3h::Slot* slots, uint64_t n, uint64_t cus) {
 }
 
 // Both digests of 2,049-8,192 parts (sha256_md5_group_kernel) run every chain at skewp's rate
-// beside a self-fed MD5 wave: ~2,550 cycles per block (C4 shard, 457 GiB/s for both), against
-// ~2,280 for a skew group with its MD5 wave on a CU of its own (kDualGroupSkew: 125 vs 121.5
-// ms for 8 MiB parts).  A ragged batch is timed by its longest parts, so
-// sha256_md5_group_mixed_kernel gives the longest F x 8 slots skew groups and the rest skewp
-// groups: F = the fewest 8-slot groups after which every remaining part, at the skewp rate,
-// ends before the longest part does at the skew rate; 0 (the plain group kernel) when that
-// grid would not fit one workgroup per CU (e.g. equal lengths) or there is nothing to gain.
-constexpr double kDualSkewpOverSkew = 2550.0 / 2280.0;
-uint32_t dual_mixed_solo(const s3h::Slot* slots, uint64_t n, uint64_t cus) {
+// beside a self-fed MD5 wave: ~2,550 cycles per block (C4 shard, 457 GiB/s for both).  A
+// ragged batch is timed by its longest parts, so sha256_md5_group_mixed_kernel gives the
+// longest F x 8 slots skew groups and the rest skewp groups: F = the fewest 8-slot groups
+// after which every remaining part, at the skewp rate, ends before the longest part does at
+// the skew rate.  Preferred form (`apart`): the skew groups' MD5 chains run on workgroups of
+// their own after the skewp ones (64 chains each), so each skew group runs its SHA-256 alone
+// at ~2,224 cycles per block -- C3 both digests 136.0 -> 141.5 GiB/s, the SHA-256-alone rate
+// (profiles/r04_exp_dual_mixed_apart.jsonl); when that grid does not fit one workgroup per
+// CU, each skew group keeps its MD5 wave (~2,280 cycles per block; round 3's form).  0 (the
+// plain group kernel) when neither fits (e.g. equal lengths) or there is nothing to gain.
+uint32_t dual_mixed_solo(const s3h::Slot* slots, uint64_t n, uint64_t cus, bool* apart) {
   constexpr uint64_t kSkew = 8, kSkewp = 32;
+  *apart = false;
   if (n <= 2048 || cus == 0 || (n + kSkewp - 1) / kSkewp > cus) return 0;
   const double longest = double(s3h::nblocks(slots[0].len));
-  uint64_t lo = 0, hi = n;  // first slot whose part ends in time at the skewp rate
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) / 2;
-    if (double(s3h::nblocks(slots[mid].len)) * kDualSkewpOverSkew > longest) lo = mid + 1;
-    else hi = mid;
+  for (int a = S3H_EXP_MIXED_MD5_APART; a >= 0; --a) {
+    const double ratio = a ? 2550.0 / 2224.0 : 2550.0 / 2280.0;
+    uint64_t lo = 0, hi = n;  // first slot whose part ends in time at the skewp rate
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) / 2;
+      if (double(s3h::nblocks(slots[mid].len)) * ratio > longest) lo = mid + 1;
+      else hi = mid;
+    }
+    const uint64_t F = (lo + kSkew - 1) / kSkew;
+    if (F == 0 || F * kSkew >= n) return 0;
+    const uint64_t wgs = F + (n - F * kSkew + kSkewp - 1) / kSkewp + (a ? (8 * F + 63) / 64 : 0);
+    if (wgs <= cus) {
+      *apart = a != 0;
+      return uint32_t(F);
+    }
   }
-  const uint64_t F = (lo + kSkew - 1) / kSkew;
-  if (F == 0 || F * kSkew >= n) return 0;
-  const uint64_t wgs = F + (n - F * kSkew + kSkewp - 1) / kSkewp;
-  return wgs <= cus ? uint32_t(F) : 0u;
+  return 0;
 }
 
 uint64_t sort_slots(const uint64_t* offsets, const uint64_t* lengths, uint64_t n, bool nopad,
@@ -299,7 +310,8 @@ int plan_geometry(s3h_plan_s* P, const uint64_t* offsets, const uint64_t* length
     P->solo = plan_solo(h_slots, n, uint64_t(device_cus(P->device)));
 #endif
   }
-  P->dual_solo = P->algo == S3H_ALGO_SHA256 ? dual_mixed_solo(h_slots, n, uint64_t(device_cus(P->device))) : 0;
+  P->dual_solo = P->algo == S3H_ALGO_SHA256
+                     ? dual_mixed_solo(h_slots, n, uint64_t(device_cus(P->device)), &P->dual_apart) : 0;
   P->grid = P->solo ? P->solo + uint32_t(((n + 7) / 8 - P->solo + 1) / 2)
             : P->kernel == S3H_KERNEL_PC ? uint32_t((n + 63) / 64)
             : P->kernel == S3H_KERNEL_PAIR || P->kernel == S3H_KERNEL_SKEWP
@@ -503,10 +515,12 @@ int dual_launch(s3h_plan_s* S, s3h_plan_s* M, const void* d_base, uint32_t* d_sh
   if (mode == kDualGroup)
     hipLaunchKernelGGL(s3h::sha256_md5_group_kernel<true>, dim3(uint32_t((S->n + 31) / 32)),
                        dim3(192), 0, stream, A, B);
-  else if (mode == kDualGroupMixed)  // the LDS pad keeps one workgroup per CU
-    hipLaunchKernelGGL(s3h::sha256_md5_group_mixed_kernel,
-                       dim3(uint32_t(S->dual_solo + (S->n - 8ull * S->dual_solo + 31) / 32)),
-                       dim3(192), kMixedLdsPad, stream, A, B, S->dual_solo);
+  else if (mode == kDualGroupMixed) {  // the LDS pad keeps one workgroup per CU
+    const uint32_t F = S->dual_solo, G = uint32_t((S->n - 8ull * F + 31) / 32);
+    const uint32_t lead = S->dual_apart ? (8 * F + 63) / 64 : 0;
+    hipLaunchKernelGGL(s3h::sha256_md5_group_mixed_kernel, dim3(F + G + lead), dim3(192),
+                       kMixedLdsPad, stream, A, B, F, G, lead);
+  }
   else if (mode == kDualGroupSkew)
     hipLaunchKernelGGL(s3h::sha256_md5_group_kernel<false>, dim3(uint32_t((S->n + 7) / 8)),
                        dim3(192), 0, stream, A, B);
@@ -1097,8 +1111,9 @@ int plan_refill(s3h_plan_s* P, const uint64_t* offsets, const uint64_t* lengths,
     const uint64_t groups = (P->n + 7) / 8;
     P->grid = uint32_t(P->solo + (groups - P->solo + 1) / 2);
   }
+  P->dual_apart = false;
   P->dual_solo = P->algo == S3H_ALGO_SHA256 && !nopad
-                     ? dual_mixed_solo(h_slots, P->n, uint64_t(device_cus(P->device))) : 0;
+                     ? dual_mixed_solo(h_slots, P->n, uint64_t(device_cus(P->device)), &P->dual_apart) : 0;
   HIP_TRY(hipMemcpyAsync(P->d_slots, h_slots, P->n * sizeof(s3h::Slot), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(P->d_out_idx, h_order, P->n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   return S3H_OK;

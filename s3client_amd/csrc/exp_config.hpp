@@ -35,6 +35,11 @@
 #ifndef S3H_EXP_MD5_PSETS1
 #define S3H_EXP_MD5_PSETS1 3  // the same for md5_pc_kernel<1> (1-block steps): two blocks ahead
 #endif
+#ifndef S3H_EXP_MIXED_MD5_APART
+// ragged dual grid: 1 = the skew groups' MD5 chains on workgroups of their own when that grid
+// fits (else in the skew groups), 0 = always in the skew groups (round 3)
+#define S3H_EXP_MIXED_MD5_APART 1
+#endif
 #ifndef S3H_EXP_TAIL_RAMP_DIV
 // host pipeline: once fewer than DIV slices are left, each slice carries 1/DIV of what is left
 // (slices shrink by (DIV-1)/DIV each, down to 1/16 of a full slice)
@@ -58,6 +63,7 @@ static_assert(S3H_EXP_MD5_BPS == 4, "product build: MD5 kernel with 4-block prod
 static_assert(S3H_EXP_MD5_ROLL == 1, "product build: rolling MD5 row reads");
 static_assert(S3H_EXP_MD5_PSETS == 2, "product build: two MD5 producer register sets");
 static_assert(S3H_EXP_MD5_PSETS1 == 3, "product build: three sets for 1-block MD5 steps");
+static_assert(S3H_EXP_MIXED_MD5_APART == 1, "product build: skew groups' MD5 apart when it fits");
 static_assert(S3H_EXP_TAIL_RAMP_DIV == 8, "product build: host tail slices shrink by 7/8");
 static_assert(S3H_EXP_SPIN_LIMIT == (1u << 24), "product build: flag waits give up after 2^24 polls");
 static_assert(S3H_EXP_STALL_PRODUCER == 0, "product build: producers publish every step");

@@ -1893,8 +1893,12 @@ __global__ __launch_bounds__(192) void sha256_md5_group_kernel(LaunchArgs S, Lau
 // picks F (capi.hip dual_mixed_solo) and launches at most one workgroup per CU (LDS pad).
 // Both bodies index slots from their own group number, so the skewp half runs on LaunchArgs
 // whose slot / out_idx arrays start at slot 8F; the clock probe is off (two group numberings).
+// With `lead_md5` > 0 the 8F longest slots' MD5 chains run apart, on `lead_md5` workgroups
+// after the G skewp ones (one self-fed MD5 wave of 64 chains each), so those skew groups run
+// their SHA-256 alone on their CUs (capi.hip dual_mixed_solo: when that grid fits).
 __global__ __launch_bounds__(192) void sha256_md5_group_mixed_kernel(LaunchArgs S, LaunchArgs M,
-                                                                    uint32_t F) {
+                                                                    uint32_t F, uint32_t G,
+                                                                    uint32_t lead_md5) {
   __shared__ union {
     SkewLds<1, false> skew;
     SkewLds<1, true> skewp;
@@ -1904,14 +1908,20 @@ __global__ __launch_bounds__(192) void sha256_md5_group_mixed_kernel(LaunchArgs 
   __syncthreads();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   S.clocks = nullptr;
+  constexpr uint32_t kSolo = SkewGeom<1, false>::kParts;
   if (blockIdx.x < F) {
-    if (wave == 1)
-      md5_self_body<SkewGeom<1, false>::kParts>(M, blockIdx.x);
-    else
+    if (wave != 1)
       skew_body<1, false, true>(S, blockIdx.x, wave >> 1, L.skew, flags);
+    else if (!lead_md5)
+      md5_self_body<kSolo>(M, blockIdx.x);
     return;
   }
-  constexpr uint32_t kSolo = SkewGeom<1, false>::kParts;
+  if (lead_md5 && blockIdx.x >= F + G) {  // MD5 of slots 0 .. 8F-1, 64 chains per workgroup
+    if (wave != 1) return;
+    M.n = M.n < kSolo * F ? M.n : kSolo * F;
+    md5_self_body<64>(M, blockIdx.x - F - G);
+    return;
+  }
   const uint32_t shift = kSolo * F;
   if (shift >= S.n) return;
   S.slots += shift; S.out_idx += shift; S.n -= shift;

@@ -7,6 +7,7 @@
 # time limit, and the first failure ends the pass (no retries).  Outputs go to
 # gpurun_out/<TAG>_<n>_<NAME>.{log,jsonl,err} and a one-line summary per step to stdout.
 #   pytest[:ARGS]        python -m pytest tests -m gpu -x -v ARGS            (900 s)
+#   pytestlib:LIB[:ARGS] the same against an experiment build (S3H_LIBRARY=LIB)
 #   smoke                __graft_entry__.smoke()                              (120 s)
 #   bench[:ARGS]         python bench.py ARGS -> one JSON line                (400 s)
 #   benchlib:LIB[:ARGS]  the same with S3H_LIBRARY=LIB (a `make exp` build)    (400 s)
@@ -32,6 +33,10 @@ for step in "$@"; do
   case $name in
     pytest)
       eval "timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread $rest" > $out.log 2>&1; rc=$?
+      tail -1 $out.log ;;
+    pytestlib)  # pytestlib:LIB:ARGS -- GPU tests against an experiment build (S3H_LIBRARY=LIB)
+      lib=${rest%%:*}; args=""; [ "$rest" != "$lib" ] && args=${rest#*:}
+      eval "S3H_LIBRARY=$lib timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread $args" > $out.log 2>&1; rc=$?
       tail -1 $out.log ;;
     smoke)
       timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $out.log 2>&1; rc=$?

@@ -48,7 +48,7 @@ ALL_KERNELS = {
     "dual_split": "_ZN3s3h22sha256_md5_dual_kernelILb0EEEvNS_10LaunchArgsES1_j",
     "dual_group": "_ZN3s3h23sha256_md5_group_kernelILb1EEEvNS_10LaunchArgsES1_",
     "dual_group_skew": "_ZN3s3h23sha256_md5_group_kernelILb0EEEvNS_10LaunchArgsES1_",
-    "dual_group_mixed": "_ZN3s3h29sha256_md5_group_mixed_kernelENS_10LaunchArgsES0_j",
+    "dual_group_mixed": "_ZN3s3h29sha256_md5_group_mixed_kernelENS_10LaunchArgsES0_jjj",
 }
 FLAG_KERNELS = ("skew_nc2", "skews", "dual_group", "dual_group_skew", "dual_group_mixed")
 ERR_STORE = re.compile(r"^\t(global|flat|buffer)_atomic_or\b")
