@@ -10,11 +10,11 @@ from .hashing import (Plan, device_count, digests_to_text, generate_parts, hash_
                       sha256_md5_file_parts,
                       trim, sha256_batch_host_on, host_threads, device_pci_bus_id,
                       route_model, route_estimate, sha256_batch_routed,
-                      sha256_file_parts_routed)
+                      sha256_file_parts_routed, BufferParts)
 from .upload import upload_parts_geometry, UploadPart
 from ._native import S3HashError, LIB_PATH
 
-__all__ = ["Plan", "device_count", "digests_to_text", "generate_parts", "hash_to_text",
+__all__ = ["BufferParts", "Plan", "device_count", "digests_to_text", "generate_parts", "hash_to_text",
            "hmac256", "nblocks", "sha256", "sha256_batch_device", "sha256_batch_host",
            "cpu_backend", "md5", "md5_batch_device", "md5_batch_host", "multipart_etag",
            "verify_batch_device", "verify_batch_host", "Stream",

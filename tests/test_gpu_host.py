@@ -515,3 +515,33 @@ def test_dual_digest_host_beyond_one_grid(torch_cuda, oracle):
     assert np.array_equal(sha, oracle.batch(h, po, pl, threads=16))
     assert np.array_equal(m5, oracle.md5_batch(h, po, pl, threads=16))
     del pinned, h, pv
+
+
+def test_buffer_parts_match_views(torch_cuda, oracle):
+    """BufferParts (pointers formed in numpy from one buffer) and a list of views give the
+    same digests through every host entry point: SHA-256, MD5, both, verification and the
+    routed call; pinned and pageable buffers; empty parts included."""
+    torch = torch_cuda
+    rng = np.random.default_rng(4242)
+    n = 3000
+    lens = rng.integers(0, 200000, n)
+    lens[:4] = [0, 1, 64, 0]
+    offs = np.concatenate([[0], np.cumsum(lens + 5)[:-1]])
+    size = int(offs[-1] + lens[-1]) + 64
+    pinned = torch.empty(size, dtype=torch.uint8, pin_memory=True)
+    for buf in (pinned, rng.integers(0, 256, size, dtype=np.uint8)):
+        h = buf.numpy() if hasattr(buf, "numpy") else buf
+        if hasattr(buf, "numpy"):
+            h[:] = rng.integers(0, 256, size, dtype=np.uint8)
+        bp = s3.BufferParts(buf, offs, lens)
+        want = oracle.batch(h, offs, lens, threads=16)
+        assert np.array_equal(s3.sha256_batch_host(bp), want)
+        assert np.array_equal(s3.md5_batch_host(bp), oracle.md5_batch(h, offs, lens, threads=16))
+        sha, m5 = s3.sha256_md5_batch_host(bp)
+        assert np.array_equal(sha, want)
+        exp = want.copy()
+        exp[[7, 2999]] ^= 1
+        assert np.flatnonzero(s3.verify_batch_host(bp, exp)).tolist() == [7, 2999]
+        got, taken = s3.sha256_batch_routed(bp, route="gpu")
+        assert np.array_equal(got, want) and taken == "gpu"
+    del pinned
