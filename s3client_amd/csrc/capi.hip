@@ -1147,7 +1147,10 @@ struct s3h_stream_s {
   uint64_t* h_bits[2] = {nullptr, nullptr};
   hipEvent_t staged[2] = {nullptr, nullptr};
   hipEvent_t done = nullptr;  // end of the last update / final: the next call's stream waits on it
+  hipStream_t done_on = nullptr;  // the stream `done` was recorded on (same stream: no wait)
+  bool done_set = false;
   unsigned set = 0;
+  bool used_stage = false;  // this call copied from staging set `set ^ 1` (else no staged[] record)
   // What the head / body plans' device slots hold: an update whose lengths equal them and
   // whose offsets are them plus one constant (equal chunks appended in place) reuses the
   // slots with the launch base moved by that constant -- no re-sort, no copies.
@@ -1193,14 +1196,19 @@ int stream_reset(s3h_stream_s* S, hipStream_t s) {
 int stream_begin(s3h_stream_s* S, hipStream_t s, unsigned* b) {
   *b = S->set;
   S->set ^= 1u;
+  S->used_stage = false;
   HIP_TRY(hipEventSynchronize(S->staged[*b]));
-  HIP_TRY(hipStreamWaitEvent(s, S->done, 0));
+  if (!S->done_set || s != S->done_on) HIP_TRY(hipStreamWaitEvent(s, S->done, 0));
   return S3H_OK;
 }
 
+// staged[b] is recorded only when the call copied from set b (an update that reused the
+// device slots copied nothing; the set's previous record still bounds its last use).
 int stream_end(s3h_stream_s* S, hipStream_t s, unsigned b) {
-  HIP_TRY(hipEventRecord(S->staged[b], s));
+  if (S->used_stage) HIP_TRY(hipEventRecord(S->staged[b], s));
   HIP_TRY(hipEventRecord(S->done, s));
+  S->done_on = s;
+  S->done_set = true;
   return S3H_OK;
 }
 
@@ -1228,6 +1236,7 @@ int stream_plan_base(s3h_stream_s* S, int which, s3h_plan_s* P, const uint8_t* b
     }
   }
   S->up_valid[which] = false;
+  S->used_stage = true;
   if (int rc = plan_refill(P, offs.data(), lens.data(), true, S->h_slots[b][which], S->h_order[b][which], s))
     return rc;
   S->up_offs[which] = offs;
@@ -1274,6 +1283,7 @@ int stream_update(s3h_stream_s* S, const uint8_t* base, const uint64_t* offsets,
     S->lens2[i] = B;
   }
   if (any_splice) {
+    S->used_stage = true;
     HIP_TRY(hipMemcpyAsync(S->d_jobs, h_jobs, n * sizeof(s3h::SpliceJob), hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(s3h::stream_splice_kernel, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, s,
                        base, S->d_jobs, S->d_carry, S->d_head, n);
@@ -1317,6 +1327,7 @@ int stream_final(s3h_stream_s* S, uint32_t* d_digests, hipStream_t s) {
     S->lens[i] = S->carry[i];
     S->h_bits[b][i] = S->total[i] << 3;
   }
+  S->used_stage = true;
   HIP_TRY(hipMemcpyAsync(S->d_bits, S->h_bits[b], n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
   if (int rc = plan_refill(S->fin, S->offs.data(), S->lens.data(), false, S->h_slots[b][0], S->h_order[b][0], s)) return rc;
   // one or two padded blocks per message, starting from the appended state
