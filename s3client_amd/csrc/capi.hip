@@ -923,7 +923,11 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
       uniform = lens[j] == lens[0] && parts[sh.parts[j]] - parts[sh.parts[j - 1]] == stride;
   }
   // Too many pageable parts for the staging cap even at 64 B per slice: pageable DMAs.
+#ifdef S3H_EXP_PAGEABLE_DIRECT  // tools/ experiment builds only: pageable DMAs, no staging
+  bool direct_pageable = staged && parts;
+#else
   bool direct_pageable = staged && parts && n * 64 > kStageSlot;
+#endif
   if (direct_pageable) staged = false;
   if (slice == 0)
     slice = staged ? std::max<uint64_t>(std::max<uint64_t>(64, kStageSlot / n / 64 * 64),

@@ -4,7 +4,7 @@ and box: one 8 GiB file (random 64 MiB pattern repeated), 1,024 ranges of 8 MiB.
 JSON line per call and a summary line (median GiB/s per size); every call's digests must
 equal the first call's.
 
-usage: python3 tools/file_parts_ab.py [GIB] [SIZES_KIB] [ROUNDS] [SOURCE] [PART_MIB]  (defaults 8,
+usage: python3 tools/file_parts_ab.py [GIB] [SIZES_KIB] [ROUNDS] [SOURCE] [PART_MIB] [LIBRARY]  (defaults 8,
 0,32,64,128,256, 3, file, 8; 0 = the library's own choice; SOURCE file = s3h_sha256_file_parts,
 dual = s3h_sha256_md5_file_parts, memory = the file read into pageable RAM, then
 s3h_sha256_batch_host over 1,024 views: host threads memcpy into the staging slot)"""
@@ -17,6 +17,8 @@ import time
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if len(sys.argv) > 6:  # an experiment build (make exp) instead of the product library
+    os.environ["S3H_LIBRARY"] = sys.argv[6]
 import s3client_amd as s3  # noqa: E402
 
 
