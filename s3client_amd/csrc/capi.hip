@@ -1196,7 +1196,9 @@ int stream_reset(s3h_stream_s* S, hipStream_t s) {
 }
 
 // Claims the next staging set for a call on stream `s`: waits (host) until the set's previous
-// use has completed, and orders `s` after the previous call's work on any stream.
+// use has completed, and orders `s` after the previous call's work on any stream (on the
+// same stream, stream order does it; a handle reused after hipStreamDestroy is safe too, as
+// destroying a stream waits for its work).
 int stream_begin(s3h_stream_s* S, hipStream_t s, unsigned* b) {
   *b = S->set;
   S->set ^= 1u;
