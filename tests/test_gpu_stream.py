@@ -224,3 +224,22 @@ def test_stream_updates_on_alternating_streams(torch_cuda, oracle):
         st.status(streams[0])
     want = oracle.batch(host, starts, np.array(total), threads=16)
     assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+
+
+def test_stream_host_updates_from_buffer_parts(torch_cuda, oracle):
+    """Host-form updates whose chunks are BufferParts ranges of one host buffer (pointers
+    formed in numpy): digests equal the oracle's over the concatenated chunks."""
+    rng = np.random.default_rng(77)
+    n, rounds = 200, 4
+    lens_r = _schedule(rng, n, rounds, 30000)
+    msgs = [bytearray() for _ in range(n)]
+    with s3.Stream(n) as st:
+        for lens in lens_r:
+            buf = rng.integers(0, 256, int(lens.sum()) + 64, dtype=np.uint8)
+            offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
+            st.update(s3.BufferParts(buf, offs, lens))
+            for i in range(n):
+                msgs[i] += buf[offs[i]:offs[i] + lens[i]].tobytes()
+        got = st.final()
+    want = np.stack([oracle.sha256(bytes(m)) for m in msgs])
+    assert np.array_equal(got, want)
