@@ -35,7 +35,7 @@
 //
 //   s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory] [--per-job]
 //                  [--cpu] [--verify] [--print-headers] [--send] [--get-verify] [--retries N]
-//                  [--content-md5] [--route gpu|cpu|auto]
+//                  [--content-md5] [--check-etag] [--route gpu|cpu|auto]
 //                  [--devices N]
 //                  [--repeat R] [--endpoint URL[,URL...] --bucket B --key K --access A
 //                  --secret S --upload-id ID]
@@ -234,7 +234,7 @@ void usage() {
   std::fprintf(stderr,
                "usage: s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory]\n"
                "       [--per-job] [--cpu] [--verify] [--print-headers] [--send] [--get-verify]\n"
-               "       [--retries N] [--content-md5] [--route gpu|cpu|auto]\n"
+               "       [--retries N] [--content-md5] [--check-etag] [--route gpu|cpu|auto]\n"
                "       [--endpoint URL[,URL...] --bucket B --key K --access A --secret S --upload-id ID]\n"
                "       [--devices N] [--repeat R]\n");
 }
@@ -249,6 +249,11 @@ int main(int argc, char** argv) {
   int jobs = 1, ppj = 1, devices = 0, repeat = 1, max_retries = 0;
   bool cpu = false, verify = false, print_headers = false, per_job = false, send_parts = false;
   bool content_md5 = false;  // also send Content-MD5: both digests from one pass
+  // --check-etag: each UploadPart's ETag must equal the part's MD5 (plain buckets).  Off by
+  // default, as in the reference (DoUploadFilePart / DoUploadPart only require an ETag,
+  // multipart_upload.cpp:101-105, 138-143): SSE-KMS / SSE-C parts have non-MD5 ETags, and a
+  // Content-MD5 header already makes the server check the body.
+  bool check_etag = false;
   bool get_verify = false;   // after the upload, GET every part back and verify it
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
@@ -265,6 +270,7 @@ int main(int argc, char** argv) {
     else if (a == "--send") send_parts = true;
     else if (a == "--retries") max_retries = std::atoi(next().c_str());
     else if (a == "--content-md5") content_md5 = true;
+    else if (a == "--check-etag") check_etag = true;
     else if (a == "--get-verify") get_verify = true;
     else if (a == "--endpoint") endpoint = next();
     else if (a == "--bucket") bucket = next();
@@ -320,8 +326,9 @@ int main(int argc, char** argv) {
     offs.push_back(p.offset);
   }
 
-  std::vector<std::string> hex(parts.size()), md5b64(content_md5 ? parts.size() : 0);
-  std::vector<uint32_t> md5w(content_md5 ? 4 * parts.size() : 0);  // GPU MD5s: ETag check
+  const bool want_md5 = content_md5 || check_etag;  // MD5s: Content-MD5 and/or the ETag check
+  std::vector<std::string> hex(parts.size()), md5b64(want_md5 ? parts.size() : 0);
+  std::vector<uint32_t> md5w(want_md5 ? 4 * parts.size() : 0);  // GPU MD5s
   // GPU runtime start-up (device discovery, code-object load) happens once per process in a
   // real uploader: do it before the timed hash stage with a one-part warm-up batch.
   double init_s = 0;
@@ -393,8 +400,8 @@ int main(int argc, char** argv) {
   // Part i to endpoint e, signed afresh (new x-amz-date) on every attempt; a failed attempt
   // is repeated while the shared retry budget lasts (retriesG, upload.cpp:55-69).  As
   // DoUploadFilePart / DoUploadPart (multipart_upload.cpp:101-105, 138-143) a 200 without an
-  // ETag fails the attempt; with --content-md5 the ETag must also equal the part's MD5 from
-  // the GPU (S3 returns the body's MD5 as a part's ETag), else the attempt fails.
+  // ETag fails the attempt; with --check-etag the ETag must also equal the part's MD5 from
+  // the GPU (S3 returns a plain part's body MD5 as its ETag), else the attempt fails.
   auto put = [&](size_t i, size_t e) {
     const uint8_t* mem = source == "file" ? nullptr : ptrs[i];
     std::string why;
@@ -406,7 +413,7 @@ int main(int argc, char** argv) {
                                 s3h::sigv4::SignHeaders(c), mem, fd, offs[i], lens[i], &etag);
       if (code == 200 && etag.empty()) {
         why = "no ETag found in the HTTP header";
-      } else if (code == 200 && content_md5) {
+      } else if (code == 200 && check_etag) {
         char want[33];
         md5::hash_to_text(&md5w[4 * i], want);
         std::string got(etag);
@@ -433,7 +440,7 @@ int main(int argc, char** argv) {
     char t[65];
     sha256::hash_to_text(h, t);
     hex[i] = t;
-    if (content_md5) {
+    if (want_md5) {
       uint32_t* m = &md5w[4 * i];
       md5::md5(ptrs[i], lens[i], m);
       md5b64[i] = base64(reinterpret_cast<const uint8_t*>(m), 16);
@@ -448,7 +455,7 @@ int main(int argc, char** argv) {
       l.push_back(lens[i]);
       o.push_back(offs[i]);
     }
-    if (content_md5) {  // both digests, each slice read and copied once
+    if (want_md5) {  // both digests, each slice read and copied once
       const sha256::DualDigests d = source == "file"
                                         ? sha256::file_part_sha256_md5(file, o, l, devices)
                                         : sha256::sha256_md5_batch(p, l, devices);
@@ -605,7 +612,7 @@ int main(int argc, char** argv) {
   if (!cpu) std::fprintf(stderr, " (GPU runtime start-up before it: %.3f s)", init_s);
   std::fprintf(stderr, "\n");
   for (const std::string& f : failures) std::fprintf(stderr, "upload failed: %s\n", f.c_str());
-  if (content_md5) {  // the ETag CompleteMultipartUpload would return, from the GPU MD5s
+  if (want_md5) {  // the ETag CompleteMultipartUpload would return, from the GPU MD5s
     try {
       std::fprintf(stderr, "multipart etag: %s\n", md5::multipart_etag(md5w).c_str());
     } catch (const std::exception& e) {

@@ -481,6 +481,8 @@ def main():
             "issue": issue,
             "power": power[0] if world == 1 else power,
         }
+        if world == 1:
+            line["power"].update(energy(power[0], value))
         default_c2 = (world == 1 and args.config == "c2" and args.algo == "sha256"
                       and not args.parts_per_gpu and not args.part_bytes)
         if default_c2 and not args.no_host_resident:
@@ -652,6 +654,16 @@ def issue_model(kname: str, nparts: int, kern_ms: float, info: dict, probe) -> d
             "parallelism_ceiling": round(min(nparts, 65536) / 65536, 5)}
 
 
+def energy(power: dict, gibps: float) -> dict:
+    """Joules per GiB hashed (board power over the timed launches / rate) and the energy-delay
+    product (J/GiB x s/GiB) that s3h_kernel_policy's "efficiency" minimises."""
+    w = power.get("busy_mean_W") if isinstance(power, dict) else None
+    if not w or not gibps:
+        return {}
+    return {"J_per_GiB": round(w / gibps, 4),
+            "energy_delay_J_s_per_GiB2": round(w / gibps / gibps, 7)}
+
+
 def parity_failures(obj, path: str = "") -> list:
     """Every digest comparison in the line that failed: a non-zero mismatch count or a false
     digests-match flag anywhere in the nested sub-measurements."""
@@ -765,34 +777,89 @@ def h2d_copy_rate(torch, host, dev, chunk: int = 1 << 30, reps: int = 3,
     return res
 
 
+def allowed_mem_nodes() -> list:
+    """NUMA nodes this process may allocate on (/proc/self/status Mems_allowed_list)."""
+    try:
+        with open("/proc/self/status") as f:
+            s = next(l.split(":", 1)[1].strip() for l in f if l.startswith("Mems_allowed_list"))
+    except (OSError, StopIteration):
+        return []
+    out = []
+    for part in s.split(","):
+        lo, _, hi = part.partition("-")
+        out += list(range(int(lo), int(hi or lo) + 1))
+    return out
+
+
+def pinned_on(s3, torch, nbytes: int, node: int):
+    """(PinnedBuffer on NUMA node `node`, CPU torch view of it)."""
+    buf = s3.PinnedBuffer(nbytes, node)
+    return buf, torch.from_numpy(buf.array)
+
+
 def host_resident(s3, torch, data, ids, lens, offs, gd, reps: int = 3):
     """The same C2 batch starting and ending in HOST memory (H2D included): the parts are
-    copied once into pinned memory (outside the timed region), then s3h_sha256_batch_host
-    streams them through the HBM ring and returns the digests to the host."""
+    copied once into pinned memory on the device's NUMA node (s3h_host_alloc, outside the timed
+    region), then s3h_sha256_batch_host streams them through the HBM ring and returns the
+    digests to the host.  On a multi-node host the same bytes are also pinned on another node
+    and the two buffers timed alternately (`numa`: the local/remote A/B)."""
     end = int(offs[-1] + lens[-1])
-    host = torch.empty(end, dtype=torch.uint8, pin_memory=True)
+    dev = data.device
+    dev_node = s3.device_numa(dev.index)["node"]
+    local_buf, host = pinned_on(s3, torch, end, dev_node)
     host.copy_(data[:end])
     parts = s3.BufferParts(host, offs, lens)  # part pointers formed in numpy
     out = s3.sha256_batch_host(parts, ndevices=1)  # warm: the per-device context is cached
-    times = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        out = s3.sha256_batch_host(parts, ndevices=1)
-        times.append(time.perf_counter() - t0)
     gib = float(lens.sum()) / 2**30
+
+    def timed(p):
+        t0 = time.perf_counter()
+        o = s3.sha256_batch_host(p, ndevices=1)
+        return time.perf_counter() - t0, o
+
+    others = [n for n in allowed_mem_nodes() if n != dev_node] if dev_node >= 0 else []
+    remote = rparts = rhost = None
+    if others:
+        remote, rhost = pinned_on(s3, torch, end, others[0])
+        rhost.copy_(host)
+        rparts = s3.BufferParts(rhost, offs, lens)
+        s3.sha256_batch_host(rparts, ndevices=1)
+    times, rtimes, rsame = [], [], True
+    for _ in range(reps):  # local and remote alternately
+        t, out = timed(parts)
+        times.append(t)
+        if rparts is not None:
+            t, ro = timed(rparts)
+            rtimes.append(t)
+            rsame = rsame and bool(np.array_equal(ro, out))
     uniform = bool((np.diff(offs) == lens[0]).all() and (lens == lens[0]).all()) and offs[0] == 0
-    h2d = h2d_copy_rate(torch, host, data.device, rows=len(lens) if uniform else 0,
+    h2d = h2d_copy_rate(torch, host, dev, rows=len(lens) if uniform else 0,
                         row_bytes=256 * 1024)
+    numa = {"device_node": dev_node, "buffer_node": s3.mem_node(host),
+            "host_path": s3.host_numa_info(dev.index),
+            "policy": "staging + copy threads on the device's node (s3h_host_numa local)"}
+    if rparts is not None:
+        rh2d = h2d_copy_rate(torch, rhost, dev)
+        numa.update({"remote_buffer_node": s3.mem_node(rhost),
+                     "local_GiBps": round(gib / float(np.mean(times)), 3),
+                     "remote_GiBps": round(gib / float(np.mean(rtimes)), 3),
+                     "remote_over_local": round(float(np.mean(times)) / float(np.mean(rtimes)), 4),
+                     "remote_h2d_copy_GiBps": rh2d["GiBps"],
+                     "digests_match_remote_run": rsame,
+                     "ab": f"{reps} alternating calls per buffer, same bytes pinned on node "
+                           f"{dev_node} (local) and node {others[0]} (remote)"})
     res = {"metric": "host-resident (H2D-inclusive) SHA-256 GiB/s, same C2 parts",
            "value": round(gib / float(np.mean(times)), 3), "best": round(gib / min(times), 3),
            "unit": "GiB/s", "ms_per_batch": round(1e3 * float(np.mean(times)), 2), "reps": reps,
            "h2d_copy": h2d,
            "frac_of_h2d_copy": round(gib / float(np.mean(times)) / h2d["GiBps"], 4),
-           "path": "pinned host parts -> 3-slot HBM ring (one 2-D H2D copy per 256 KiB slice) -> "
-                   "skew kernel per slice -> digests D2H (s3h_sha256_batch_host)",
+           "numa": numa,
+           "path": "pinned host parts (device's NUMA node) -> 3-slot HBM ring (one 2-D H2D copy "
+                   "per 256 KiB slice) -> skew kernel per slice -> digests D2H "
+                   "(s3h_sha256_batch_host)",
            "fixture_mismatches": _fixture_mismatches(s3, ids, out),
            "digests_match_device_run": bool(np.array_equal(out, gd))}
-    del host, parts
+    del host, parts, rhost, rparts, local_buf, remote
     return res
 
 
@@ -902,6 +969,8 @@ def single_gpu_config(s3, torch, dev, cfg: str, ident: dict, steps: int = 2) -> 
             "issue_frac": iss["frac"] if probe else None,
             "power": pw.summary(),
             "parity": {"fixtures_checked": len(checked), "mismatches": int(bad)}}
+        kernels[kinfo["kernel"]].update(energy(kernels[kinfo["kernel"]]["power"],
+                                               part_bytes / 2**30 / wall))
         if kern == "auto":
             gd, info = kd, kinfo
         elif not np.array_equal(kd, gd):
@@ -916,8 +985,25 @@ def single_gpu_config(s3, torch, dev, cfg: str, ident: dict, steps: int = 2) -> 
                                    "clock_GHz", "cycles_per_block", "issue_frac", "power")},
            "bound": "the longest part's chain" if cfg == "c3" else "per-wave issue of 8,192 chains",
            "parity": auto["parity"]}
+    res.update(energy(auto["power"], auto["GiBps"]))
     if len(kernels) > 1:
         res["kernels"] = kernels
+        # s3h_kernel_policy: AUTO under "throughput" = the faster kernel, under "efficiency"
+        # = the lower energy-delay product (J/GiB x s/GiB)
+        ok = {k: v for k, v in kernels.items() if v.get("energy_delay_J_s_per_GiB2")}
+        prev = s3.kernel_policy("efficiency")
+        try:
+            with s3.Plan(offs, lens, device=dev.index) as p:
+                eff_kernel = p.info()["kernel"]
+        finally:
+            s3.kernel_policy(prev)
+        if ok:
+            res["policy_choice"] = {
+                "measured_faster": max(kernels, key=lambda k: kernels[k]["GiBps"]),
+                "measured_lower_energy_delay": min(
+                    ok, key=lambda k: ok[k]["energy_delay_J_s_per_GiB2"]),
+                "auto_throughput_policy": info["kernel"],
+                "auto_efficiency_policy": eff_kernel}
     if dual:
         res["sha256_md5"] = dual
     return res
@@ -1076,6 +1162,8 @@ def c4_shard(args, s3, torch, dist, dev, rank, world, local, ident, ph, steps: i
             "clock_GHz_per_gpu": [x[4] / 1e3 for x in r],
             "cycles_per_block_per_gpu": [x[5] for x in r],
             "board_W_busy_mean_per_gpu": [p.get("busy_mean_W") for p in pws],
+            "J_per_GiB_per_gpu": [energy(p, gib_gpu / t).get("J_per_GiB")
+                                  for p, t in zip(pws, t_rank)],
             "board_W_max_per_gpu": [p.get("max_W") for p in pws],
             "parity": {"fixtures_checked": sum(x[2] for x in r), "mismatches": sum(x[3] for x in r),
                        "fixtures_checked_per_rank": [x[2] for x in r]}}
@@ -1091,11 +1179,13 @@ def c4_shard(args, s3, torch, dist, dev, rank, world, local, ident, ph, steps: i
     return res
 
 
-def shared_buffer_views(h: np.ndarray, per: int, ndev: int, L: int) -> list:
+def shared_buffer_views(h, per: int, ndev: int, L: int) -> list:
     """host_resident_multi's parts: global part i = buffer part i // ndev, so the host path's
     split (part i on device i % ndev) gives every device buffer parts 0..per-1 in order, at the
-    buffer's constant stride L (its 2-D copy form)."""
-    return [h[(i // ndev) * L:(i // ndev + 1) * L] for i in range(per * ndev)]
+    buffer's constant stride L (its 2-D copy form).  `h` is one buffer, or a list of ndev
+    buffers (device d reads h[d]: the buffer on its own NUMA node)."""
+    pick = (lambda i: h[i % ndev]) if isinstance(h, list) else (lambda i: h)
+    return [pick(i)[(i // ndev) * L:(i // ndev + 1) * L] for i in range(per * ndev)]
 
 
 def host_resident_multi(s3, torch, dev, world: int, ph, per: int = 1024, reps: int = 3):
@@ -1103,29 +1193,35 @@ def host_resident_multi(s3, torch, dev, world: int, ph, per: int = 1024, reps: i
     ending in HOST memory, through s3h_sha256_batch_host(..., ndevices=N) -- part i on device
     i % N, one host thread per device -- with every H2D copy inside the timed region.
 
-    Bounded host memory: ONE pinned buffer of 1,024 parts (8 GiB, C2 ids 0..1023) whatever N,
-    and global part i is buffer part i // N, so every device hashes all 1,024 buffer parts
-    (the same per-device work as the device-resident line) and the host DRAM is read N times
-    over, as an uploader staging N devices' parts would.  Parity: every device's digest of
+    Bounded host memory: ONE pinned buffer of 1,024 parts (8 GiB, C2 ids 0..1023) per NUMA
+    node in use, allocated on that node (s3h_host_alloc), whatever N; global part i is part
+    i // N of the buffer on device i % N's node, so every device hashes all 1,024 buffer parts
+    (the same per-device work as the device-resident line) from its own socket's memory, as an
+    uploader staging each device's parts on its node would.  Parity: every device's digest of
     buffer part j equals every other's, and the C2 fixtures pin parts 0..15, 511, 1022, 1023."""
     L = 8 * MIB
     ndev = min(world, torch.cuda.device_count())
     n = per * ndev
     t_setup = time.perf_counter()
-    try:
-        host = torch.empty(per * L, dtype=torch.uint8, pin_memory=True)
-    except RuntimeError as e:
-        return {"error": f"pinned host buffer of {per * L / 2**30:.0f} GiB: {e}"}
+    dev_nodes = [s3.device_numa(d)["node"] for d in range(ndev)]
+    bufs = {}
     buf = torch.empty(per * L, dtype=torch.uint8, device=dev)
     lens = np.full(per, L, dtype=np.uint64)
     offs = np.arange(per, dtype=np.uint64) * np.uint64(L)
     s3.generate_parts(buf, offs, lens, np.arange(per), SEED)
-    host.copy_(buf)
+    try:
+        for node in sorted(set(dev_nodes)):
+            pb, t = pinned_on(s3, torch, per * L, node)
+            t.copy_(buf)
+            bufs[node] = (pb, t)
+    except Exception as e:  # noqa: BLE001 -- reported in the line
+        return {"error": f"pinned host buffer of {per * L / 2**30:.0f} GiB per node: {e}"}
     del buf
     torch.cuda.empty_cache()
-    views = shared_buffer_views(host.numpy(), per, ndev, L)
+    views = shared_buffer_views([bufs[dev_nodes[d]][0].array for d in range(ndev)], per, ndev, L)
+    buffer_nodes = {str(k): s3.mem_node(v[1]) for k, v in bufs.items()}
     setup = time.perf_counter() - t_setup
-    ph.mark("host_resident setup (8 GiB pinned)")
+    ph.mark(f"host_resident setup ({len(bufs)} x 8 GiB pinned, one per NUMA node)")
     out = s3.sha256_batch_host(views, ndevices=ndev)  # warm: a cached context per device
     times = []
     for _ in range(reps):
@@ -1138,18 +1234,23 @@ def host_resident_multi(s3, torch, dev, world: int, ph, per: int = 1024, reps: i
     same = bool((out.reshape(per, ndev, 8) == out.reshape(per, ndev, 8)[:, :1]).all())
     threads, cpus = s3.host_threads(ndev)
     gib = n * L / 2**30
-    del host, views
+    shard_cpus = [s3.host_numa_info(d)["bound_cpus"] for d in range(ndev)]
+    del bufs, views
     s3.trim()
     return {"metric": f"host-resident (H2D-inclusive) SHA-256 GiB/s over {ndev} GPU(s)",
             "value": round(gib / float(np.mean(times)), 3), "best": round(gib / min(times), 3),
             "per_gpu": round(gib / float(np.mean(times)) / ndev, 3), "unit": "GiB/s",
             "devices": ndev, "parts": n, "parts_per_device": per, "reps": reps,
-            "pinned_host_GiB": per * L / 2**30,
+            "pinned_host_GiB": per * L / 2**30 * len(buffer_nodes),
+            "numa": {"device_nodes": dev_nodes, "buffer_nodes": buffer_nodes,
+                     "shard_thread_cpus_per_device": shard_cpus,
+                     "layout": "one 8 GiB pinned buffer per NUMA node in use; each device reads "
+                               "the buffer on its own node, its shard thread bound to that "
+                               "node's CPUs"},
             "ms_per_batch": round(1e3 * float(np.mean(times)), 2), "setup_s": round(setup, 2),
             "path": "pinned host parts -> per-device 3-slot HBM ring (one 2-D H2D copy per "
                     "256 KiB slice) -> skew kernel per slice -> digests D2H "
-                    "(s3h_sha256_batch_host, one host thread per device); one 8 GiB pinned "
-                    "buffer read by every device",
+                    "(s3h_sha256_batch_host, one host thread per device, on its node)",
             "host_cpus": cpus, "staging_threads_per_device": threads,
             "fixtures_checked": len(chk), "fixture_mismatches": int(bad),
             "digests_match_across_devices": same}

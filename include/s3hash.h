@@ -55,6 +55,13 @@ enum s3h_algo {
   S3H_ALGO_MD5 = 1     /* MD5 (Content-MD5, multipart ETags), digests n x 4 words */
 };
 
+/* What AUTO optimises when several kernels fit a batch (s3h_kernel_policy):
+ * S3H_POLICY_THROUGHPUT (default) -- the fastest kernel; S3H_POLICY_EFFICIENCY -- the lowest
+ * energy-delay product.  They differ only for 4,097 - 32 x CUs parts (8,192 on MI355X: the C4
+ * shard), where the shared-SIMD SKEWS kernel is 8.6 % faster than SKEWP but draws 1.2-1.4 kW
+ * against 0.8 kW (2.44 vs 1.66 J/GiB): EFFICIENCY runs SKEWP there. */
+enum s3h_policy { S3H_POLICY_THROUGHPUT = 0, S3H_POLICY_EFFICIENCY = 1 };
+
 /* Last error message of the calling thread ("" if none). */
 const char *s3h_last_error(void);
 int s3h_api_version(void);
@@ -66,6 +73,9 @@ int s3h_api_version(void);
  * into one batch (their digests are the same as from separate calls).  s3h_trim releases the
  * contexts of idle devices. */
 int s3h_trim(void);
+/* Set AUTO's kernel policy for plans created afterwards (initially S3H_POLICY_EFFICIENCY when
+ * the environment has S3H_PREFER_EFFICIENCY=1); *previous receives the old one.  No GPU. */
+int s3h_kernel_policy(int policy, int *previous);
 /* Host threads (the calling thread included) the host path uses per device to stage
  * pageable parts and file ranges when `ndevices` device shards run at once: the CPUs this
  * process may use -- its sched_getaffinity mask, capped by the cgroup CPU quota (cpu.max, or
@@ -79,6 +89,48 @@ int s3h_device_count(int *count);
  * which physical GPU a device index names, so a multi-GPU run can show that its N ranks
  * hashed on N distinct devices.  S3H_ENODEV / S3H_EINVAL as s3h_plan_create. */
 int s3h_device_pci_bus_id(int device, char *out, int len);
+
+/* ---------------------------------------------------------------- NUMA placement
+ * MI355X hosts are dual-socket with four GPUs behind each socket.  The host path puts each
+ * device's pinned staging (pageable parts, file ranges, stream bookkeeping) on the device's
+ * NUMA node and binds its copy threads -- and, for multi-device calls, each device's shard
+ * thread -- to that node's CPUs within the process's affinity mask.  The reference's upload
+ * jobs run wherever the host schedules them (lib/src/upload.cpp:136-140, std::async; bytes
+ * read by ReadFile, lib/src/webclient.cpp:105-116).  None of these needs a GPU except where
+ * stated; S3H_SYSFS_ROOT (tests) replaces /sys.
+ *
+ * NUMA record of a PCI function "dddd:bb:dd.f": sysfs numa_node (-1 when the platform gives
+ * none), local_cpulist (into cpulist, NUL-terminated, truncated to len) and how many of those
+ * CPUs this thread's affinity mask allows.  S3H_EINVAL when the function has no sysfs entry. */
+int s3h_pci_numa(const char *pci_bus_id, int *node, char *cpulist, int len, int *usable_cpus);
+/* The same for HIP device `device` (needs the device: its PCI address). */
+int s3h_device_numa_node(int device, int *node, char *cpulist, int len);
+/* Placement policy of the host path: S3H_NUMA_LOCAL (default: each device's own node),
+ * S3H_NUMA_OFF (no binding: the runtime's placement, unbound threads) or a node >= 0 (every
+ * device's staging and threads on that node -- for local/remote measurements).  Initial value
+ * from the environment: S3H_HOST_NUMA=local|off|<node>.  Idle cached contexts are released
+ * so the next call re-places them.  *previous (if non-null) receives the old mode. */
+#define S3H_NUMA_LOCAL (-1)
+#define S3H_NUMA_OFF (-2)
+int s3h_host_numa(int mode, int *previous);
+typedef struct {
+  int device_node;  /* sysfs numa_node of the device (-1: unknown) */
+  int target_node;  /* node the policy places its staging on (-1: none) */
+  int bound_cpus;   /* CPUs its copy / shard threads bind to (0: unbound) */
+  int staging_node; /* measured node of the cached context's staging ring (-1: none yet) */
+  int threads_node; /* node the cached context's copy threads are bound to (-1: unbound/none) */
+  int copy_threads; /* copy threads of the cached context (0: none yet) */
+} s3h_host_numa_t;
+/* Placement of device `device` under the current policy, plus what its cached host context
+ * actually holds (needs the device). */
+int s3h_host_numa_info(int device, s3h_host_numa_t *info);
+/* Pinned (page-locked, DMA-able) host memory whose pages are bound to NUMA node `node`
+ * (-1: the runtime's placement): an uploader's read buffers on its device's node.  Needs a
+ * HIP device.  Free with s3h_host_free. */
+int s3h_host_alloc(int node, uint64_t bytes, void **out);
+int s3h_host_free(void *p);
+/* NUMA node of the page holding host address p (get_mempolicy). */
+int s3h_mem_node(const void *p, int *node);
 
 /* ---------------------------------------------------------------- device-resident path
  * A plan captures the part geometry (byte offsets relative to a base pointer, lengths) of
@@ -125,6 +177,14 @@ int s3h_plan_groups(s3h_plan_t plan, uint32_t *groups, uint32_t *solo);
  * workgroups of the one-grid dual kernel run the longest parts as 8-part skew groups (a
  * ragged batch of 2,049 - 32 x CUs parts); 0 when the dual pass uses another form. */
 int s3h_plan_dual_solo(s3h_plan_t plan, uint32_t *solo);
+/* The same plus which form of that mixed grid runs: *apart = 1 when the skew groups' MD5
+ * chains run on workgroups of their own (round 4, each skew group at the SHA-256-alone rate),
+ * 0 when each skew group carries its MD5 wave (round 3; used when the apart grid would exceed
+ * one workgroup per CU). */
+int s3h_plan_dual_layout(s3h_plan_t plan, uint32_t *solo, int *apart);
+/* That choice for a batch of `lengths` on a device of `cus` CUs, without a device (pure host
+ * arithmetic, the rule the plan applies). */
+int s3h_dual_layout(const uint64_t *lengths, uint64_t n, int cus, uint32_t *solo, int *apart);
 
 /* Measurement hook (not part of the lib/hash surface): while d_clocks (device memory,
  * 4 x *waves uint64) is set, every launch of a plan on the skew kernel records, per consumer
@@ -218,11 +278,14 @@ int s3h_sha256_md5_batch_device(int device, const void *d_base, const uint64_t *
  * on s3h_host_threads' CPU count, parts longest first; S3H_ROUTE_AUTO = whichever the model
  * below estimates to finish first.  The model's rates are measured once per process on the
  * first AUTO call (~0.1 s: a lone GPU chain, a pinned 32 MiB H2D copy, a one-block host call,
- * 4 MiB on the drop-in).  AUTO needs a visible GPU (S3H_ENODEV otherwise): it chooses
- * between two paths with identical digests and is never a fallback for a missing device.
+ * the drop-in on one thread and on all of them, the threads' staging memcpy).  AUTO needs a
+ * visible GPU (S3H_ENODEV otherwise): it chooses between two paths with identical digests and
+ * is never a fallback for a missing device.
  * *taken (if non-null) receives the route that ran (S3H_ROUTE_GPU or S3H_ROUTE_CPU).
- *   gpu_s = call_s + max(longest part / chain rate, bytes per device / H2D rate)
- *   cpu_s = max(bytes / (threads x per-thread rate), longest part / per-thread rate) */
+ *   gpu_s = call_s + max(longest part / chain rate, bytes per device / feed rate)
+ *           feed = h2d (pinned parts) or min(h2d, staged) (pageable parts, file ranges)
+ *   cpu_s = (longest-first schedule of the parts on k = min(n, threads) threads) / (rate(k) / k)
+ *           rate(k) = min(k x cpu_bytes_per_s, cpu_all_bytes_per_s) */
 enum s3h_route { S3H_ROUTE_GPU = 0, S3H_ROUTE_CPU = 1, S3H_ROUTE_AUTO = 2 };
 typedef struct {
   double cpu_bytes_per_s;   /* one host thread on the lib/hash drop-in (s3h_cpu_backend) */
@@ -231,6 +294,11 @@ typedef struct {
   double call_s;            /* fixed cost of one host-path GPU call (setup, launch, sync) */
   int cpu_threads;          /* host threads of the CPU route (affinity and cgroup quota) */
   int devices;              /* visible HIP devices */
+  double cpu_all_bytes_per_s; /* all cpu_threads threads at once, aggregate: the CPU route on k
+                               * threads runs at min(k x cpu_bytes_per_s, this) -- not linear
+                               * (memory bandwidth, SMT siblings, the cgroup quota) */
+  double staged_bytes_per_s;  /* pageable sources: cpu_threads threads' memcpy into pinned
+                               * staging, aggregate; the GPU route is fed at min(h2d, this) */
 } s3h_route_model_t;
 /* The measured model (measures it on first use).  S3H_ENODEV without a GPU (cpu fields set). */
 int s3h_route_model(s3h_route_model_t *m);
@@ -238,6 +306,11 @@ int s3h_route_model(s3h_route_model_t *m);
  * arithmetic): returns S3H_ROUTE_GPU or S3H_ROUTE_CPU and both time estimates in seconds. */
 int s3h_route_estimate(const s3h_route_model_t *m, const uint64_t *lengths, uint64_t n,
                        int ndevices, double *gpu_s, double *cpu_s);
+/* The same for parts of a given source: S3H_SOURCE_PINNED (as s3h_route_estimate),
+ * S3H_SOURCE_PAGEABLE (staged through pinned memory) or S3H_SOURCE_FILE (file ranges). */
+enum s3h_source { S3H_SOURCE_PINNED = 0, S3H_SOURCE_PAGEABLE = 1, S3H_SOURCE_FILE = 2 };
+int s3h_route_estimate_ex(const s3h_route_model_t *m, const uint64_t *lengths, uint64_t n,
+                          int ndevices, int source, double *gpu_s, double *cpu_s);
 int s3h_sha256_batch_routed(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                             uint32_t *digests, int ndevices, int route, int *taken);
 int s3h_sha256_file_parts_routed(const char *path, const uint64_t *offsets,
@@ -284,6 +357,11 @@ int s3h_stream_final_host(s3h_stream_t s, uint32_t *digests);
 /* Device forms: waits for `stream` and reports (and clears) a fault of any update / final
  * launch since the last check, as s3h_plan_status does for a plan. */
 int s3h_stream_status(s3h_stream_t s, void *stream);
+/* Update launches that found their plan's device slots in place (equal chunk lengths at
+ * offsets moved by one constant: the base pointer moves, no re-sort, no copies) and those
+ * that re-sorted and uploaded the slots.  Host counters, no device sync.  A call that fails
+ * after queueing work leaves the object failed: later calls return S3H_EINVAL (destroy it). */
+int s3h_stream_stats(s3h_stream_t s, uint64_t *slot_reuses, uint64_t *slot_refills);
 /* Bytes appended so far to message i (host bookkeeping; no device sync). */
 int s3h_stream_total(s3h_stream_t s, uint64_t i, uint64_t *total);
 int s3h_stream_destroy(s3h_stream_t s);

@@ -10,7 +10,9 @@ from .hashing import (Plan, device_count, digests_to_text, generate_parts, hash_
                       sha256_md5_file_parts,
                       trim, sha256_batch_host_on, host_threads, device_pci_bus_id,
                       route_model, route_estimate, sha256_batch_routed,
-                      sha256_file_parts_routed, BufferParts)
+                      sha256_file_parts_routed, BufferParts, pci_numa, device_numa,
+                      host_numa, host_numa_info, mem_node, PinnedBuffer,
+                      kernel_policy, dual_layout)
 from .upload import upload_parts_geometry, UploadPart
 from ._native import S3HashError, LIB_PATH
 
@@ -21,5 +23,6 @@ __all__ = ["BufferParts", "Plan", "device_count", "digests_to_text", "generate_p
            "sha256_md5_batch_device", "sha256_md5_batch_host", "sha256_file_parts",
            "sha256_md5_file_parts", "trim", "sha256_batch_host_on", "host_threads",
            "device_pci_bus_id", "route_model", "route_estimate", "sha256_batch_routed",
-           "sha256_file_parts_routed",
+           "sha256_file_parts_routed", "pci_numa", "device_numa", "host_numa", "host_numa_info",
+           "mem_node", "PinnedBuffer", "kernel_policy", "dual_layout",
            "upload_parts_geometry", "UploadPart", "S3HashError", "LIB_PATH"]

@@ -39,8 +39,15 @@ C_ABI_SYMBOLS = (
     "s3h_sha256_md5_file_parts", "s3h_plan_status", "s3h_stream_status", "s3h_host_threads",
     "s3h_plan_dual_solo", "s3h_device_pci_bus_id", "s3h_multipart_etag",
     "s3h_route_model", "s3h_route_estimate", "s3h_sha256_batch_routed",
-    "s3h_sha256_file_parts_routed",
+    "s3h_sha256_file_parts_routed", "s3h_pci_numa", "s3h_device_numa_node", "s3h_host_numa",
+    "s3h_host_numa_info", "s3h_host_alloc", "s3h_host_free", "s3h_mem_node",
+    "s3h_route_estimate_ex", "s3h_kernel_policy", "s3h_stream_stats", "s3h_plan_dual_layout",
+    "s3h_dual_layout",
 )
+POLICY_IDS = {"throughput": 0, "efficiency": 1}
+POLICY_NAMES = {v: k for k, v in POLICY_IDS.items()}
+SOURCE_IDS = {"pinned": 0, "pageable": 1, "file": 2}
+NUMA_LOCAL, NUMA_OFF = -1, -2
 ROUTE_GPU, ROUTE_CPU, ROUTE_AUTO = 0, 1, 2
 ROUTE_IDS = {"gpu": ROUTE_GPU, "cpu": ROUTE_CPU, "auto": ROUTE_AUTO}
 ROUTE_NAMES = {v: k for k, v in ROUTE_IDS.items()}
@@ -50,7 +57,15 @@ class RouteModel(ctypes.Structure):
     """s3h_route_model_t (include/s3hash.h)."""
     _fields_ = [("cpu_bytes_per_s", ctypes.c_double), ("chain_bytes_per_s", ctypes.c_double),
                 ("h2d_bytes_per_s", ctypes.c_double), ("call_s", ctypes.c_double),
-                ("cpu_threads", ctypes.c_int), ("devices", ctypes.c_int)]
+                ("cpu_threads", ctypes.c_int), ("devices", ctypes.c_int),
+                ("cpu_all_bytes_per_s", ctypes.c_double), ("staged_bytes_per_s", ctypes.c_double)]
+
+
+class HostNuma(ctypes.Structure):
+    """s3h_host_numa_t (include/s3hash.h)."""
+    _fields_ = [("device_node", ctypes.c_int), ("target_node", ctypes.c_int),
+                ("bound_cpus", ctypes.c_int), ("staging_node", ctypes.c_int),
+                ("threads_node", ctypes.c_int), ("copy_threads", ctypes.c_int)]
 
 
 ALGO_SHA256, ALGO_MD5 = 0, 1
@@ -97,6 +112,21 @@ def lib() -> ctypes.CDLL:
             L.s3h_last_error.restype = ctypes.c_char_p
             L.s3h_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
             L.s3h_device_pci_bus_id.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+            L.s3h_pci_numa.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int),
+                                       ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+            L.s3h_device_numa_node.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                               ctypes.c_char_p, ctypes.c_int]
+            L.s3h_host_numa.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+            L.s3h_host_numa_info.argtypes = [ctypes.c_int, ctypes.POINTER(HostNuma)]
+            L.s3h_host_alloc.argtypes = [ctypes.c_int, ctypes.c_uint64,
+                                         ctypes.POINTER(ctypes.c_void_p)]
+            L.s3h_host_free.argtypes = [ctypes.c_void_p]
+            L.s3h_kernel_policy.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+            L.s3h_stream_stats.argtypes = [ctypes.c_void_p, u64p, u64p]
+            L.s3h_plan_dual_layout.argtypes = [ctypes.c_void_p, u32p, ctypes.POINTER(ctypes.c_int)]
+            L.s3h_dual_layout.argtypes = [u64p, ctypes.c_uint64, ctypes.c_int, u32p,
+                                          ctypes.POINTER(ctypes.c_int)]
+            L.s3h_mem_node.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
             L.s3h_plan_create.argtypes = [ctypes.c_int, u64p, u64p, ctypes.c_uint64, ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_void_p)]
             L.s3h_plan_create_ex.argtypes = [ctypes.c_int, ctypes.c_int, u64p, u64p,
@@ -164,6 +194,10 @@ def lib() -> ctypes.CDLL:
             L.s3h_route_estimate.argtypes = [ctypes.POINTER(RouteModel), u64p, ctypes.c_uint64,
                                              ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(ctypes.c_double)]
+            L.s3h_route_estimate_ex.argtypes = [ctypes.POINTER(RouteModel), u64p, ctypes.c_uint64,
+                                                ctypes.c_int, ctypes.c_int,
+                                                ctypes.POINTER(ctypes.c_double),
+                                                ctypes.POINTER(ctypes.c_double)]
             L.s3h_sha256_batch_routed.argtypes = [ctypes.POINTER(ctypes.c_void_p), u64p,
                                                   ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
                                                   ctypes.c_int, ctypes.POINTER(ctypes.c_int)]

@@ -7,8 +7,11 @@
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
+#include <pthread.h>
 #include <sched.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <cctype>
@@ -49,12 +52,16 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
+// A failed call also clears the thread's last HIP error: a later hipGetLastError after a
+// launch must report that launch, not an allocation that failed (and was reported) before.
 #define HIP_TRY(expr)                                                                      \
   do {                                                                                     \
     hipError_t e_ = (expr);                                                                \
-    if (e_ != hipSuccess)                                                                  \
+    if (e_ != hipSuccess) {                                                                \
+      (void)hipGetLastError();                                                             \
       return fail(e_ == hipErrorOutOfMemory ? S3H_ENOMEM : S3H_EHIP, "%s: %s (%s:%d)",     \
                   #expr, hipGetErrorString(e_), __FILE__, __LINE__);                       \
+    }                                                                                      \
   } while (0)
 
 int check_device(int device) {
@@ -215,7 +222,10 @@ uint32_t dual_mixed_solo(const s3h::Slot* slots, uint64_t n, uint64_t cus, bool*
       else hi = mid;
     }
     const uint64_t F = (lo + kSkew - 1) / kSkew;
-    if (F == 0 || F * kSkew >= n) return 0;
+    if (F == 0) return 0;  // the smaller ratio below gives no more skew groups
+    // every part would need a skew group at the apart form's ratio: round 3's ratio may
+    // still leave some to the skewp groups (advisor r4)
+    if (F * kSkew >= n) continue;
     const uint64_t wgs = F + (n - F * kSkew + kSkewp - 1) / kSkewp + (a ? (8 * F + 63) / 64 : 0);
     if (wgs <= cus) {
       *apart = a != 0;
@@ -242,11 +252,22 @@ uint64_t sort_slots(const uint64_t* offsets, const uint64_t* lengths, uint64_t n
 // at the skew kernel's 8 VALU per round with its producer on the same SIMD: C4 shard 500 vs
 // 469 GiB/s for skewp on one box (profiles/r02_bench_c4_skews_mulf.jsonl), at about twice the
 // board power (r02_smi_c4_power.txt; INTEGRATION.md: pass S3H_KERNEL_SKEWP to trade it back).
+// Under S3H_POLICY_EFFICIENCY (s3h_kernel_policy; env S3H_PREFER_EFFICIENCY=1) AUTO keeps
+// skewp in that range: the C4 shard runs 8.6 % slower (464 vs 504 GiB/s) but at 1.66 instead
+// of 2.44 J/GiB (board 0.77 vs 1.23 kW, BENCH_r04 configs.c4.kernels) --
+// the lower energy-delay product (J/GiB x s/GiB: 3.6e-3 vs 4.9e-3).  Outside 4,097 - 32 x CUs
+// parts both policies choose the same kernel.
+std::atomic<int> g_kernel_policy{[] {
+  const char* e = std::getenv("S3H_PREFER_EFFICIENCY");
+  return e && std::atoi(e) == 1 ? S3H_POLICY_EFFICIENCY : S3H_POLICY_THROUGHPUT;
+}()};
+
 int resolve_kernel(int algo, uint64_t n, int kernel, uint64_t cus) {
   if (algo == S3H_ALGO_MD5) return S3H_KERNEL_PC;  // MD5 has one kernel (4 VALU per step)
   if (kernel != S3H_KERNEL_AUTO) return kernel;
+  const bool efficient = g_kernel_policy.load() == S3H_POLICY_EFFICIENCY;
   return n <= kQuadMaxParts    ? S3H_KERNEL_SKEW
-         : n <= 32 * cus       ? S3H_KERNEL_SKEWS
+         : n <= 32 * cus       ? (efficient ? S3H_KERNEL_SKEWP : S3H_KERNEL_SKEWS)
          : n <= kSkewpMaxParts ? S3H_KERNEL_SKEWP
          : n <= kPairMaxParts  ? S3H_KERNEL_PAIR
          : n <= kPcMaxParts    ? S3H_KERNEL_PC
@@ -271,20 +292,25 @@ int plan_alloc(int device, int algo, uint64_t cap, s3h_plan_s** out) {
   P->device = device;
   P->algo = algo;
   P->cap = cap;
+  const char* what = "slots";
   hipError_t e = hipMalloc(&P->d_slots, cap * sizeof(s3h::Slot));
-  if (e == hipSuccess) e = hipMalloc(&P->d_out_idx, cap * sizeof(uint32_t));
-  if (e == hipSuccess) e = hipMalloc(&P->d_zero, 256);
+  if (e == hipSuccess) e = hipMalloc(&P->d_out_idx, cap * sizeof(uint32_t)), what = "output order";
+  if (e == hipSuccess) e = hipMalloc(&P->d_zero, 256), what = "zero page";
   if (e == hipSuccess) e = hipMemset(P->d_zero, 0, 256);
-  if (e == hipSuccess) e = hipMalloc(&P->d_err, sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc(&P->d_err, sizeof(uint32_t)), what = "error word";
   if (e == hipSuccess) e = hipMemset(P->d_err, 0, sizeof(uint32_t));
   if (e != hipSuccess) {
+    (void)hipGetLastError();
     (void)hipFree(P->d_slots);
     (void)hipFree(P->d_out_idx);
     (void)hipFree(P->d_zero);
     (void)hipFree(P->d_err);
     delete P;
     *out = nullptr;
-    return fail(e == hipErrorOutOfMemory ? S3H_ENOMEM : S3H_EHIP, "plan alloc: %s", hipGetErrorString(e));
+    return fail(e == hipErrorOutOfMemory ? S3H_ENOMEM : S3H_EHIP,
+                "plan alloc (%llu parts: %llu B of slots + %llu B of output order in HBM; failed at "
+                "the %s): %s", (unsigned long long)cap, (unsigned long long)(cap * sizeof(s3h::Slot)),
+                (unsigned long long)(cap * 4), what, hipGetErrorString(e));
   }
   *out = P;
   return S3H_OK;
@@ -401,6 +427,7 @@ int launch_args(s3h_plan_s* P, const void* d_base, uint32_t* d_digests, uint32_t
                 uint64_t b0, uint64_t b1, uint64_t origin, uint32_t flags, const uint64_t* d_bits,
                 hipStream_t stream) {
   const s3h::LaunchArgs A = make_args(P, d_base, d_digests, d_state, b0, b1, origin, flags, d_bits);
+  (void)hipGetLastError();  // the check below must see this launch, not an older failure
   if (P->algo == S3H_ALGO_MD5 && P->grid <= uint64_t(device_cus(P->device)))
     hipLaunchKernelGGL(s3h::md5_pc_kernel<s3h::kMd5Bps>, dim3(P->grid), dim3(s3h::kPcThreads), 0,
                        stream, A);
@@ -578,14 +605,213 @@ unsigned host_threads_per_device(int ndevices) {
   return std::min(16u, std::max(1u, host_cpus() / unsigned(std::max(1, ndevices))));
 }
 
+// ------------------------------------------------------------------ NUMA placement
+// MI355X nodes are dual-socket hosts with four GPUs behind each socket (the GPU box: devices
+// on node 1, CPUs 64-127,192-255 local to them).  A device's DMA reads host memory through
+// its socket's root complex, so the pinned staging it copies from and the threads that fill
+// that staging (memcpy / pread) belong on the device's node: the sysfs numa_node and
+// local_cpulist of its PCI function.  The reference's jobs run wherever the host schedules
+// them (lib/src/upload.cpp:136-140 std::async, ReadFile lib/src/webclient.cpp:105-116).
+// S3H_SYSFS_ROOT (tests) replaces /sys.  Placement policy: s3h_host_numa (env S3H_HOST_NUMA
+// = local | off | <node>) -- device-local by default.
+constexpr int kMpolBind = 2;
+constexpr int kMpolFNode = 1, kMpolFAddr = 2;
+constexpr unsigned kMaxNumaNodes = 1024;
+
+std::string sysfs_root() {
+  const char* e = std::getenv("S3H_SYSFS_ROOT");
+  return e && *e ? std::string(e) : std::string("/sys");
+}
+
+bool read_line(const std::string& path, std::string* out) {
+  FILE* f = std::fopen(path.c_str(), "r");
+  if (!f) return false;
+  char buf[4096];
+  const bool ok = std::fgets(buf, sizeof buf, f) != nullptr;
+  std::fclose(f);
+  if (!ok) return false;
+  *out = buf;
+  while (!out->empty() && std::isspace(static_cast<unsigned char>(out->back()))) out->pop_back();
+  return true;
+}
+
+// "0-63,128-191" -> set; false when malformed (an empty list is a valid empty set)
+bool parse_cpulist(const std::string& s, cpu_set_t* set) {
+  CPU_ZERO(set);
+  const char* p = s.c_str();
+  while (*p) {
+    char* end = nullptr;
+    const long a = std::strtol(p, &end, 10);
+    if (end == p || a < 0) return false;
+    long b = a;
+    p = end;
+    if (*p == '-') {
+      b = std::strtol(p + 1, &end, 10);
+      if (end == p + 1 || b < a) return false;
+      p = end;
+    }
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET(int(c), set);
+    if (*p == ',') ++p;
+    else if (*p) return false;
+  }
+  return true;
+}
+
+// sysfs NUMA record of one PCI function: node (-1 when the platform gives none) and the
+// CPUs local to it.  S3H_EINVAL when <root>/bus/pci/devices/<bdf> does not exist.
+int pci_numa(const char* bdf, int* node, std::string* cpulist) {
+  if (!bdf || !*bdf) return fail(S3H_EINVAL, "pci numa: empty PCI address");
+  std::string b(bdf);
+  for (char& c : b) c = char(std::tolower(static_cast<unsigned char>(c)));
+  const std::string dir = sysfs_root() + "/bus/pci/devices/" + b;
+  std::string v;
+  if (!read_line(dir + "/numa_node", &v))
+    return fail(S3H_EINVAL, "pci numa: cannot read %s/numa_node", dir.c_str());
+  *node = std::atoi(v.c_str());
+  if (*node < 0) *node = -1;
+  if (!read_line(dir + "/local_cpulist", cpulist)) cpulist->clear();
+  return S3H_OK;
+}
+
+// CPUs of a NUMA node (<root>/devices/system/node/node<k>/cpulist)
+bool node_cpulist(int node, std::string* cpulist) {
+  return node >= 0 && read_line(sysfs_root() + "/devices/system/node/node" + std::to_string(node) + "/cpulist", cpulist);
+}
+
+// Node of the page holding p (get_mempolicy MPOL_F_NODE | MPOL_F_ADDR); -1 if unknown.
+int mem_node(const void* p) {
+  int node = -1;
+  if (!p || syscall(SYS_get_mempolicy, &node, nullptr, 0, p, kMpolFNode | kMpolFAddr) != 0) return -1;
+  return node;
+}
+
+// Pinned host memory whose pages live on `node`: anonymous pages bound there (mbind
+// MPOL_BIND), touched, then page-locked for DMA with hipHostRegister.  node < 0: the
+// runtime's own hipHostMalloc.  pinned_free releases either kind.
+std::mutex g_reg_mu;
+std::vector<std::pair<void*, size_t>>& registered_bufs() {
+  static auto* v = new std::vector<std::pair<void*, size_t>>();
+  return *v;
+}
+
+hipError_t pinned_alloc(void** out, uint64_t bytes, int node) {
+  *out = nullptr;
+  if (node < 0 || node >= int(kMaxNumaNodes)) return hipHostMalloc(out, bytes, hipHostMallocDefault);
+  const size_t len = std::max<size_t>(size_t(bytes), 1);
+  void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) return hipErrorOutOfMemory;
+  unsigned long mask[kMaxNumaNodes / 64] = {};
+  mask[node / 64] = 1ul << (node % 64);
+  if (syscall(SYS_mbind, p, len, kMpolBind, mask, kMaxNumaNodes + 1, 0) != 0) {
+    munmap(p, len);  // node not allowed (cpuset mems) or absent: the runtime's placement
+    return hipHostMalloc(out, bytes, hipHostMallocDefault);
+  }
+  // first touch under the binding (large buffers: 8 threads, ~0.2 s for 8 GiB instead of ~2)
+  const unsigned toucher = len >= (64u << 20) ? std::min(8u, host_cpus()) : 1u;
+  std::vector<std::thread> ts;
+  const size_t per = (len / toucher + 4095) & ~size_t(4095);
+  for (unsigned t = 1; t < toucher; ++t)
+    if (t * per < len)
+      ts.emplace_back([=] { std::memset(static_cast<char*>(p) + t * per, 0, std::min(per, len - t * per)); });
+  std::memset(p, 0, std::min(per, len));
+  for (auto& th : ts) th.join();
+  const hipError_t e = hipHostRegister(p, len, hipHostRegisterDefault);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    munmap(p, len);
+    return e;
+  }
+  std::lock_guard<std::mutex> l(g_reg_mu);
+  registered_bufs().push_back({p, len});
+  *out = p;
+  return hipSuccess;
+}
+
+void pinned_free(void* p) {
+  if (!p) return;
+  size_t len = 0;
+  {
+    std::lock_guard<std::mutex> l(g_reg_mu);
+    auto& v = registered_bufs();
+    for (auto it = v.begin(); it != v.end(); ++it)
+      if (it->first == p) {
+        len = it->second;
+        v.erase(it);
+        break;
+      }
+  }
+  if (len) {
+    (void)hipHostUnregister(p);
+    munmap(p, len);
+  } else {
+    (void)hipHostFree(p);
+  }
+}
+
+// Placement policy: kNumaLocal (the device's node), kNumaOff (no binding), or a forced node
+// (measurements: the remote-node side of an A/B).  Changing it re-places the next contexts.
+constexpr int kNumaLocal = -1, kNumaOff = -2;
+std::atomic<int> g_numa_mode{[] {
+  const char* e = std::getenv("S3H_HOST_NUMA");
+  if (!e || !*e || std::strcmp(e, "local") == 0) return kNumaLocal;
+  if (std::strcmp(e, "off") == 0) return kNumaOff;
+  return std::isdigit(static_cast<unsigned char>(e[0])) ? std::atoi(e) : kNumaLocal;
+}()};
+
+// Where the host path puts device `device`'s pinned staging and copy threads under the
+// current policy: target node (-1 = none) and the CPUs to bind to (the node's CPUs within
+// this thread's affinity mask; empty = unbound).
+struct Place {
+  int dev_node = -1;  // sysfs numa_node of the device (-1: unknown)
+  int node = -1;      // staging target
+  cpu_set_t cpus;
+  int ncpus = 0;
+  Place() { CPU_ZERO(&cpus); }
+};
+
+Place device_place(int device) {
+  Place P;
+  char bdf[32] = {0};
+  std::string local;
+  if (hipDeviceGetPCIBusId(bdf, sizeof bdf, device) == hipSuccess) {
+    if (pci_numa(bdf, &P.dev_node, &local) != S3H_OK) {
+      P.dev_node = -1;
+      local.clear();
+    }
+  } else {
+    (void)hipGetLastError();
+  }
+  const int mode = g_numa_mode.load();
+  if (mode == kNumaOff) return P;
+  P.node = mode == kNumaLocal ? P.dev_node : mode;
+  if (P.node < 0) return P;
+  std::string list = mode == kNumaLocal ? local : std::string();
+  if (list.empty()) node_cpulist(P.node, &list);
+  cpu_set_t want, mine;
+  if (!parse_cpulist(list, &want) || sched_getaffinity(0, sizeof mine, &mine) != 0) return P;
+  (void)CPU_AND(&P.cpus, &want, &mine);
+  P.ncpus = CPU_COUNT(&P.cpus);
+  return P;
+}
+
+void bind_self(const Place& P) {
+  if (P.ncpus > 0) (void)pthread_setaffinity_np(pthread_self(), sizeof P.cpus, &P.cpus);
+}
+
 // Host threads that fill a pinned staging slot from pageable part memory (one task per part
 // slice).  DMA straight from pageable memory goes through the runtime's bounce buffer and
 // serialises with the host; staging keeps the copy engine fed from pinned memory.
 class CopyPool {
  public:
-  explicit CopyPool(unsigned workers) {
-    for (unsigned i = 0; i < workers; ++i) threads_.emplace_back([this] { loop(); });
+  // Workers bound to place.cpus (the device's node) when that set is non-empty.
+  CopyPool(unsigned workers, const Place& place) : bound_(place.ncpus > 0 ? place.node : -1) {
+    for (unsigned i = 0; i < workers; ++i)
+      threads_.emplace_back([this, place] {
+        bind_self(place);
+        loop();
+      });
   }
+  int bound_node() const { return bound_; }
   ~CopyPool() {
     {
       std::lock_guard<std::mutex> l(m_);
@@ -630,6 +856,7 @@ class CopyPool {
       if (--busy_ == 0) done_.notify_one();
     }
   }
+  int bound_ = -1;
   std::vector<std::thread> threads_;
   std::mutex m_;
   std::condition_variable cv_, done_;
@@ -695,6 +922,7 @@ struct PartSource {
 
 struct HostCtx {
   int device = 0;
+  Place place;  // NUMA node of the pinned staging and CPUs of the copy threads (device_place)
   hipStream_t copy_s = nullptr, hash_s[kHostMaxAlgo] = {};
   hipEvent_t copied[kHostRing] = {}, hashed[kHostRing][kHostMaxAlgo] = {};
   std::unique_ptr<CopyPool> pool;
@@ -729,12 +957,13 @@ struct HostCtx {
     if (e == hipSuccess) *have = want;
     return e;
   }
-  static hipError_t grow_pinned(uint8_t** p, uint64_t* have, uint64_t want) {
+  // pinned host buffers on the context's NUMA node (place.node; < 0: the runtime's choice)
+  hipError_t grow_pinned(uint8_t** p, uint64_t* have, uint64_t want) {
     if (*have >= want) return hipSuccess;
-    if (*p) (void)hipHostFree(*p);
+    pinned_free(*p);
     *p = nullptr;
     *have = 0;
-    const hipError_t e = hipHostMalloc(p, want, hipHostMallocDefault);
+    const hipError_t e = pinned_alloc(reinterpret_cast<void**>(p), want, place.node);
     if (e == hipSuccess) *have = want;
     return e;
   }
@@ -742,7 +971,7 @@ struct HostCtx {
     return grow_dev(reinterpret_cast<uint8_t**>(&d_dig[a]), &dig_bytes[a], bytes);
   }
   CopyPool* ensure_pool(unsigned workers) {  // exactly `workers` threads beside the caller
-    if (!pool || pool->size() != workers) pool.reset(new CopyPool(workers));
+    if (!pool || pool->size() != workers) pool.reset(new CopyPool(workers, place));
     return pool.get();
   }
   // plan[a] for algorithm `algo` with room for n parts (reallocated only to grow)
@@ -776,7 +1005,7 @@ struct HostCtx {
       ring_bytes = 0;
     }
     if (stage_bytes > kHostRing * kFileStageSlot) {
-      (void)hipHostFree(stage);
+      pinned_free(stage);
       stage = nullptr;
       stage_bytes = 0;
     }
@@ -798,8 +1027,8 @@ struct HostCtx {
     for (s3h_plan_s* p : plan)
       if (p) s3h_plan_destroy(p);
     if (ring) (void)hipFree(ring);
-    if (stage) (void)hipHostFree(stage);
-    if (pin) (void)hipHostFree(pin);
+    pinned_free(stage);
+    pinned_free(pin);
   }
 };
 
@@ -819,11 +1048,13 @@ struct HostCtxCache {
     if (busy[device]) {
       auto* p = new HostCtx();
       p->device = device;
+      p->place = device_place(device);
       return p;
     }
     if (!v[device]) {
       v[device] = new HostCtx();
       v[device]->device = device;
+      v[device]->place = device_place(device);
     }
     busy[device] = true;
     return v[device];
@@ -843,6 +1074,16 @@ struct HostCtxCache {
       }
     }
     delete c;
+  }
+  // NUMA record of device's cached context (false: none, or busy in a call right now)
+  bool numa_of(int device, s3h_host_numa_t* info) {
+    std::lock_guard<std::mutex> l(m);
+    if (device < 0 || size_t(device) >= v.size() || !v[device] || busy[device]) return false;
+    const HostCtx* c = v[device];
+    info->staging_node = c->stage ? mem_node(c->stage) : -1;
+    info->threads_node = c->pool ? c->pool->bound_node() : -1;
+    info->copy_threads = c->pool ? int(c->pool->size()) : 0;
+    return true;
   }
   void trim() {
     std::vector<HostCtx*> idle;
@@ -946,7 +1187,7 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
   HIP_TRY(C.ensure_streams());
   hipError_t ce = hipSuccess;
   if (staged) {
-    ce = HostCtx::grow_pinned(&C.stage, &C.stage_bytes, kHostRing * slot_bytes);
+    ce = C.grow_pinned(&C.stage, &C.stage_bytes, kHostRing * slot_bytes);
     if (ce != hipSuccess) {
       (void)hipGetLastError();
       if (!parts) return fail(S3H_ENOMEM, "pinned staging (%llu B): %s",
@@ -1075,12 +1316,14 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
   if (trace_host())
     std::fprintf(stderr,
                  "[s3h host] dev %d: %llu parts, slice %llu B, %s, %llu slices: setup %.2f ms, "
-                 "issue %.2f ms, drain %.2f ms; copy threads %u (%u CPUs over %d devices)\n",
+                 "issue %.2f ms, drain %.2f ms; copy threads %u (%u CPUs over %d devices); "
+                 "numa: device node %d, staging node %d, copy threads on %d CPUs of node %d\n",
                  sh.device, (unsigned long long)n, (unsigned long long)slice,
                  !parts ? "staged (file pread)" : staged ? "staged (pageable)"
                  : direct_pageable ? "pageable per-part" : uniform ? "pinned 2-D" : "pinned per-part",
                  (unsigned long long)k, 1e3 * (t_setup - t_start), 1e3 * (t_issue - t_setup),
-                 1e3 * (wall_s() - t_issue), staged ? threads : 0u, host_cpus(), sh.ndevices);
+                 1e3 * (wall_s() - t_issue), staged ? threads : 0u, host_cpus(), sh.ndevices,
+                 C.place.dev_node, staged ? mem_node(C.stage) : -1, C.place.ncpus, C.place.node);
   return rc;
 }
 
@@ -1160,6 +1403,10 @@ struct s3h_stream_s {
   // slots with the launch base moved by that constant -- no re-sort, no copies.
   std::vector<uint64_t> up_offs[2], up_lens[2];
   bool up_valid[2] = {false, false};
+  uint64_t slot_reuses = 0, slot_refills = 0;  // s3h_stream_stats: how updates found their slots
+  // A call that failed after it started queueing work leaves the messages' host bookkeeping
+  // (carries, totals) ahead of or behind the device state: the object refuses further calls.
+  std::string failed;
   hipStream_t own = nullptr;
   std::vector<uint64_t> total;
   std::vector<uint32_t> carry;
@@ -1179,7 +1426,7 @@ void stream_free(s3h_stream_s* S) {
   for (void* p : {(void*)S->d_state, (void*)S->d_carry, (void*)S->d_head, (void*)S->d_jobs,
                   (void*)S->d_bits, (void*)S->d_stage, (void*)S->d_dig})
     (void)hipFree(p);
-  (void)hipHostFree(S->h_pin);
+  pinned_free(S->h_pin);
   for (hipEvent_t e : {S->staged[0], S->staged[1], S->done})
     if (e) (void)hipEventDestroy(e);
   if (S->own) (void)hipStreamDestroy(S->own);
@@ -1238,9 +1485,11 @@ int stream_plan_base(s3h_stream_s* S, int which, s3h_plan_s* P, const uint8_t* b
     }
     if (same) {  // base + off_now == (base + delta) + off_uploaded, modulo 2^64 like the slots
       *launch_base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(base) + delta);
+      ++S->slot_reuses;
       return S3H_OK;
     }
   }
+  ++S->slot_refills;
   S->up_valid[which] = false;
   S->used_stage = true;
   if (int rc = plan_refill(P, offs.data(), lens.data(), true, S->h_slots[b][which], S->h_order[b][which], s))
@@ -1252,11 +1501,31 @@ int stream_plan_base(s3h_stream_s* S, int which, s3h_plan_s* P, const uint8_t* b
   return S3H_OK;
 }
 
-int stream_update(s3h_stream_s* S, const uint8_t* base, const uint64_t* offsets,
-                  const uint64_t* lengths, hipStream_t s) {
-  const uint64_t n = S->n;
+// Runs one update / final body between stream_begin and stream_end.  stream_end runs on
+// every exit after stream_begin succeeded -- staged[b] and `done` are recorded even when the
+// body failed midway, so a later call never rewrites a staging set a queued copy still reads,
+// nor skips waiting for partly queued work -- and a failed body marks the object failed.
+template <typename Body>
+int stream_call(s3h_stream_s* S, hipStream_t s, Body body) {
+  if (!S->failed.empty())
+    return fail(S3H_EINVAL, "stream object failed earlier (%s): destroy it", S->failed.c_str());
   unsigned b = 0;
   if (int rc = stream_begin(S, s, &b)) return rc;
+  const int rc = body(b);
+  const std::string err = g_err;
+  const int rc_end = stream_end(S, s, b);
+  if (rc) {
+    S->failed = err;
+    g_err = err;
+    return rc;
+  }
+  if (rc_end) S->failed = g_err;
+  return rc_end;
+}
+
+int stream_update_body(s3h_stream_s* S, const uint8_t* base, const uint64_t* offsets,
+                       const uint64_t* lengths, hipStream_t s, unsigned b) {
+  const uint64_t n = S->n;
   s3h::SpliceJob* const h_jobs = S->h_jobs[b];
   bool any_splice = false, any_head = false, any_body = false;
   for (uint64_t i = 0; i < n; ++i) {
@@ -1306,7 +1575,12 @@ int stream_update(s3h_stream_s* S, const uint8_t* base, const uint64_t* offsets,
     if (int rc = stream_plan_base(S, 1, S->body, base, S->offs2, S->lens2, b, s, &bb)) return rc;
     if (int rc = launch_args(S->body, bb, nullptr, S->d_state, 0, S->body->max_blocks, 0, kAppend, nullptr, s)) return rc;
   }
-  return stream_end(S, s, b);
+  return S3H_OK;
+}
+
+int stream_update(s3h_stream_s* S, const uint8_t* base, const uint64_t* offsets,
+                  const uint64_t* lengths, hipStream_t s) {
+  return stream_call(S, s, [&](unsigned b) { return stream_update_body(S, base, offsets, lengths, s, b); });
 }
 
 // The error words of the stream's three plans (head / body / final launches), once `s` has
@@ -1324,10 +1598,8 @@ int stream_check(s3h_stream_s* S, hipStream_t s) {
   return first;
 }
 
-int stream_final(s3h_stream_s* S, uint32_t* d_digests, hipStream_t s) {
+int stream_final_body(s3h_stream_s* S, uint32_t* d_digests, hipStream_t s, unsigned b) {
   const uint64_t n = S->n;
-  unsigned b = 0;
-  if (int rc = stream_begin(S, s, &b)) return rc;
   for (uint64_t i = 0; i < n; ++i) {
     S->offs[i] = 64 * i;
     S->lens[i] = S->carry[i];
@@ -1339,8 +1611,11 @@ int stream_final(s3h_stream_s* S, uint32_t* d_digests, hipStream_t s) {
   // one or two padded blocks per message, starting from the appended state
   if (int rc = launch_args(S->fin, S->d_carry, d_digests, S->d_state, 0, S->fin->max_blocks, 0,
                            s3h::kResume, S->d_bits, s)) return rc;
-  if (int rc = stream_reset(S, s)) return rc;
-  return stream_end(S, s, b);
+  return stream_reset(S, s);
+}
+
+int stream_final(s3h_stream_s* S, uint32_t* d_digests, hipStream_t s) {
+  return stream_call(S, s, [&](unsigned b) { return stream_final_body(S, d_digests, s, b); });
 }
 
 }  // namespace
@@ -1534,6 +1809,14 @@ int s3h_trim(void) {
   return S3H_OK;
 }
 
+int s3h_kernel_policy(int policy, int* previous) {
+  if (policy != S3H_POLICY_THROUGHPUT && policy != S3H_POLICY_EFFICIENCY)
+    return fail(S3H_EINVAL, "kernel policy: unknown policy %d", policy);
+  const int prev = g_kernel_policy.exchange(policy);
+  if (previous) *previous = prev;
+  return S3H_OK;
+}
+
 int s3h_host_threads(int ndevices, int* cpus) {
   if (cpus) *cpus = int(host_cpus());
   return int(host_threads_per_device(ndevices));
@@ -1555,6 +1838,75 @@ int s3h_device_pci_bus_id(int device, char* out, int len) {
   HIP_TRY(hipDeviceGetPCIBusId(out, len, device));
   for (char* c = out; *c; ++c) *c = char(tolower(*c));
   return S3H_OK;
+}
+
+int s3h_pci_numa(const char* pci_bus_id, int* node, char* cpulist, int len, int* usable_cpus) {
+  if (!node) return fail(S3H_EINVAL, "pci numa: null node");
+  *node = -1;
+  if (cpulist && len > 0) cpulist[0] = 0;
+  if (usable_cpus) *usable_cpus = 0;
+  std::string local;
+  if (int rc = pci_numa(pci_bus_id, node, &local)) return rc;
+  if (cpulist && len > 0) std::snprintf(cpulist, size_t(len), "%s", local.c_str());
+  cpu_set_t want, mine, both;
+  if (usable_cpus && parse_cpulist(local, &want) && sched_getaffinity(0, sizeof mine, &mine) == 0) {
+    (void)CPU_AND(&both, &want, &mine);
+    *usable_cpus = CPU_COUNT(&both);
+  }
+  return S3H_OK;
+}
+
+int s3h_device_numa_node(int device, int* node, char* cpulist, int len) {
+  if (!node) return fail(S3H_EINVAL, "device numa: null node");
+  *node = -1;
+  char bdf[32];
+  if (int rc = s3h_device_pci_bus_id(device, bdf, sizeof bdf)) return rc;
+  return s3h_pci_numa(bdf, node, cpulist, len, nullptr);
+}
+
+int s3h_host_numa(int mode, int* previous) {
+  if (mode < kNumaOff || mode >= int(kMaxNumaNodes))
+    return fail(S3H_EINVAL, "host numa: mode %d (want -1 local, -2 off, or a node)", mode);
+  const int prev = g_numa_mode.exchange(mode);
+  if (previous) *previous = prev;
+  if (prev != mode) host_ctx_cache().trim();  // idle contexts re-place on their next call
+  return S3H_OK;
+}
+
+int s3h_host_numa_info(int device, s3h_host_numa_t* info) {
+  if (!info) return fail(S3H_EINVAL, "host numa info: null argument");
+  *info = s3h_host_numa_t{-1, -1, 0, -1, -1, 0};
+  if (int rc = check_device(device)) return rc;
+  const Place P = device_place(device);
+  info->device_node = P.dev_node;
+  info->target_node = P.node;
+  info->bound_cpus = P.ncpus;
+  (void)host_ctx_cache().numa_of(device, info);
+  return S3H_OK;
+}
+
+int s3h_host_alloc(int node, uint64_t bytes, void** out) {
+  if (!out || bytes == 0) return fail(S3H_EINVAL, "host alloc: null out-pointer or 0 bytes");
+  *out = nullptr;
+  if (node < -1 || node >= int(kMaxNumaNodes)) return fail(S3H_EINVAL, "host alloc: bad node %d", node);
+  const hipError_t e = pinned_alloc(out, bytes, node);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(e == hipErrorOutOfMemory ? S3H_ENOMEM : S3H_EHIP, "host alloc (%llu B on node %d): %s",
+                (unsigned long long)bytes, node, hipGetErrorString(e));
+  }
+  return S3H_OK;
+}
+
+int s3h_host_free(void* p) {
+  pinned_free(p);
+  return S3H_OK;
+}
+
+int s3h_mem_node(const void* p, int* node) {
+  if (!p || !node) return fail(S3H_EINVAL, "mem node: null argument");
+  *node = mem_node(p);
+  return *node >= 0 ? S3H_OK : fail(S3H_EINVAL, "mem node: get_mempolicy failed (%s)", std::strerror(errno));
 }
 
 int s3h_plan_create(int device, const uint64_t* offsets, const uint64_t* lengths, uint64_t n,
@@ -1631,6 +1983,26 @@ int s3h_plan_dual_solo(s3h_plan_t P, uint32_t* solo) {
   return S3H_OK;
 }
 
+int s3h_plan_dual_layout(s3h_plan_t P, uint32_t* solo, int* apart) {
+  if (!P) return fail(S3H_EINVAL, "plan dual layout: null plan");
+  if (solo) *solo = P->dual_solo;
+  if (apart) *apart = P->dual_apart ? 1 : 0;
+  return S3H_OK;
+}
+
+int s3h_dual_layout(const uint64_t* lengths, uint64_t n, int cus, uint32_t* solo, int* apart) {
+  if (!lengths || n == 0 || n > kMaxParts || cus <= 0 || !solo || !apart)
+    return fail(S3H_EINVAL, "dual layout: bad argument");
+  std::vector<uint64_t> offs(n, 0);
+  std::vector<s3h::Slot> slots(n);
+  std::vector<uint32_t> order(n);
+  sort_slots(offs.data(), lengths, n, false, slots.data(), order.data());
+  bool a = false;
+  *solo = dual_mixed_solo(slots.data(), n, uint64_t(cus), &a);
+  *apart = a ? 1 : 0;
+  return S3H_OK;
+}
+
 int s3h_plan_info(s3h_plan_t P, uint64_t* n, uint64_t* total_blocks, uint64_t* max_blocks,
                   int* kernel, uint32_t* grid) {
   if (!P) return fail(S3H_EINVAL, "null plan");
@@ -1699,10 +2071,14 @@ static int batch_host_on(const int* algos, int nalgo, const PartSource& src,
     errs[k] = r.err;
   };
   if (nshards == 1) {
-    run(0);
-  } else {
+    run(0);  // the caller's own thread: its affinity is the caller's business
+  } else {   // one thread per device shard, on that device's node (it stages and issues DMAs)
     std::vector<std::thread> pool;
-    for (int k = 0; k < nshards; ++k) pool.emplace_back(run, k);
+    for (int k = 0; k < nshards; ++k)
+      pool.emplace_back([&run, k, place = device_place(shards[k].device)] {
+        bind_self(place);
+        run(k);
+      });
     for (auto& t : pool) t.join();
   }
   for (int k = 0; k < nshards; ++k)
@@ -1963,15 +2339,19 @@ int s3h_stream_create(int device, int algo, uint64_t n, int kernel, s3h_stream_t
     return rc;
   }
   DeviceGuard g(device);
+  const char* what = "chaining state";
   hipError_t e = hipMalloc(&S->d_state, n * 32);
-  if (e == hipSuccess) e = hipMalloc(&S->d_carry, n * 64);
-  if (e == hipSuccess) e = hipMalloc(&S->d_head, n * 64);
-  if (e == hipSuccess) e = hipMalloc(&S->d_jobs, n * sizeof(s3h::SpliceJob));
-  if (e == hipSuccess) e = hipMalloc(&S->d_bits, n * 8);
+  if (e == hipSuccess) e = hipMalloc(&S->d_carry, n * 64), what = "carries";
+  if (e == hipSuccess) e = hipMalloc(&S->d_head, n * 64), what = "head blocks";
+  if (e == hipSuccess) e = hipMalloc(&S->d_jobs, n * sizeof(s3h::SpliceJob)), what = "splice jobs";
+  if (e == hipSuccess) e = hipMalloc(&S->d_bits, n * 8), what = "bit lengths";
   // per message and set: a splice job, two slots, the bit length, two order entries (8-B
   // aligned in this order)
   const size_t per = sizeof(s3h::SpliceJob) + 2 * sizeof(s3h::Slot) + 8 + 2 * 4;
-  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&S->h_pin), 2 * n * per, hipHostMallocDefault);
+  if (e == hipSuccess) {
+    e = pinned_alloc(reinterpret_cast<void**>(&S->h_pin), 2 * n * per, device_place(device).node);
+    what = e == hipSuccess ? "events / stream" : "pinned update staging";
+  }
   for (int b = 0; b < 2 && e == hipSuccess; ++b) {
     uint8_t* pin = S->h_pin + b * n * per;
     S->h_jobs[b] = reinterpret_cast<s3h::SpliceJob*>(pin);
@@ -1991,7 +2371,9 @@ int s3h_stream_create(int device, int algo, uint64_t n, int kernel, s3h_stream_t
       if (!rc && hipEventRecord(ev, S->own) != hipSuccess) rc = fail(S3H_EHIP, "stream: event record failed");
     if (!rc && hipStreamSynchronize(S->own) != hipSuccess) rc = fail(S3H_EHIP, "stream: init failed");
   } else {
-    rc = fail(e == hipErrorOutOfMemory ? S3H_ENOMEM : S3H_EHIP, "stream: %s", hipGetErrorString(e));
+    (void)hipGetLastError();
+    rc = fail(e == hipErrorOutOfMemory ? S3H_ENOMEM : S3H_EHIP, "stream (%llu messages): %s: %s",
+              (unsigned long long)n, what, hipGetErrorString(e));
   }
   if (rc) {
     stream_free(S);
@@ -2062,6 +2444,13 @@ int s3h_stream_status(s3h_stream_t S, void* stream) {
   if (!S) return fail(S3H_EINVAL, "stream status: null stream");
   DeviceGuard g(S->device);
   return stream_check(S, static_cast<hipStream_t>(stream));
+}
+
+int s3h_stream_stats(s3h_stream_t S, uint64_t* slot_reuses, uint64_t* slot_refills) {
+  if (!S) return fail(S3H_EINVAL, "stream stats: null stream");
+  if (slot_reuses) *slot_reuses = S->slot_reuses;
+  if (slot_refills) *slot_refills = S->slot_refills;
+  return S3H_OK;
 }
 
 int s3h_stream_total(s3h_stream_t S, uint64_t i, uint64_t* total) {

@@ -8,10 +8,14 @@
 // shape where it loses (128 x 8 MiB took 0.123 s on the GPU against 0.045 s on 16
 // SHA-NI threads).  S3H_ROUTE_AUTO sends each batch where a measured model says it finishes
 // first:
-//   gpu_s = call_s + max(longest part / chain rate, bytes per device / H2D rate)
-//   cpu_s = max(bytes / (threads x per-thread rate), longest part / per-thread rate)
-// The four rates are measured ONCE per process (route_model, ~0.1 s on the first AUTO call)
-// on this host and device, and s3h_route_model reports them.  AUTO needs a visible GPU
+//   gpu_s = call_s + max(longest part / chain rate, bytes per device / feed rate)
+//           feed = pinned H2D rate, or min(H2D, staging memcpy rate) for pageable parts / files
+//   cpu_s = longest-first makespan of the parts on k = min(n, threads) threads
+//           / (rate(k) / k),  rate(k) = min(k x one-thread rate, all-threads rate)
+// Round 5 replaced a linear "threads x one-thread rate" CPU estimate with the measured
+// all-threads rate: SMT siblings, memory bandwidth and the cgroup quota bend it.
+// The rates are measured ONCE per process (route_model, ~0.1 s on the first AUTO call) on
+// this host and device, and s3h_route_model reports them.  AUTO needs a visible GPU
 // (S3H_ENODEV otherwise): it is a routing choice between two equal-result paths, never a
 // fallback for a missing device.  S3H_ROUTE_GPU (the default everywhere, and the only route
 // the bench metric uses) is s3h_sha256_batch_host / s3h_sha256_file_parts unchanged.
@@ -81,6 +85,39 @@ double seconds_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// `threads` threads at once, each hashing its own 2 MiB buffer three times (memcpy: copying
+// it into a second buffer, the staging fill): aggregate bytes per second, best of 2 rounds.
+// Not 1 thread x threads: SMT siblings, memory bandwidth and the cgroup quota bend the curve.
+double team_rate(unsigned threads, bool copy) {
+  constexpr uint64_t kBuf = 2ull << 20;
+  constexpr int kReps = 3;
+  std::vector<std::vector<uint8_t>> src(threads, std::vector<uint8_t>(kBuf, 0x5a));
+  std::vector<std::vector<uint8_t>> dst(copy ? threads : 0, std::vector<uint8_t>(kBuf, 0));
+  double best = 1e30;
+  for (int round = 0; round < 2; ++round) {
+    std::atomic<unsigned> ready{0};
+    std::atomic<bool> go{false};
+    auto work = [&](unsigned t) {
+      uint32_t h[8];
+      ready.fetch_add(1);
+      while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+      for (int r = 0; r < kReps; ++r) {
+        if (copy) std::memcpy(dst[t].data(), src[t].data(), kBuf);
+        else sha256::sha256(src[t].data(), kBuf, h);
+      }
+    };
+    std::vector<std::thread> pool;
+    for (unsigned t = 1; t < threads; ++t) pool.emplace_back(work, t);
+    while (ready.load() + 1 < threads) std::this_thread::yield();
+    const auto t0 = std::chrono::steady_clock::now();
+    go.store(true, std::memory_order_release);
+    work(0);
+    for (auto& th : pool) th.join();
+    best = std::min(best, seconds_since(t0));
+  }
+  return double(threads) * kBuf * kReps / best;
+}
+
 // Measures the model's rates on this host and device 0 (once per process).
 RouteModel measure_route_model() {
   RouteModel R;
@@ -97,6 +134,8 @@ RouteModel measure_route_model() {
     }
     m.cpu_bytes_per_s = double(buf.size()) / best;
   }
+  m.cpu_all_bytes_per_s = team_rate(unsigned(m.cpu_threads), false);
+  m.staged_bytes_per_s = team_rate(unsigned(m.cpu_threads), true);
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
     R.rc = S3H_ENODEV;
@@ -205,23 +244,56 @@ RouteModel route_model() {
   return R;
 }
 
+// CPU route on k threads: aggregate rate min(k x one-thread rate, all-threads rate); a model
+// without the all-threads rate (recorded before round 5) scales linearly.
+double cpu_rate(const s3h_route_model_t& m, double k) {
+  const double lin = k * m.cpu_bytes_per_s;
+  return m.cpu_all_bytes_per_s > 0 ? std::min(lin, m.cpu_all_bytes_per_s) : lin;
+}
+
+// Makespan, in bytes of one thread, of the parts hashed longest first on k threads (each takes
+// the next part when it frees): exact for up to 4,096 parts, the fluid bound beyond.
+double cpu_makespan_bytes(const uint64_t* lengths, uint64_t n, uint64_t k, uint64_t total,
+                          uint64_t longest) {
+  if (n > 4096 || k >= n) return std::max(double(total) / double(k), double(longest));
+  std::vector<uint64_t> L(lengths, lengths + n);
+  std::sort(L.begin(), L.end(), std::greater<uint64_t>());
+  std::vector<double> load(k, 0.0);  // min-heap of thread loads
+  for (uint64_t x : L) {
+    std::pop_heap(load.begin(), load.end(), std::greater<double>());
+    load.back() += double(x);
+    std::push_heap(load.begin(), load.end(), std::greater<double>());
+  }
+  return *std::max_element(load.begin(), load.end());
+}
+
 // AUTO's decision for a batch (S3H_ROUTE_GPU or S3H_ROUTE_CPU) and both estimates.
 int route_choose(const s3h_route_model_t& m, const uint64_t* lengths, uint64_t n, int ndevices,
-                 double* gpu_s, double* cpu_s) {
+                 int source, double* gpu_s, double* cpu_s) {
   uint64_t total = 0, longest = 0;
   for (uint64_t i = 0; i < n; ++i) {
     total += lengths[i];
     longest = std::max(longest, lengths[i]);
   }
   const int devs = std::max(1, int(std::min<uint64_t>(n, uint64_t(ndevices > 0 ? std::min(ndevices, m.devices) : m.devices))));
+  const double feed = source == S3H_SOURCE_PINNED || !(m.staged_bytes_per_s > 0)
+                          ? m.h2d_bytes_per_s : std::min(m.h2d_bytes_per_s, m.staged_bytes_per_s);
   const double g = m.call_s + std::max(double(longest) / m.chain_bytes_per_s,
-                                       double(total) / devs / m.h2d_bytes_per_s);
-  const double threads = double(std::min<uint64_t>(n, uint64_t(std::max(1, m.cpu_threads))));
-  const double c = std::max(double(total) / (threads * m.cpu_bytes_per_s),
-                            double(longest) / m.cpu_bytes_per_s);
+                                       double(total) / devs / feed);
+  const uint64_t k = std::min<uint64_t>(n, uint64_t(std::max(1, m.cpu_threads)));
+  const double per_thread = cpu_rate(m, double(k)) / double(k);
+  const double c = cpu_makespan_bytes(lengths, n, k, total, longest) / per_thread;
   if (gpu_s) *gpu_s = g;
   if (cpu_s) *cpu_s = c;
   return c < g ? S3H_ROUTE_CPU : S3H_ROUTE_GPU;
+}
+
+// every non-empty part in page-locked host memory (hipPointerGetAttributes): the GPU route
+// DMAs them directly instead of staging
+bool all_pinned_parts(const uint8_t* const* parts, const uint64_t* lengths, uint64_t n) {
+  std::vector<uint64_t> idx(n);
+  std::iota(idx.begin(), idx.end(), 0);
+  return parts && all_pinned(parts, lengths, idx);
 }
 
 bool trace_route() {
@@ -243,10 +315,13 @@ int routed(const uint8_t* const* parts, const char* path, const uint64_t* offset
     const RouteModel& R = route_model();
     if (R.rc) return fail(R.rc, "%s", R.err.c_str());
     double g = 0, c = 0;
-    use = route_choose(R.m, lengths, n, ndevices, &g, &c);
+    const int source = path ? S3H_SOURCE_FILE : all_pinned_parts(parts, lengths, n) ? S3H_SOURCE_PINNED
+                                                                                : S3H_SOURCE_PAGEABLE;
+    use = route_choose(R.m, lengths, n, ndevices, source, &g, &c);
     if (trace_route())
-      std::fprintf(stderr, "[s3h route] %llu parts: gpu %.4f s, cpu %.4f s (%d threads) -> %s\n",
-                   (unsigned long long)n, g, c, R.m.cpu_threads, use == S3H_ROUTE_CPU ? "cpu" : "gpu");
+      std::fprintf(stderr, "[s3h route] %llu parts (%s): gpu %.4f s, cpu %.4f s (%d threads) -> %s\n",
+                   (unsigned long long)n, source == S3H_SOURCE_FILE ? "file" : source ? "pageable" : "pinned",
+                   g, c, R.m.cpu_threads, use == S3H_ROUTE_CPU ? "cpu" : "gpu");
   }
   int rc;
   if (use == S3H_ROUTE_GPU) {
@@ -288,7 +363,17 @@ int s3h_route_estimate(const s3h_route_model_t* m, const uint64_t* lengths, uint
   if (!m || !lengths || n == 0) return fail(S3H_EINVAL, "route estimate: bad argument");
   if (!(m->cpu_bytes_per_s > 0 && m->chain_bytes_per_s > 0 && m->h2d_bytes_per_s > 0))
     return fail(S3H_EINVAL, "route estimate: the model's rates must be positive");
-  return route_choose(*m, lengths, n, ndevices, gpu_s, cpu_s);
+  return route_choose(*m, lengths, n, ndevices, S3H_SOURCE_PINNED, gpu_s, cpu_s);
+}
+
+int s3h_route_estimate_ex(const s3h_route_model_t* m, const uint64_t* lengths, uint64_t n,
+                          int ndevices, int source, double* gpu_s, double* cpu_s) {
+  if (source < S3H_SOURCE_PINNED || source > S3H_SOURCE_FILE)
+    return fail(S3H_EINVAL, "route estimate: unknown source %d", source);
+  if (!m || !lengths || n == 0) return fail(S3H_EINVAL, "route estimate: bad argument");
+  if (!(m->cpu_bytes_per_s > 0 && m->chain_bytes_per_s > 0 && m->h2d_bytes_per_s > 0))
+    return fail(S3H_EINVAL, "route estimate: the model's rates must be positive");
+  return route_choose(*m, lengths, n, ndevices, source, gpu_s, cpu_s);
 }
 
 int s3h_sha256_batch_routed(const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,

@@ -86,11 +86,12 @@ class Plan:
                                   ctypes.byref(k), ctypes.byref(g)))
         groups, solo = ctypes.c_uint32(), ctypes.c_uint32()
         check(lib().s3h_plan_groups(self._h, ctypes.byref(groups), ctypes.byref(solo)))
-        dual_solo = ctypes.c_uint32()
-        check(lib().s3h_plan_dual_solo(self._h, ctypes.byref(dual_solo)))
+        dual_solo, apart = ctypes.c_uint32(), ctypes.c_int()
+        check(lib().s3h_plan_dual_layout(self._h, ctypes.byref(dual_solo), ctypes.byref(apart)))
         return {"n": n.value, "total_blocks": tb.value, "max_blocks": mb.value,
                 "kernel": _native.KERNEL_NAMES[k.value], "grid": g.value,
-                "groups": groups.value, "solo": solo.value, "dual_solo": dual_solo.value}
+                "groups": groups.value, "solo": solo.value, "dual_solo": dual_solo.value,
+                "dual_apart": bool(apart.value)}
 
     def set_clock_probe(self, clocks=None) -> int:
         """Record per-consumer-wave clock counters on later launches (skew kernel only):
@@ -375,6 +376,13 @@ class Stream:
         (s3h_stream_status).  The host forms check by themselves."""
         check(lib().s3h_stream_status(self._h, ctypes.c_void_p(_stream_handle(stream))))
 
+    def stats(self) -> dict:
+        """How updates found their plans' device slots (s3h_stream_stats): reused in place
+        (equal chunks appended at a moved base) or re-sorted and uploaded."""
+        r, f = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib().s3h_stream_stats(self._h, ctypes.byref(r), ctypes.byref(f)))
+        return {"slot_reuses": r.value, "slot_refills": f.value}
+
     def total(self, i: int) -> int:
         t = ctypes.c_uint64()
         check(lib().s3h_stream_total(self._h, i, ctypes.byref(t)))
@@ -452,14 +460,18 @@ def route_model() -> dict:
     return {f: getattr(m, f) for f, _ in m._fields_}
 
 
-def route_estimate(lengths, model: dict, ndevices: int = 0) -> tuple[str, float, float]:
+def route_estimate(lengths, model: dict, ndevices: int = 0, pinned: bool = True,
+                   source: str | None = None) -> tuple[str, float, float]:
     """AUTO's choice for a batch of parts of ``lengths`` under ``model`` (any dict with
-    route_model()'s fields; pure host arithmetic, s3h_route_estimate): (route, gpu_s, cpu_s)."""
+    route_model()'s fields; pure host arithmetic, s3h_route_estimate_ex): (route, gpu_s,
+    cpu_s).  ``source``: "pinned", "pageable" or "file" (default: pinned or pageable by
+    ``pinned``) -- pageable parts and file ranges feed the GPU at min(h2d, staged)."""
     m = _native.RouteModel(**model)
     lens = _u64(lengths)
+    src = _native.SOURCE_IDS[source or ("pinned" if pinned else "pageable")]
     g, c = ctypes.c_double(), ctypes.c_double()
-    r = lib().s3h_route_estimate(ctypes.byref(m), _p64(lens), lens.size, ndevices,
-                                 ctypes.byref(g), ctypes.byref(c))
+    r = lib().s3h_route_estimate_ex(ctypes.byref(m), _p64(lens), lens.size, ndevices, src,
+                                    ctypes.byref(g), ctypes.byref(c))
     if r < 0:
         check(r)
     return _native.ROUTE_NAMES[r], g.value, c.value
@@ -497,6 +509,91 @@ def host_threads(ndevices: int = 1) -> tuple[int, int]:
     cpus = ctypes.c_int(0)
     per = lib().s3h_host_threads(ndevices, ctypes.byref(cpus))
     return per, cpus.value
+
+
+def pci_numa(pci_bus_id: str) -> dict:
+    """sysfs NUMA record of a PCI function (s3h_pci_numa; no GPU needed): node, local CPU
+    list and how many of those CPUs this thread may run on."""
+    node, usable = ctypes.c_int(-1), ctypes.c_int(0)
+    buf = ctypes.create_string_buffer(4096)
+    check(lib().s3h_pci_numa(pci_bus_id.encode(), ctypes.byref(node), buf, len(buf),
+                             ctypes.byref(usable)))
+    return {"node": node.value, "local_cpulist": buf.value.decode(), "usable_cpus": usable.value}
+
+
+def device_numa(device: int) -> dict:
+    """NUMA node and local CPU list of HIP device ``device`` (s3h_device_numa_node)."""
+    node = ctypes.c_int(-1)
+    buf = ctypes.create_string_buffer(4096)
+    check(lib().s3h_device_numa_node(device, ctypes.byref(node), buf, len(buf)))
+    return {"node": node.value, "local_cpulist": buf.value.decode()}
+
+
+def host_numa(mode) -> int:
+    """Set the host path's placement policy -- "local" (each device's node, the default), "off"
+    (runtime placement, unbound threads) or a node number -- and return the previous mode
+    (-1 local, -2 off, else a node): s3h_host_numa."""
+    m = {"local": _native.NUMA_LOCAL, "off": _native.NUMA_OFF}.get(mode, mode)
+    prev = ctypes.c_int(0)
+    check(lib().s3h_host_numa(int(m), ctypes.byref(prev)))
+    return prev.value
+
+
+def host_numa_info(device: int) -> dict:
+    """Where the host path places device ``device``'s staging and copy threads, and what its
+    cached context holds (s3h_host_numa_info)."""
+    info = _native.HostNuma()
+    check(lib().s3h_host_numa_info(device, ctypes.byref(info)))
+    return {f: getattr(info, f) for f, _ in info._fields_}
+
+
+def mem_node(buf) -> int:
+    """NUMA node of the page holding the start of ``buf`` (numpy array, CPU torch tensor or an
+    address): s3h_mem_node."""
+    addr = buf if isinstance(buf, int) else (buf.data_ptr() if hasattr(buf, "data_ptr")
+                                             else _as_bytes(buf).ctypes.data)
+    node = ctypes.c_int(-1)
+    check(lib().s3h_mem_node(ctypes.c_void_p(addr), ctypes.byref(node)))
+    return node.value
+
+
+class PinnedBuffer:
+    """Pinned host memory on a NUMA node (s3h_host_alloc; node -1 = the runtime's placement),
+    e.g. an uploader's read buffer on its device's node.  ``array`` is a uint8 numpy view (it
+    keeps the buffer alive); the memory is freed when the last view is gone or on close()."""
+
+    def __init__(self, nbytes: int, node: int = -1):
+        import weakref
+        p = ctypes.c_void_p()
+        check(lib().s3h_host_alloc(int(node), int(nbytes), ctypes.byref(p)))
+        self.ptr, self.nbytes, self.node = p.value, int(nbytes), int(node)
+        raw = (ctypes.c_uint8 * self.nbytes).from_address(self.ptr)
+        # freed once the ctypes array -- held by this object and by every numpy view -- is gone
+        self._free = weakref.finalize(raw, lib().s3h_host_free, ctypes.c_void_p(self.ptr))
+        self.array = np.frombuffer(raw, dtype=np.uint8)
+
+    def close(self) -> None:
+        """Free now (no view of ``array`` may be used afterwards)."""
+        self.array = None
+        self._free()
+
+
+def dual_layout(lengths, cus: int = 256) -> tuple[int, bool]:
+    """(skew groups of the SHA-256 + MD5 mixed grid, MD5 apart?) for a batch of ``lengths`` on
+    a device of ``cus`` CUs -- the rule a plan applies, on the host (s3h_dual_layout)."""
+    lens = _u64(lengths)
+    solo, apart = ctypes.c_uint32(), ctypes.c_int()
+    check(lib().s3h_dual_layout(_p64(lens), lens.size, cus, ctypes.byref(solo), ctypes.byref(apart)))
+    return solo.value, bool(apart.value)
+
+
+def kernel_policy(policy: str) -> str:
+    """AUTO's kernel policy for plans created afterwards -- "throughput" (default) or
+    "efficiency" (skewp instead of the shared-SIMD skews kernel for 4,097 - 32 x CUs parts:
+    8.6 % slower, 32 % fewer joules per GiB) -- returns the previous one (s3h_kernel_policy)."""
+    prev = ctypes.c_int(0)
+    check(lib().s3h_kernel_policy(_native.POLICY_IDS[policy], ctypes.byref(prev)))
+    return _native.POLICY_NAMES[prev.value]
 
 
 def trim() -> None:

@@ -240,9 +240,12 @@ def test_upload_send_content_md5_gpu(programs, tmp_path, golden, s3_mock, source
 
 
 def _etag_round(args, tmp_path, golden):
-    """--content-md5 upload of the transfer geometry to a correct endpoint and to one that
-    returns a wrong ETag for part 4: the first succeeds and prints the multipart ETag (the
-    compiled reference's md5 golden), the second fails naming part 4, retries included."""
+    """Upload of the transfer geometry to a correct endpoint (--content-md5: the multipart
+    ETag printed equals the compiled reference's md5 golden) and to one that returns a
+    non-MD5 ETag for part 4 -- as S3 does for SSE-KMS / SSE-C parts.  --content-md5 alone
+    accepts it, as the reference does (DoUploadFilePart / DoUploadPart only require an ETag,
+    multipart_upload.cpp:101-105, 138-143); --check-etag (with or without Content-MD5) fails
+    the upload naming part 4, after its retries."""
     want = golden["md5"]["transfer_etag"]
     proc, url, stats = _start_mock()
     try:
@@ -255,10 +258,14 @@ def _etag_round(args, tmp_path, golden):
     proc, url, stats = _start_mock("--wrong-etag-part", "4")
     try:
         r, _ = _upload(args + ["--content-md5", "--retries", "2"], url, tmp_path, golden)
-        assert r.returncode == 1, r.stderr
-        assert "1 of 6 PUTs not 200" in r.stderr and "upload failed: part 4: ETag" in r.stderr, r.stderr
-        assert "upload failed: part" not in r.stderr.replace("upload failed: part 4:", ""), r.stderr
-        assert stats()["wrong_etags"] == 3  # the first attempt and both retries
+        assert r.returncode == 0, r.stderr  # a non-MD5 ETag is an ETag
+        assert stats()["wrong_etags"] == 1
+        for extra in (["--content-md5"], []):
+            r, _ = _upload(args + extra + ["--check-etag", "--retries", "2"], url, tmp_path, golden)
+            assert r.returncode == 1, r.stderr
+            assert "1 of 6 PUTs not 200" in r.stderr and "upload failed: part 4: ETag" in r.stderr, r.stderr
+            assert "upload failed: part" not in r.stderr.replace("upload failed: part 4:", ""), r.stderr
+        assert stats()["wrong_etags"] == 1 + 3 + 3  # each check: the first attempt and 2 retries
     finally:
         proc.kill()
         proc.wait()

@@ -146,6 +146,32 @@ def test_route_estimate_crossover():
         s3.route_estimate([1], {**_MODEL, "chain_bytes_per_s": 0.0})
 
 
+def test_route_estimate_measured_team_rate_and_schedule():
+    """Round 5 model: the CPU route on k threads runs at min(k x one-thread rate, the measured
+    all-threads rate), parts are scheduled longest first (24 equal parts on 16 threads take two
+    part-times, not 1.5), and pageable parts feed the GPU at min(h2d, staged)."""
+    M = {**_MODEL, "cpu_all_bytes_per_s": 16e9, "staged_bytes_per_s": 30e9}
+    P = 8 << 20
+    _, _, c = s3.route_estimate([P] * 4, M)  # 4 threads: 6e9 < 16e9, per thread 1.5e9
+    assert abs(c - P / 1.5e9) < 1e-12
+    _, _, c = s3.route_estimate([P] * 16, M)  # 16 threads share 16e9: 1e9 each
+    assert abs(c - P / 1e9) < 1e-12
+    _, _, c = s3.route_estimate([P] * 24, M)  # longest first: 8 threads hash two parts
+    assert abs(c - 2 * P / 1e9) < 1e-12
+    _, _, c = s3.route_estimate([3 * P, P, P, P], {**M, "cpu_threads": 2})  # 3P | P+P+P
+    assert abs(c - 3 * P / 1.5e9) < 1e-12
+    _, g_pin, _ = s3.route_estimate([P] * 1024, M, source="pinned")
+    _, g_pag, _ = s3.route_estimate([P] * 1024, M, source="pageable")
+    _, g_file, _ = s3.route_estimate([P] * 1024, M, source="file")
+    assert abs(g_pin - (2e-4 + 1024 * P / 50e9)) < 1e-9
+    assert abs(g_pag - (2e-4 + 1024 * P / 30e9)) < 1e-9 and g_file == g_pag
+    # with the linear estimate 1,024 parts looked 1.5x faster on the CPU than they are
+    r_lin, _, c_lin = s3.route_estimate([P] * 1024, _MODEL)
+    r, _, c = s3.route_estimate([P] * 1024, M)
+    assert r_lin == r == "gpu" and abs(c / c_lin - 24e9 / 16e9) < 1e-9
+    assert s3._native.lib().s3h_route_estimate_ex(None, None, 1, 0, 3, None, None) == -1
+
+
 def test_cpu_route_batch_vs_oracle(oracle):
     """S3H_ROUTE_CPU: the lib/hash drop-in on host threads, longest part first, bit-exact vs
     the oracle (empty parts, every tail length)."""

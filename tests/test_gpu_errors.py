@@ -33,10 +33,32 @@ def _probe(lib=None):
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
+PRODUCT = os.path.join(ROOT, "s3client_amd", "lib", "libs3hash.so")
+
+
+def exported_abi(path: str) -> set:
+    """The C-ABI symbols (s3h_*) a library exports (nm -D --defined-only)."""
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True,
+                         check=True).stdout
+    return {l.split()[-1] for l in out.splitlines() if l.split() and l.split()[-1].startswith("s3h_")}
+
+
+def stale_stall_library() -> str:
+    """"" when the forced-fault build exports exactly the product's C-ABI; otherwise why not
+    (a stale prebuilt stall library once lacked a new entry point and failed a GPU run)."""
+    want, got = exported_abi(PRODUCT), exported_abi(STALL)
+    if want == got:
+        return ""
+    return (f"{STALL} is stale -- rebuild it with `make stall`: missing {sorted(want - got)}, "
+            f"extra {sorted(got - want)}")
+
+
 @pytest.mark.gpu
 def test_forced_stall_fails_every_entry_point():
     if not os.path.exists(STALL):  # test-only build, not part of `make all`
         pytest.skip("forced-fault library not built: run `make stall` (__graft_entry__.build() does)")
+    stale = stale_stall_library()
+    assert not stale, stale
     res = _probe(STALL)
     assert res.pop("library").endswith("libs3hash_stall.so")
     assert res.pop("control_1000_parts") == 0  # barrier kernels are unaffected
@@ -53,3 +75,13 @@ def test_product_library_passes_the_same_probe():
     res = _probe()
     assert res.pop("library").endswith(os.path.join("lib", "libs3hash.so"))
     assert all(v == 0 for v in res.values()), {k: v for k, v in res.items() if v != 0}
+
+
+def test_stall_library_exports_the_product_abi():
+    """CPU: the forced-fault library the GPU test loads is built from the same source as the
+    product (Makefile `stall`, rebuilt whenever capi.hip changes) -- same exported C-ABI."""
+    if not (os.path.exists(STALL) and os.path.exists(PRODUCT)):
+        pytest.skip("libraries not built")
+    assert not stale_stall_library(), stale_stall_library()
+    assert len(exported_abi(PRODUCT)) > 50
+

@@ -488,6 +488,42 @@ def test_route_auto_by_batch_shape(torch_cuda, oracle, golden, tmp_path):
     del host, h, views
 
 
+def test_route_auto_near_the_faster_route(torch_cuda):
+    """AUTO is within 10 % of the faster forced route at n = 128 (CPU side of the crossover
+    on the box's 16 SHA-NI threads) and n = 1,024 (GPU side), pinned 8 MiB parts: median of
+    three alternating calls per route (tools/route_sweep.py covers n = 8 ... 1,024, pinned and
+    pageable: profiles/r05_route_sweep.json).  The model's CPU rate is the measured
+    all-threads rate, not threads x one thread."""
+    import time
+    torch = torch_cuda
+    m = s3.route_model()
+    assert 0 < m["cpu_all_bytes_per_s"] <= m["cpu_threads"] * m["cpu_bytes_per_s"] * 1.05, m
+    assert m["staged_bytes_per_s"] > 1e9, m
+    n, L = 1024, 8 * MIB
+    lens = np.full(n, L, dtype=np.uint64)
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(L)
+    dev = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    s3.generate_parts(dev, offs, lens, np.arange(n), 20241008)
+    ref = s3.sha256_batch_device(dev, offs, lens).cpu().numpy().view(np.uint32)
+    buf = s3.PinnedBuffer(n * L, s3.device_numa(0)["node"])
+    torch.from_numpy(buf.array).copy_(dev)
+    del dev
+    _free(torch)
+    for k in (128, 1024):
+        parts = s3.BufferParts(buf.array, offs[:k], lens[:k])
+        t = {r: [] for r in ("gpu", "cpu", "auto")}
+        for rep in range(4):
+            for r in t:
+                t0 = time.perf_counter()
+                d, taken = s3.sha256_batch_routed(parts, ndevices=1, route=r)
+                if rep:
+                    t[r].append(time.perf_counter() - t0)
+                assert np.array_equal(d, ref[:k]), (k, r)
+        med = {r: float(np.median(v)) for r, v in t.items()}
+        assert med["auto"] <= 1.10 * min(med["gpu"], med["cpu"]), (k, med, m)
+    buf.close()
+
+
 def test_dual_digest_host_beyond_one_grid(torch_cuda, oracle):
     """SHA-256 + MD5 from host memory for more parts than any one-grid dual form holds (9,000
     ragged pageable parts: the two plans per slice on the two hash streams) and, in another

@@ -312,20 +312,35 @@ def test_md5_beyond_one_workgroup_per_cu(torch_cuda, oracle):
         assert np.array_equal(s3.md5_batch_host(views, slice_bytes=sl), want), sl
 
 
-@pytest.mark.parametrize("n", [2100, 3000, 6000])
-def test_dual_mixed_grid_ragged(torch_cuda, oracle, n):
+@pytest.mark.parametrize("n,shape,apart", [(2100, "ragged", True), (3000, "ragged", True),
+                                           (6000, "ragged", False), (2100, "between", False)])
+def test_dual_mixed_grid_ragged(torch_cuda, oracle, n, shape, apart):
     """SHA-256 + MD5 of a ragged batch in the skewp-group range (C3-like lengths, scaled):
     the one-grid mixed kernel (the longest parts in skew groups, the rest in skewp groups,
-    slot arrays offset for the second half) vs the oracle, device- and host-resident; equal
-    lengths keep the plain group kernel (dual_solo 0)."""
+    slot arrays offset for the second half) vs the oracle, device- and host-resident, BOTH
+    forms of it: the skew groups' MD5 on workgroups of their own (2,100 / 3,000 parts) and,
+    when that grid would exceed one workgroup per CU (6,000 parts), inside each skew group.
+    "between": one longest part and 2,099 at 0.88 of it -- every part needs a skew group at
+    the apart form's rate ratio, so only the in-group form's smaller ratio gives a mixed grid
+    (F = 1; before the advisor-r4 fix this fell to the plain group kernel).  Equal lengths keep
+    the plain group kernel (dual_solo 0)."""
     rng = np.random.default_rng(n)
-    lens = 5 * 1024 + rng.integers(0, 59 * 1024 + 1, n)
-    lens[:5] = [64 * 1024, 64 * 1024 - 1, 0, 55, 64 * 1024 + 9]
+    if shape == "between":
+        lens = np.full(n, int(64 * 1024 * 0.88), dtype=np.int64)
+        lens[0] = 64 * 1024
+    else:
+        lens = 5 * 1024 + rng.integers(0, 59 * 1024 + 1, n)
+        lens[:5] = [64 * 1024, 64 * 1024 - 1, 0, 55, 64 * 1024 + 9]
     offs = np.concatenate([[0], np.cumsum(lens + 7)[:-1]])
     host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
     with s3.Plan(offs, lens) as plan:
-        solo = plan.info()["dual_solo"]
+        info = plan.info()
+    solo = info["dual_solo"]
     assert 0 < solo and 8 * solo < n
+    assert info["dual_apart"] == apart
+    assert s3.dual_layout(lens, torch_cuda.cuda.get_device_properties(0).multi_processor_count) == (solo, apart)
+    if shape == "between":
+        assert solo == 1
     data = _dev_buffer(torch_cuda, host)
     sha, m5 = s3.sha256_md5_batch_device(data, offs, lens)
     want_sha, want_md5 = oracle.batch(host, offs, lens), oracle.md5_batch(host, offs, lens)

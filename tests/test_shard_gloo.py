@@ -257,3 +257,19 @@ def test_host_resident_multi_views_give_every_device_the_whole_buffer():
             mine = views[k::ndev]
             assert [v.ctypes.data - h.ctypes.data for v in mine] == [j * L for j in range(per)]
             assert all(v.size == L for v in mine)
+
+
+def test_host_resident_multi_views_read_each_devices_own_node_buffer():
+    """With one pinned buffer per NUMA node (round 5), device k reads the buffer on its own
+    node -- e.g. devices 0-3 on node 0 and 4-7 on node 1 -- parts 0..per-1 in order at the
+    buffer's stride, and never a byte of the other node's buffer."""
+    import bench
+    per, L, ndev = 16, 64, 8
+    node_buf = {0: np.arange(per * L, dtype=np.uint8), 1: np.arange(per * L, dtype=np.uint8)}
+    dev_nodes = [0, 0, 0, 0, 1, 1, 1, 1]
+    views = bench.shared_buffer_views([node_buf[dev_nodes[d]] for d in range(ndev)], per, ndev, L)
+    assert len(views) == per * ndev
+    for k in range(ndev):
+        h = node_buf[dev_nodes[k]]
+        mine = views[k::ndev]
+        assert [v.ctypes.data - h.ctypes.data for v in mine] == [j * L for j in range(per)]

@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""AUTO routing across the GPU/CPU crossover.
+
+For n in {8, 32, 64, 128, 256, 512, 1024} parts of 8 MiB (C2 parts 0..n-1, generator G), from
+pinned host memory (on the device's node) and from pageable memory, time
+s3h_sha256_batch_routed with route gpu, cpu and auto, round-robin (`--reps` timed calls each
+after one warm call), and record the model's two estimates and AUTO's choice beside the
+measured medians.  Every digest must equal the device-resident run's.  One JSON object on
+stdout; `auto_over_best` = AUTO's median / min(gpu, cpu) medians (the bar: <= 1.10).
+
+    python3 tools/route_sweep.py [--reps 3] [--ns 8,32,...]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+SEED = 20241008
+MIB = 1 << 20
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--ns", default="8,32,64,128,256,512,1024")
+    ap.add_argument("--sources", default="pinned,pageable")
+    a = ap.parse_args()
+    import torch
+
+    import s3client_amd as s3
+    ns = [int(x) for x in a.ns.split(",")]
+    N, L = max(ns), 8 * MIB
+    lens = np.full(N, L, dtype=np.uint64)
+    offs = np.arange(N, dtype=np.uint64) * np.uint64(L)
+    dev = torch.device("cuda", 0)
+    data = torch.empty(N * L, dtype=torch.uint8, device=dev)
+    s3.generate_parts(data, offs, lens, np.arange(N), SEED)
+    ref = s3.sha256_batch_device(data, offs, lens).cpu().numpy().view(np.uint32)
+    bufs = {}
+    if "pinned" in a.sources:
+        pb = s3.PinnedBuffer(N * L, s3.device_numa(0)["node"])
+        torch.from_numpy(pb.array).copy_(data)
+        bufs["pinned"] = (pb, pb.array)
+    if "pageable" in a.sources:
+        pg = np.empty(N * L, dtype=np.uint8)
+        torch.from_numpy(pg).copy_(data)
+        bufs["pageable"] = (None, pg)
+    del data
+    torch.cuda.empty_cache()
+    t0 = time.perf_counter()
+    model = s3.route_model()
+    out = {"model": model, "model_measure_s": round(time.perf_counter() - t0, 3),
+           "part_bytes": L, "reps": a.reps, "cpu_backend": s3.cpu_backend(),
+           "host_threads": s3.host_threads(1), "rows": [], "mismatches": 0}
+    worst = 0.0
+    for src, (_, arr) in bufs.items():
+        for n in ns:
+            parts = s3.BufferParts(arr, offs[:n], lens[:n])
+            est_route, g_est, c_est = s3.route_estimate(lens[:n], model, pinned=src == "pinned")
+            times = {r: [] for r in ("gpu", "cpu", "auto")}
+            taken = None
+            for k in range(a.reps + 1):
+                for r in times:
+                    t1 = time.perf_counter()
+                    d, tk = s3.sha256_batch_routed(parts, ndevices=1, route=r)
+                    dt = time.perf_counter() - t1
+                    if k:
+                        times[r].append(dt)
+                    if r == "auto":
+                        taken = tk
+                    out["mismatches"] += int(not np.array_equal(d, ref[:n]))
+            med = {r: float(np.median(v)) for r, v in times.items()}
+            ratio = med["auto"] / min(med["gpu"], med["cpu"])
+            worst = max(worst, ratio)
+            out["rows"].append({
+                "source": src, "n": n, "GiB": round(n * L / 2**30, 3),
+                "median_s": {r: round(v, 4) for r, v in med.items()},
+                "all_s": {r: [round(x, 4) for x in v] for r, v in times.items()},
+                "auto_taken": taken, "faster": min(("gpu", "cpu"), key=lambda r: med[r]),
+                "auto_over_best": round(ratio, 4),
+                "model": {"route": est_route, "gpu_s": round(g_est, 4), "cpu_s": round(c_est, 4)}})
+            print(f"[route_sweep] {src} n={n}: gpu {med['gpu']:.4f} cpu {med['cpu']:.4f} "
+                  f"auto {med['auto']:.4f} ({taken}) model gpu {g_est:.4f} cpu {c_est:.4f}",
+                  file=sys.stderr, flush=True)
+    out["worst_auto_over_best"] = round(worst, 4)
+    print(json.dumps(out))
+    return 0 if out["mismatches"] == 0 else 3
+
+
+if __name__ == "__main__":
+    sys.exit(main())
