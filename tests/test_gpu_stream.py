@@ -243,3 +243,42 @@ def test_stream_host_updates_from_buffer_parts(torch_cuda, oracle):
         got = st.final()
     want = np.stack([oracle.sha256(bytes(m)) for m in msgs])
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("chunk", [64 << 10, 1000, 4096 + 17])
+@pytest.mark.parametrize("alternate", [False, True])
+def test_stream_equal_chunks_reuse_device_slots(torch_cuda, oracle, chunk, alternate):
+    """Equal-length device chunks appended at advancing offsets (the usual streamed upload):
+    an update whose lengths equal the ones in the plan's device slots and whose offsets are
+    those plus one constant launches on the same slots with the base moved by that constant
+    (capi.hip stream_plan_base).  Chunk sizes that are a multiple of 64 B (the body plan is
+    reused on every update after the first) and ones that are not (a carry at every
+    boundary: the head plan's slots are reused), on one HIP stream and on two in turn, with
+    two finals; messages start at unrelated byte offsets; every digest vs the oracle, and the
+    slot-reuse counter shows the path was taken."""
+    torch = torch_cuda
+    rng = np.random.default_rng(chunk + alternate)
+    n, rounds, finals = 96, 9, 2
+    span = rounds * chunk
+    starts = (np.arange(n, dtype=np.int64) * (span + 13) + rng.integers(0, 64, n)).astype(np.int64)
+    host = rng.integers(0, 256, int(starts[-1]) + span + 64, dtype=np.uint8)
+    data = torch.from_numpy(host).cuda()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    lens = np.full(n, chunk, dtype=np.uint64)
+    want = oracle.batch(host, starts, np.full(n, span), threads=16)
+    with s3.Stream(n) as st:
+        for f in range(finals):
+            for k in range(rounds):
+                s = streams[k % 2] if alternate else streams[0]
+                st.update_device(data, (starts + k * chunk).astype(np.uint64), lens, s)
+            out = torch.zeros((n, 8), dtype=torch.int32, device="cuda")
+            st.final_device(out, streams[0])
+            torch.cuda.synchronize()
+            st.status(streams[0])
+            got = out.cpu().numpy().view(np.uint32)
+            bad = np.flatnonzero((got != want).any(axis=1))
+            assert bad.size == 0, (f, bad[:8])
+        stats = st.stats()
+    # multiple of 64: body slots reused on every update after the first of each final round;
+    # otherwise the heads (64 B at 64*i in the splice buffer) reuse theirs
+    assert stats["slot_reuses"] >= (finals * (rounds - 1) if chunk % 64 == 0 else rounds - 2), stats
