@@ -1,0 +1,96 @@
+"""Property tests (hypothesis) of the host-side rules that need no GPU: the SHA-256 + MD5
+mixed-grid layout (s3h_dual_layout = capi.hip dual_mixed_solo) and AUTO's route estimate
+(s3h_route_estimate_ex = route.hpp route_choose).  The unit tests pin chosen shapes; these
+check the rules' invariants over random batches."""
+import heapq
+
+import numpy as np
+from hypothesis import given, settings, strategies as st
+
+import s3client_amd as s3
+
+MIB = 1 << 20
+SKEW, SKEWP = 8, 32  # parts per skew group / per skewp group (capi.hip kSkew / kSkewp)
+
+
+def batch(seed, n, shape):
+    """A ragged batch of n parts: C3-like uniform 5-64 MiB, bimodal, or a few giants."""
+    rng = np.random.default_rng(seed)
+    if shape == "uniform":
+        return (5 * MIB + rng.integers(0, 59 * MIB + 1, n)).tolist()
+    if shape == "bimodal":
+        return np.where(rng.random(n) < 0.1, 64 * MIB, rng.integers(MIB, 8 * MIB, n)).tolist()
+    out = rng.integers(0, 4 * MIB, n)
+    out[rng.integers(0, n, 1 + n // 500)] = 64 * MIB
+    return out.tolist()
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.integers(0, 2**32), st.integers(1, 9000), st.sampled_from(["uniform", "bimodal", "giants"]),
+       st.integers(64, 304))
+def test_dual_layout_fits_the_cus(seed, n, shape, cus):
+    """Whatever the batch, a mixed grid (F > 0) exists only for 2,049 - 32 x CUs parts, leaves
+    some parts to the skewp groups, and fits one workgroup per CU in the form it reports."""
+    lengths = batch(seed, n, shape)
+    F, apart = s3.dual_layout(lengths, cus=cus)
+    if F == 0:
+        assert not apart
+        return
+    assert 2048 < n <= SKEWP * cus
+    assert F * SKEW < n
+    wgs = F + -(-(n - F * SKEW) // SKEWP) + (-(-(SKEW * F) // 64) if apart else 0)
+    assert wgs <= cus
+
+
+def test_dual_layout_takes_both_forms_over_c3_shapes():
+    """Over C3-like batches both forms occur: the apart form while it fits, round 3's beyond."""
+    forms = {s3.dual_layout(batch(k, n, "uniform"))[1] for k, n in enumerate(range(2100, 8192, 350))}
+    assert forms == {True, False}
+
+
+@settings(max_examples=30, deadline=None)
+@given(st.integers(1, 8), st.integers(2049, 8192))
+def test_dual_layout_equal_lengths_keep_the_group_kernel(scale, n):
+    assert s3.dual_layout([scale * MIB] * n) == (0, False)
+
+
+MODEL = dict(cpu_bytes_per_s=2.5e9, chain_bytes_per_s=69e6, h2d_bytes_per_s=55e9, call_s=1.5e-4,
+             cpu_threads=16, devices=1, cpu_all_bytes_per_s=37.5e9, staged_bytes_per_s=45e9)
+
+
+def lpt(lengths, k):
+    """Longest-first list schedule on k threads (the makespan route.hpp models)."""
+    loads = [0] * k
+    for x in sorted(lengths, reverse=True):
+        heapq.heapreplace(loads, loads[0] + x)
+    return max(loads)
+
+
+@settings(max_examples=80, deadline=None)
+@given(st.lists(st.integers(0, 64 * MIB), min_size=1, max_size=300),
+       st.integers(1, 64), st.sampled_from(["pinned", "pageable", "file"]))
+def test_route_estimate_matches_its_formula(lengths, threads, source):
+    """The estimates are exactly the documented formulas (include/s3hash.h), and the route is
+    the smaller one."""
+    m = {**MODEL, "cpu_threads": threads}
+    route, g, c = s3.route_estimate(lengths, m, source=source)
+    total, longest, n = sum(lengths), max(lengths), len(lengths)
+    feed = m["h2d_bytes_per_s"] if source == "pinned" else min(m["h2d_bytes_per_s"], m["staged_bytes_per_s"])
+    want_g = m["call_s"] + max(longest / m["chain_bytes_per_s"], total / feed)
+    k = min(n, threads)
+    per_thread = min(k * m["cpu_bytes_per_s"], m["cpu_all_bytes_per_s"]) / k
+    want_c = lpt(lengths, k) / per_thread
+    assert np.isclose(g, want_g, rtol=1e-12, atol=1e-15)
+    assert np.isclose(c, want_c, rtol=1e-12, atol=1e-15)
+    assert route == ("cpu" if c < g else "gpu")
+    # no schedule beats the larger of the longest part and an even split
+    assert c >= max(longest, total / k) / per_thread * (1 - 1e-12)
+
+
+@settings(max_examples=40, deadline=None)
+@given(st.integers(1, 2000), st.integers(1, 16 * MIB))
+def test_route_estimate_is_monotone_in_the_batch(n, part):
+    """More parts of the same size never make either estimate shorter."""
+    _, g1, c1 = s3.route_estimate([part] * n, MODEL)
+    _, g2, c2 = s3.route_estimate([part] * (n + 1), MODEL)
+    assert g2 >= g1 and c2 >= c1
