@@ -747,6 +747,12 @@ __device__ __forceinline__ void flag_wait_ge(uint32_t* f, uint32_t v, bool& aliv
 #else
 #include "sha256_producer_simple.inc"
 #endif
+#if defined(S3H_PROD_ZYV) && !defined(S3H_EXPERIMENT_BUILD)
+// gen_producer.py --zyv / --zyv-plain: byte swap from unaligned in-block loads -- measured
+// slower on the C4 shard (2,246-2,250 vs 2,241 cycles per block at the same board power,
+// profiles/r05_exp_producer_zyv.jsonl), so an experiment only
+#error "the --zyv producer is an experiment (make exp)"
+#endif
 
 // The same for a producer that shares its consumer's SIMD (sha256_skew_shared_kernel): that
 // SIMD issues a second wave's v_add_u32, v_xor/or/and_b32, v_lshrrev_b32 and f32 add/mul
@@ -758,13 +764,63 @@ __device__ __forceinline__ void flag_wait_ge(uint32_t* f, uint32_t v, bool& aliv
 // words as little-endian dwords: the raw loads
 // when every lane of the wave reads dword-aligned parts (`aligned`), one v_perm per word
 // otherwise, and the padded tail block (once per part) byte-swapped back with v_perm.
+#ifdef S3H_PROD_ZYV
+// The block's bytes loaded again at byte offsets 4k+1 (z[k], k = 0..14) and 4j-1 (y[j-1],
+// j = 1..15): unaligned global loads that stay inside the block (bytes 1..60 and 3..62), so each
+// word's four bytes arrive in the lanes its big-endian form needs and the producer assembles
+// them with three v_bitop3 selects instead of doublings (tools/gen_producer.py bswap_zyv).
+// The loads go to the memory pipeline, not the VALU the consumer's round stream shares.
+struct ZYBlock { uint32_t z[15], y[15]; };
+typedef uint32_t v4u32a1 __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t v3u32a1 __attribute__((ext_vector_type(3), aligned(1)));
+typedef const __attribute__((address_space(1))) v4u32a1 gv4u32a1;
+typedef const __attribute__((address_space(1))) v3u32a1 gv3u32a1;
+
+__device__ __forceinline__ void fetch_zy(const uint8_t* p, bool ok, const uint8_t* zero, ZYBlock& r) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(ok ? p : zero);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const v4u32a1 z = *reinterpret_cast<gv4u32a1*>(a + 1 + 16 * i);
+    const v4u32a1 y = *reinterpret_cast<gv4u32a1*>(a + 3 + 16 * i);
+    r.z[4 * i] = z.x; r.z[4 * i + 1] = z.y; r.z[4 * i + 2] = z.z; r.z[4 * i + 3] = z.w;
+    r.y[4 * i] = y.x; r.y[4 * i + 1] = y.y; r.y[4 * i + 2] = y.z; r.y[4 * i + 3] = y.w;
+  }
+  const v3u32a1 z = *reinterpret_cast<gv3u32a1*>(a + 49);
+  const v3u32a1 y = *reinterpret_cast<gv3u32a1*>(a + 51);
+  r.z[12] = z.x; r.z[13] = z.y; r.z[14] = z.z;
+  r.y[12] = y.x; r.y[13] = y.y; r.y[14] = y.z;
+}
+
+// The same values formed from the block's 16 little-endian words (blocks that were not loaded
+// in place: unaligned parts, the padded tail, blocks past the launch).
+__device__ __forceinline__ void zy_from_words(const uint32_t w[16], ZYBlock& r) {
+#pragma unroll
+  for (int k = 0; k < 15; ++k) r.z[k] = (w[k] >> 8) | (w[k + 1] << 24);
+#pragma unroll
+  for (int j = 1; j < 16; ++j) r.y[j - 1] = (w[j - 1] >> 24) | (w[j] << 8);
+}
+#endif
+
 template <int kRow>
-__device__ __forceinline__ void produce_block_simple(const RawBlock& r, uint32_t sel,
+__device__ __forceinline__ void produce_block_simple(const RawBlock& r,
+#ifdef S3H_PROD_ZYV
+                                                     const ZYBlock& zy_loaded,
+#endif
+                                                     uint32_t sel,
                                                      const uint8_t* bp, uint64_t len, uint64_t bits,
                                                      uint64_t blk, uint64_t limit, bool aligned,
                                                      uint4 (*buf)[kRow], uint32_t lane) {
   static_assert(kRow * 16 == 144, "tools/gen_producer.py ROW");
   uint32_t w[16];
+#ifdef S3H_PROD_ZYV
+  ZYBlock zy;
+  const bool in_place = aligned && blk < limit && blk < (len >> 6);
+  if (in_place) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = r.d[j];
+    zy = zy_loaded;
+  } else {
+#endif
   if (blk >= limit) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) w[j] = 0;
@@ -782,6 +838,17 @@ __device__ __forceinline__ void produce_block_simple(const RawBlock& r, uint32_t
 #pragma unroll
     for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
   }
+#ifdef S3H_PROD_ZYV
+    zy_from_words(w, zy);
+  }
+  uint32_t z0 = zy.z[0], z1 = zy.z[1], z2 = zy.z[2], z3 = zy.z[3], z4 = zy.z[4], z5 = zy.z[5],
+           z6 = zy.z[6], z7 = zy.z[7], z8 = zy.z[8], z9 = zy.z[9], z10 = zy.z[10], z11 = zy.z[11],
+           z12 = zy.z[12], z13 = zy.z[13], z14 = zy.z[14];
+  uint32_t y1 = zy.y[0], y2 = zy.y[1], y3 = zy.y[2], y4 = zy.y[3], y5 = zy.y[4], y6 = zy.y[5],
+           y7 = zy.y[6], y8 = zy.y[7], y9 = zy.y[8], y10 = zy.y[9], y11 = zy.y[10], y12 = zy.y[11],
+           y13 = zy.y[12], y14 = zy.y[13], y15 = zy.y[14];
+  const uint32_t mhi = 0xFF000000u, mlo = 0xFFFFFF00u, mmid = 0xFFFF0000u;
+#endif
   typedef __attribute__((address_space(3))) uint4 lds_uint4;
   const uint32_t la = uint32_t(reinterpret_cast<uintptr_t>((lds_uint4*)(&buf[0][lane])));
   uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4], w5 = w[5], w6 = w[6], w7 = w[7],
@@ -801,8 +868,13 @@ __device__ __forceinline__ void produce_block_simple(const RawBlock& r, uint32_t
 #else
   S3H_PROD_SIMPLE_TEMPS
   const uint32_t bsel = 0x00010203u;  // v_perm byte swap (tools/gen_producer.py --perm-bswap only)
+#ifdef S3H_PROD_ZYV
+  asm volatile(S3H_ALIGN8 S3H_PROD_SIMPLE_ASM : S3H_PROD_SIMPLE_OUTS
+               : [la] "v"(la), [bsel] "v"(bsel), S3H_PROD_SIMPLE_INS : "memory");
+#else
   asm volatile(S3H_ALIGN8 S3H_PROD_SIMPLE_ASM : S3H_PROD_SIMPLE_OUTS : [la] "v"(la), [bsel] "v"(bsel)
                : "memory");
+#endif
 #endif
 }
 
@@ -867,22 +939,37 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
     }
     // SIMPLE: every lane's part starts dword-aligned (wave-uniform: the s_bswap decode)
     const bool aligned = SIMPLE && __all(sel[0] == 0x00010203u);
-#define S3H_PRODUCE(RAW, R, BP, BLK, BUF)                                                      \
+#ifdef S3H_PROD_ZYV  // the SIMPLE producer's in-place unaligned loads, double-buffered like RAW
+#define S3H_ZY(ZY) ZY,
+#define S3H_FETCH_ZY(PTR, OK, ZY)                             \
+  do {                                                        \
+    if constexpr (SIMPLE) fetch_zy(PTR, OK, A.zero, ZY);      \
+  } while (0)
+#else
+#define S3H_ZY(ZY)
+#define S3H_FETCH_ZY(PTR, OK, ZY) do {} while (0)
+#endif
+#define S3H_PRODUCE(RAW, ZY, R, BP, BLK, BUF)                                                  \
   do {                                                                                         \
     if constexpr (SIMPLE)                                                                      \
-      produce_block_simple(RAW, sel[R], BP, len[R], bits[R], BLK, A.blk_end, aligned, BUF, part[R]); \
+      produce_block_simple(RAW, S3H_ZY(ZY) sel[R], BP, len[R], bits[R], BLK, A.blk_end, aligned, BUF, part[R]); \
     else                                                                                       \
       produce_block(RAW, sel[R], BP, len[R], bits[R], BLK, A.blk_end, BUF, part[R]);           \
   } while (0)
     constexpr uint64_t kStride = 64ull * kBps;
     RawBlock ra[kItems], rb[kItems];
+#ifdef S3H_PROD_ZYV
+    ZYBlock za[kItems], zb[kItems];
+#endif
 #pragma unroll
     for (uint32_t r = 0; r < kItems; ++r) {
       fetch_full(p[r], bh[r] < fend[r], A.zero, ra[r]);
+      S3H_FETCH_ZY(p[r], bh[r] < fend[r], za[r]);
       fetch_full(p[r] + kStride, bh[r] + kBps < fend[r], A.zero, rb[r]);
+      S3H_FETCH_ZY(p[r] + kStride, bh[r] + kBps < fend[r], zb[r]);
     }
 #pragma unroll
-    for (uint32_t r = 0; r < kItems; ++r) S3H_PRODUCE(ra[r], r, p[r], bh[r], rows(0, h[r]));
+    for (uint32_t r = 0; r < kItems; ++r) S3H_PRODUCE(ra[r], za[r], r, p[r], bh[r], rows(0, h[r]));
     S3H_SYNC_PRODUCED(1u);
     // Step k goes into buffer k & 1, which held step k - 2: FLAGS waits until the consumer
     // has released that step (the barrier of the other mode orders the same thing).
@@ -894,7 +981,8 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
         S3H_PROD_UNROLL
         for (uint32_t r = 0; r < kItems; ++r) {
           fetch_full(p[r] + kStride * (k + 1), bh[r] + kBps * (k + 1) < fend[r], A.zero, ra[r]);
-          S3H_PRODUCE(rb[r], r, p[r] + kStride * k, bh[r] + kBps * k, rows(1, h[r]));
+          S3H_FETCH_ZY(p[r] + kStride * (k + 1), bh[r] + kBps * (k + 1) < fend[r], za[r]);
+          S3H_PRODUCE(rb[r], zb[r], r, p[r] + kStride * k, bh[r] + kBps * k, rows(1, h[r]));
         }
       }
       S3H_SYNC_PRODUCED(uint32_t(k + 1));
@@ -904,7 +992,8 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
         S3H_PROD_UNROLL
         for (uint32_t r = 0; r < kItems; ++r) {
           fetch_full(p[r] + kStride * (k + 2), bh[r] + kBps * (k + 2) < fend[r], A.zero, rb[r]);
-          S3H_PRODUCE(ra[r], r, p[r] + kStride * (k + 1), bh[r] + kBps * (k + 1), rows(0, h[r]));
+          S3H_FETCH_ZY(p[r] + kStride * (k + 2), bh[r] + kBps * (k + 2) < fend[r], zb[r]);
+          S3H_PRODUCE(ra[r], za[r], r, p[r] + kStride * (k + 1), bh[r] + kBps * (k + 1), rows(0, h[r]));
         }
       }
       S3H_SYNC_PRODUCED(uint32_t(k + 2));
@@ -912,6 +1001,8 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
     return;
   }
 #undef S3H_PRODUCE
+#undef S3H_ZY
+#undef S3H_FETCH_ZY
 #undef S3H_SYNC_PRODUCED
   // ------------------------------------------------------------------ consumer
 #ifdef S3H_EXP_LONE_CONSUMER  // experiment: only consumer wave 0 works (wrong digests)

@@ -90,13 +90,28 @@ def test_shared_kernel_keeps_f32_denormals():
 
 @pytest.mark.parametrize("variant", [{"perm": True}, {"lds": True}, {"mulf": False, "merge3": False},
                                      {"perm": True, "mulf": False, "merge3": False},
-                                     {"lds": True, "mulf": False, "merge3": False}])
+                                     {"lds": True, "mulf": False, "merge3": False},
+                                     {"zyv": True}, {"zyv": "plain"}])
 def test_experiment_variants_compute_the_same_schedule(variant):
-    """The v_perm and LDS-pipe byte-swap variants and the doublings-only first version
-    (experiments, profiles/r02_exp_producer_*)."""
+    """The v_perm and LDS-pipe byte-swap variants, the doublings-only first version
+    (experiments, profiles/r02_exp_producer_*) and the byte swap from unaligned in-block loads
+    (--zyv / --zyv-plain, profiles/r05_exp_producer_zyv.jsonl; the simulator forms the loads'
+    values from the block's bytes, gen_producer.zyv_inputs)."""
     rng = random.Random(9)
     for _ in range(10):
         blk = bytes(rng.randrange(256) for _ in range(64))
         le = [int.from_bytes(blk[4 * j:4 * j + 4], "little") for j in range(16)]
         out = gen_producer.simulate(le, **variant)
         assert [out[gen_producer.wk_offset(t)] for t in range(64)] == gen_producer.reference_wk(blk)
+
+
+def test_zyv_loads_stay_inside_the_block():
+    """The --zyv statement's loads (kernel fetch_zy: bytes 1..60 and 3..62 of the block) are the
+    values zyv_inputs forms from the block's own bytes: no byte before or after it is read."""
+    blk = bytes(range(64))
+    le = [int.from_bytes(blk[4 * j:4 * j + 4], "little") for j in range(16)]
+    regs = gen_producer.zyv_inputs(le)
+    for k in range(15):
+        assert regs[gen_producer.ZR[k]] == int.from_bytes(blk[4 * k + 1:4 * k + 5], "little")
+    for j in range(1, 16):
+        assert regs[gen_producer.YR[j - 1]] == int.from_bytes(blk[4 * j - 1:4 * j + 3], "little")

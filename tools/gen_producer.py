@@ -58,6 +58,11 @@ KR = [f"k{i}" for i in range(8)]
 L0B = [f"l0b_{i}" for i in range(16)]   # merge3 only: d14 beside d25 (L0), d15 beside d13 (L1)
 L1B = [f"l1b_{i}" for i in range(4)]
 TEMPS = ["c0", "c1", "c2", "c3", "c4", "c5", "s0", "s1", "s2", "s3"]
+# --zyv: the block's bytes also loaded at byte offsets 4k+1 (ZR[k], k = 0..14) and 4j-1 (YR[j-1],
+# j = 1..15) -- unaligned global loads inside the block -- and three byte-lane masks
+ZR = [f"z{k}" for k in range(15)]
+YR = [f"y{j}" for j in range(1, 16)]
+MASKS = {"mhi": 0xFF000000, "mlo": 0xFFFFFF00, "mmid": 0xFFFF0000}
 # op tuples: ("add", d, a, b) ("xor", d, a, b) ("or", d, a, b) ("and", d, a, imm)
 #            ("shr", d, imm, a) ("xor3", d, a, b, c) ("addk", d, a, imm) ("dsw", src, offset)
 SIMPLE_OPS = {"add", "xor", "or", "and", "shr", "addk", "mulf"}   # bitop3 (xor3) is the partial class
@@ -143,6 +148,41 @@ def bswap(t, perm=False, mulf=False):
              ("or", x, "s0", "s2")])
 
 
+def bswap_zyv(t, plain=False):
+    """--zyv byte swap of word t: the bytes c0 c1 c2 c3 of the word each come in the right lane
+    of some load, so three v_bitop3 selects (a & m | b & ~m) assemble the big-endian word:
+      z_t = load(4t-3) = ZR[t-1] has c0 in bits 24-31, y_t = load(4t-1) = YR[t-1] has c1 in
+      16-23, v_t = load(4t+1) = ZR[t] has c2 in 8-15, and x >> 24 is c3.
+    Word 0 (its z and y would start before the block) keeps the doublings form; word 15 (its v
+    would end past the block) takes c2 from x >> 8.  4 VALU instead of 18 per word."""
+    x = W[t]
+    if t == 0:
+        return bswap(0, mulf=True)
+    if plain:  # --zyv-plain: masks and ors (every instruction simple-class), 7-8 VALU per word
+        v = ("and", "s1", ZR[t], 0xFF00) if t < 15 else None
+        return ([("and", "s0", ZR[t - 1], 0xFF000000), ("and", "s3", YR[t - 1], 0xFF0000),
+                 ("shr", "s2", 24, x)] +
+                ([v] if v else [("shr", "s1", 8, x), ("and", "s1", "s1", 0xFF00)]) +
+                [("or", "s0", "s0", "s3"), ("or", "s1", "s1", "s2"), ("or", x, "s0", "s1")])
+    ops = [("shr", "s2", 24, x)]
+    if t == 15:
+        ops.append(("shr", "s3", 8, x))
+    ops += [("sel", "s0", ZR[t - 1], YR[t - 1], "mhi"),
+            ("sel", "s1", ZR[t] if t < 15 else "s3", "s2", "mlo"),
+            ("sel", x, "s0", "s1", "mmid")]
+    return ops
+
+
+def zyv_inputs(words_le):
+    """The --zyv loads of one block, from its 16 little-endian dwords (what the unaligned loads
+    read; the kernel forms the same values with shifts where it cannot load them)."""
+    w = [x & M32 for x in words_le]
+    regs = {ZR[k]: (w[k] >> 8) | ((w[k + 1] << 24) & M32) for k in range(15)}
+    regs.update({YR[j - 1]: (w[j - 1] >> 24) | ((w[j] << 8) & M32) for j in range(1, 16)})
+    regs.update(MASKS)
+    return regs
+
+
 def expansion(t, merge3=False):
     """W[t] = sigma1(W[t-2]) + W[t-7] + sigma0(W[t-15]) + W[t-16], t >= 16."""
     x, y = W[(t - 15) % 16], W[(t - 2) % 16]
@@ -171,9 +211,11 @@ def merge(a, b):
     return out
 
 
-def block_ops(perm=False, lds=False, mulf=True, merge3=True):
+def block_ops(perm=False, lds=False, mulf=True, merge3=True, zyv=False):
     """lds: byte swap on the LDS pipe (lds_bswap); otherwise in VALU doublings (or v_perm).
-    mulf: part of each left shift by a v_mul_f32 on a denormal bit pattern (mulf_ok)."""
+    mulf: part of each left shift by a v_mul_f32 on a denormal bit pattern (mulf_ok).
+    zyv: byte swap from the block's unaligned loads (bswap_zyv): True with v_bitop3 selects,
+    "plain" with masks and ors."""
     ops = lds_bswap() if lds else []
     for t in range(64):
         if lds and t < 16:
@@ -181,7 +223,8 @@ def block_ops(perm=False, lds=False, mulf=True, merge3=True):
             if t % 2 == 0 and 2 <= t <= 14:
                 ops += merge(lefts(t - 1, mulf, merge3), lefts(t, mulf, merge3))
         else:
-            e = bswap(t, perm, mulf) if t < 16 else expansion(t, merge3)
+            e = ((bswap_zyv(t, zyv == "plain") if zyv else bswap(t, perm, mulf)) if t < 16
+                 else expansion(t, merge3))
             ops += merge(lefts(t - 1, mulf, merge3) if t >= 1 else [], e)
         ops += [("addk", KR[t % 8], W[t % 16], K256[t]), ("dsw", KR[t % 8], wk_offset(t))]
     return ops
@@ -203,6 +246,8 @@ def asm_text(ops):
             lines.append(f"v_lshrrev_b32 %[{op[1]}], {op[2]}, %[{op[3]}]")
         elif k == "xor3":
             lines.append(f"v_bitop3_b32 %[{op[1]}], %[{op[2]}], %[{op[3]}], %[{op[4]}] bitop3:0x96")
+        elif k == "sel":  # (a & m) | (b & ~m); bitop3 index = S0*4 + S1*2 + S2
+            lines.append(f"v_bitop3_b32 %[{op[1]}], %[{op[2]}], %[{op[3]}], %[{op[4]}] bitop3:0xe4")
         elif k == "addk":
             lines.append(f"v_add_u32 %[{op[1]}], 0x{op[3]:08x}, %[{op[2]}]")
         elif k == "mulf":
@@ -225,13 +270,15 @@ def asm_text(ops):
     return lines
 
 
-def simulate(words_le, ops=None, perm=False, lds=False, mulf=True, merge3=True):
+def simulate(words_le, ops=None, perm=False, lds=False, mulf=True, merge3=True, zyv=False):
     """Run the op list on one lane: words_le = 16 little-endian-loaded dwords; returns
     {byte offset: value} of the W+K ds_write_b32s.  LDS is simulated bytewise (initially junk)."""
     regs = {W[i]: words_le[i] & M32 for i in range(16)}
+    if zyv:
+        regs.update(zyv_inputs(words_le))
     out = {}
     mem = bytearray(b"\xa5" * (16 * ROW))
-    for op in ops or block_ops(perm, lds, mulf, merge3):
+    for op in ops or block_ops(perm, lds, mulf, merge3, zyv):
         k = op[0]
         g = lambda r: regs[r]
         if k == "add":
@@ -246,6 +293,8 @@ def simulate(words_le, ops=None, perm=False, lds=False, mulf=True, merge3=True):
             regs[op[1]] = g(op[3]) >> op[2]
         elif k == "xor3":
             regs[op[1]] = g(op[2]) ^ g(op[3]) ^ g(op[4])
+        elif k == "sel":
+            regs[op[1]] = (g(op[2]) & g(op[4])) | (g(op[3]) & ~g(op[4]) & M32)
         elif k == "addk":
             regs[op[1]] = (g(op[2]) + op[3]) & M32
         elif k == "mulf":
@@ -275,8 +324,8 @@ def reference_wk(block: bytes):
     return [(w[t] + K256[t]) & M32 for t in range(64)]
 
 
-def emit_inc(path, perm=False, lds=False, mulf=True, merge3=True):
-    ops = block_ops(perm, lds, mulf, merge3)
+def emit_inc(path, perm=False, lds=False, mulf=True, merge3=True, zyv=False):
+    ops = block_ops(perm, lds, mulf, merge3, zyv)
     body = asm_text(ops)
     n_valu = sum(1 for o in ops if not o[0].startswith(("ds", "wait")))
     n_lds = sum(1 for o in ops if o[0].startswith("ds"))
@@ -298,6 +347,10 @@ def emit_inc(path, perm=False, lds=False, mulf=True, merge3=True):
         f.write("\n".join(hdr + lines) + "\n\n")
         f.write(decl + "\n")
         f.write(f"#define S3H_PROD_SIMPLE_OUTS {outs}\n")
+        if zyv:  # the loads and masks the statement reads (produce_block_simple passes them)
+            ins = ", ".join(f'[{r}] "v"({r})' for r in ZR + YR + list(MASKS))
+            f.write("#define S3H_PROD_ZYV 1\n")
+            f.write(f"#define S3H_PROD_SIMPLE_INS {ins}\n")
 
 
 def emit_rows_inc(path, lds=False):
@@ -341,6 +394,10 @@ def main():
     ap.add_argument("--rows", action="store_true", help="one asm statement per W+K row (experiment)")
     ap.add_argument("--doublings", action="store_true",
                     help="the first version: doublings only, L0/L1 xors (experiment)")
+    ap.add_argument("--zyv", action="store_true",
+                    help="byte swap from unaligned in-block loads (bswap_zyv; experiment)")
+    ap.add_argument("--zyv-plain", action="store_true",
+                    help="the same with masks and ors instead of v_bitop3 selects (experiment)")
     args = ap.parse_args()
     lds = args.lds_bswap
     if args.rows:
@@ -348,8 +405,9 @@ def main():
         print(f"wrote {args.out} (rows)")
         return
     fast = not args.doublings
-    emit_inc(args.out, args.perm_bswap, lds, fast, fast)
-    ops = block_ops(args.perm_bswap, lds, fast, fast)
+    zyv = "plain" if args.zyv_plain else args.zyv
+    emit_inc(args.out, args.perm_bswap, lds, fast, fast, zyv)
+    ops = block_ops(args.perm_bswap, lds, fast, fast, zyv)
     kinds = {}
     for o in ops:
         kinds[o[0]] = kinds.get(o[0], 0) + 1
