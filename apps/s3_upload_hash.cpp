@@ -11,8 +11,12 @@
 // MinIO are absent from this image, so the endpoint is tests/s3_mock_server.py, which checks
 // each body's SHA-256 against x-amz-content-sha256 and verifies the SigV4 signature): each job
 // thread hashes (per-job mode) and PUTs its own parts in order, as upload.cpp:136-140 runs
-// UploadParts, and the timed pass is then hash + upload.  Only UploadPart requests are sent
-// (no CreateMultipartUpload / CompleteMultipartUpload XML), one connection per part.  As in
+// UploadParts, and the timed pass is then hash + upload.  By default only UploadPart requests
+// are sent (to --upload-id), one connection per part; `--multipart` runs the whole
+// UploadFile / UploadData flow (upload.cpp:113-149): CreateMultipartUpload (the upload ID from
+// its XML), the parts, then CompleteMultipartUpload with every part's ETag
+// (multipart_upload.cpp:48-61, 157-176), and checks the object ETag the server returns against
+// the one the GPU MD5s give (with --content-md5 / --check-etag).  As in
 // upload.cpp:94-95 each job sends to an endpoint drawn at random from the --endpoint list, and
 // as DoUploadPart (upload.cpp:55-87) a failed part is sent again while a shared budget of
 // --retries lasts.
@@ -35,7 +39,7 @@
 //
 //   s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory] [--per-job]
 //                  [--cpu] [--verify] [--print-headers] [--send] [--get-verify] [--retries N]
-//                  [--content-md5] [--check-etag] [--route gpu|cpu|auto]
+//                  [--content-md5] [--check-etag] [--multipart] [--route gpu|cpu|auto]
 //                  [--devices N]
 //                  [--repeat R] [--endpoint URL[,URL...] --bucket B --key K --access A
 //                  --secret S --upload-id ID]
@@ -112,14 +116,37 @@ std::string header_value(const std::string& head, const std::string& name) {
   return v;
 }
 
-// One UploadPart request over plain HTTP/1.1 (Connection: close): the signed headers, then
-// the body from memory or, for file parts, by sendfile from the open file (what libcurl's
-// read callback does in WebClient::UploadFile, webclient.cpp:331-355).  Returns the HTTP
-// status, or -1 on a socket error; *etag receives the response's ETag (quotes trimmed), which
-// S3Api::UploadFilePart / UploadPart return (multipart_upload.cpp:101-105, 138-143).
-int put_part(const std::string& host, const std::string& port, const std::string& target,
-             const s3h::sigv4::Map& headers, const uint8_t* mem, int fd, uint64_t off,
-             uint64_t size, std::string* etag) {
+// Text of the first <tag>...</tag> element (case-insensitive, attributes allowed), trimmed:
+// the reference's XMLTag (response_parser.cpp:64-73); "" when absent.
+std::string xml_tag(const std::string& xml, const std::string& tag) {
+  std::string lower(xml), t(tag);
+  for (char& c : lower) c = char(std::tolower(static_cast<unsigned char>(c)));
+  for (char& c : t) c = char(std::tolower(static_cast<unsigned char>(c)));
+  size_t b = lower.find("<" + t);
+  while (b != std::string::npos && lower[b + 1 + t.size()] != '>' && lower[b + 1 + t.size()] != ' ')
+    b = lower.find("<" + t, b + 1);
+  if (b == std::string::npos) return "";
+  b = lower.find('>', b);
+  const size_t e = lower.find("</" + t, b);
+  if (b == std::string::npos || e == std::string::npos) return "";
+  std::string v = xml.substr(b + 1, e - b - 1);
+  while (!v.empty() && std::isspace(static_cast<unsigned char>(v.back()))) v.pop_back();
+  while (!v.empty() && std::isspace(static_cast<unsigned char>(v.front()))) v.erase(0, 1);
+  return v;
+}
+
+// An ETag as CompleteMultipartUpload's XML carries it, its quotes trimmed: literal, &#34; or
+// &quot; (S3Api::CompleteMultipartUpload, multipart_upload.cpp:165-175, handles the first two).
+std::string trim_xml_etag(std::string v) {
+  for (const char* q : {"\"", "&#34;", "&quot;"}) {
+    const size_t n = std::strlen(q);
+    if (v.size() >= 2 * n && v.compare(0, n, q) == 0 && v.compare(v.size() - n, n, q) == 0)
+      return v.substr(n, v.size() - 2 * n);
+  }
+  return v;
+}
+
+int open_conn(const std::string& host, const std::string& port) {
   addrinfo hints{}, *ai = nullptr;
   hints.ai_family = AF_UNSPEC;
   hints.ai_socktype = SOCK_STREAM;
@@ -131,6 +158,61 @@ int put_part(const std::string& host, const std::string& port, const std::string
     if (sock >= 0) close(sock);
     return -1;
   }
+  return sock;
+}
+
+// One POST with a small body (CreateMultipartUpload's empty one, CompleteMultipartUpload's
+// XML) over plain HTTP/1.1, Connection: close.  Returns the HTTP status (-1 on a socket error)
+// and the response body in *out (a chunked body decoded).
+int post_request(const std::string& host, const std::string& port, const std::string& target,
+                 const s3h::sigv4::Map& headers, const std::string& body, std::string* out) {
+  const int sock = open_conn(host, port);
+  if (sock < 0) return -1;
+  std::string req = "POST " + target + " HTTP/1.1\r\n";
+  for (const auto& kv : headers) req += kv.first + ": " + kv.second + "\r\n";
+  req += "Connection: close\r\n\r\n" + body;
+  bool ok = true;
+  for (size_t sent = 0; ok && sent < req.size();) {
+    const ssize_t w = send(sock, req.data() + sent, req.size() - sent, MSG_NOSIGNAL);
+    ok = w > 0;
+    if (ok) sent += size_t(w);
+  }
+  std::string resp;
+  char buf[4096];
+  for (ssize_t r; ok && (r = recv(sock, buf, sizeof buf, 0)) > 0;) resp.append(buf, size_t(r));
+  close(sock);
+  int code = -1;
+  const size_t he = resp.find("\r\n\r\n");
+  if (!ok || he == std::string::npos || std::sscanf(resp.c_str(), "HTTP/%*d.%*d %d", &code) != 1)
+    return -1;
+  std::string head = resp.substr(0, he + 2), b = resp.substr(he + 4);
+  for (char& c : head) c = char(std::tolower(static_cast<unsigned char>(c)));
+  if (head.find("transfer-encoding: chunked") != std::string::npos) {
+    std::string d;
+    for (size_t i = 0; i < b.size();) {
+      const size_t le = b.find("\r\n", i);
+      if (le == std::string::npos) break;
+      const size_t n = std::strtoul(b.c_str() + i, nullptr, 16);
+      if (n == 0) break;
+      d.append(b, le + 2, n);
+      i = le + 2 + n + 2;
+    }
+    b.swap(d);
+  }
+  if (out) *out = b;
+  return code;
+}
+
+// One UploadPart request over plain HTTP/1.1 (Connection: close): the signed headers, then
+// the body from memory or, for file parts, by sendfile from the open file (what libcurl's
+// read callback does in WebClient::UploadFile, webclient.cpp:331-355).  Returns the HTTP
+// status, or -1 on a socket error; *etag receives the response's ETag (quotes trimmed), which
+// S3Api::UploadFilePart / UploadPart return (multipart_upload.cpp:101-105, 138-143).
+int put_part(const std::string& host, const std::string& port, const std::string& target,
+             const s3h::sigv4::Map& headers, const uint8_t* mem, int fd, uint64_t off,
+             uint64_t size, std::string* etag) {
+  const int sock = open_conn(host, port);
+  if (sock < 0) return -1;
   auto send_all = [&](const void* p, size_t n) {
     const char* c = static_cast<const char*>(p);
     while (n > 0) {
@@ -172,17 +254,8 @@ int put_part(const std::string& host, const std::string& port, const std::string
 // socket error or a body of another length.
 int get_range(const std::string& host, const std::string& port, const std::string& target,
               const s3h::sigv4::Map& headers, uint8_t* dst, uint64_t size) {
-  addrinfo hints{}, *ai = nullptr;
-  hints.ai_family = AF_UNSPEC;
-  hints.ai_socktype = SOCK_STREAM;
-  if (getaddrinfo(host.c_str(), port.c_str(), &hints, &ai) != 0 || !ai) return -1;
-  const int sock = socket(ai->ai_family, ai->ai_socktype, ai->ai_protocol);
-  const bool connected = sock >= 0 && connect(sock, ai->ai_addr, ai->ai_addrlen) == 0;
-  freeaddrinfo(ai);
-  if (!connected) {
-    if (sock >= 0) close(sock);
-    return -1;
-  }
+  const int sock = open_conn(host, port);
+  if (sock < 0) return -1;
   std::string req = "GET " + target + " HTTP/1.1\r\n";
   for (const auto& kv : headers) req += kv.first + ": " + kv.second + "\r\n";
   req += "Connection: close\r\n\r\n";
@@ -234,7 +307,7 @@ void usage() {
   std::fprintf(stderr,
                "usage: s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory]\n"
                "       [--per-job] [--cpu] [--verify] [--print-headers] [--send] [--get-verify]\n"
-               "       [--retries N] [--content-md5] [--check-etag] [--route gpu|cpu|auto]\n"
+               "       [--retries N] [--content-md5] [--check-etag] [--multipart] [--route gpu|cpu|auto]\n"
                "       [--endpoint URL[,URL...] --bucket B --key K --access A --secret S --upload-id ID]\n"
                "       [--devices N] [--repeat R]\n");
 }
@@ -255,6 +328,7 @@ int main(int argc, char** argv) {
   // Content-MD5 header already makes the server check the body.
   bool check_etag = false;
   bool get_verify = false;   // after the upload, GET every part back and verify it
+  bool multipart = false;    // --send: CreateMultipartUpload before the parts, Complete after
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -272,6 +346,7 @@ int main(int argc, char** argv) {
     else if (a == "--content-md5") content_md5 = true;
     else if (a == "--check-etag") check_etag = true;
     else if (a == "--get-verify") get_verify = true;
+    else if (a == "--multipart") multipart = true;
     else if (a == "--endpoint") endpoint = next();
     else if (a == "--bucket") bucket = next();
     else if (a == "--key") key = next();
@@ -402,6 +477,7 @@ int main(int argc, char** argv) {
   // DoUploadFilePart / DoUploadPart (multipart_upload.cpp:101-105, 138-143) a 200 without an
   // ETag fails the attempt; with --check-etag the ETag must also equal the part's MD5 from
   // the GPU (S3 returns a plain part's body MD5 as its ETag), else the attempt fails.
+  std::vector<std::string> part_etags(parts.size());  // UploadPart ETags, for --multipart's Complete
   auto put = [&](size_t i, size_t e) {
     const uint8_t* mem = source == "file" ? nullptr : ptrs[i];
     std::string why;
@@ -418,9 +494,13 @@ int main(int argc, char** argv) {
         md5::hash_to_text(&md5w[4 * i], want);
         std::string got(etag);
         for (char& ch : got) ch = char(std::tolower(static_cast<unsigned char>(ch)));
-        if (got == want) return;
+        if (got == want) {
+          part_etags[i] = etag;
+          return;
+        }
         why = "ETag \"" + etag + "\" != the part's MD5 " + want;
       } else if (code == 200) {
+        part_etags[i] = etag;
         return;
       } else {
         why = "HTTP status " + std::to_string(code);
@@ -473,11 +553,62 @@ int main(int argc, char** argv) {
                                            : sha256::payload_hashes(p, l, devices);
     for (size_t k = 0; k < idx.size(); ++k) hex[idx[k]] = h[k];
   };
+  // --multipart: the POSTs around the parts (S3Api::CreateMultipartUpload /
+  // CompleteMultipartUpload, multipart_upload.cpp:157-204), on one endpoint drawn at random as
+  // UploadFile's S3Api is (upload.cpp:124-128).  Each is signed with its body's SHA-256 (the
+  // CPU drop-in: a few hundred bytes) where the reference sends UNSIGNED-PAYLOAD.
+  std::string object_etag, complete_error;
+  auto signed_post = [&](size_t e, const s3h::sigv4::Map& params, const std::string& body,
+                         std::string* out) {
+    uint32_t h[8];
+    sha256::sha256(reinterpret_cast<const uint8_t*>(body.data()), body.size(), h);
+    char t[65];
+    sha256::hash_to_text(h, t);
+    s3h::sigv4::SignConfig c;
+    c.access = access;
+    c.secret = secret;
+    c.endpoint = endpoints[e];
+    c.method = "POST";
+    c.bucket = bucket;
+    c.key = key;
+    c.payloadHash = t;
+    c.parameters = params;
+    c.headers = {{"content-length", std::to_string(body.size())}};
+    const std::string target = "/" + bucket + "/" + key + "?" + s3h::sigv4::UrlEncode(params);
+    return post_request(hostport[e].first, hostport[e].second, target, s3h::sigv4::SignHeaders(c),
+                        body, out);
+  };
+  auto create_upload = [&](size_t e) -> bool {
+    std::string xml;
+    const int code = signed_post(e, {{"uploads", ""}}, "", &xml);
+    upload_id = xml_tag(xml, "UploadId");  // XMLTag(xml, "uploadId"), multipart_upload.cpp:203
+    if (code == 200 && !upload_id.empty()) return true;
+    complete_error = "CreateMultipartUpload: HTTP status " + std::to_string(code) + (upload_id.empty() ? ", no UploadId" : "");
+    return false;
+  };
+  auto complete_upload = [&](size_t e) -> bool {
+    // BuildEndUploadXML (multipart_upload.cpp:48-61): every part's ETag in part-number order
+    std::string xml = "<?xml version=\"1.0\" encoding=\"UTF-8\"?>\n<CompleteMultipartUpload "
+                      "xmlns=\"http://s3.amazonaws.com/doc/2006-03-01/\">\n";
+    for (size_t i = 0; i < parts.size(); ++i)
+      xml += "<Part><ETag>" + part_etags[i] + "</ETag><PartNumber>" +
+             std::to_string(parts[i].number + 1) + "</PartNumber></Part>";
+    xml += "</CompleteMultipartUpload>";
+    std::string resp;
+    const int code = signed_post(e, {{"uploadId", upload_id}}, xml, &resp);
+    object_etag = trim_xml_etag(xml_tag(resp, "ETag"));
+    if (code == 200 && !object_etag.empty()) return true;
+    complete_error = "CompleteMultipartUpload: HTTP status " + std::to_string(code) +
+                     (object_etag.empty() ? ", no ETag" : "") + (resp.empty() ? "" : ": " + resp.substr(0, 200));
+    return false;
+  };
   // One pass over all parts.  Job threads as upload.cpp:136-140 runs them: the CPU drop-in
   // hashes each part of its job (and, with --send, PUTs it right after); on the GPU either one
   // batched call for all parts (then the jobs PUT) or, --per-job, one concurrent batch call per
   // job, each job then PUTting its own parts.
   auto hash_pass = [&]() -> bool {
+    const size_t ep0 = std::uniform_int_distribution<size_t>(0, endpoints.size() - 1)(rng);
+    if (send_parts && multipart && !create_upload(ep0)) return false;
     try {
       if (!cpu_hash_mode && !per_job) {
         std::vector<size_t> all(parts.size());
@@ -503,6 +634,8 @@ int main(int argc, char** argv) {
       std::fprintf(stderr, "%s\n", e.what());
       return false;
     }
+    // the reference's UploadParts throws on a part that failed for good, so no Complete
+    if (send_parts && multipart && !put_failed.load() && !complete_upload(ep0)) return false;
     return true;
   };
   // --repeat R: R passes (an uploader's steady state, buffers cached); the last pass is
@@ -510,7 +643,10 @@ int main(int argc, char** argv) {
   double t0 = 0, first = 0;
   for (int rep = 0; rep < repeat; ++rep) {
     t0 = now();
-    if (!hash_pass()) return 1;
+    if (!hash_pass()) {
+      if (!complete_error.empty()) std::fprintf(stderr, "upload failed: %s\n", complete_error.c_str());
+      return 1;
+    }
     if (rep == 0) first = now() - t0;
   }
   const double dt = now() - t0;
@@ -612,13 +748,27 @@ int main(int argc, char** argv) {
   if (!cpu) std::fprintf(stderr, " (GPU runtime start-up before it: %.3f s)", init_s);
   std::fprintf(stderr, "\n");
   for (const std::string& f : failures) std::fprintf(stderr, "upload failed: %s\n", f.c_str());
+  bool etag_mismatch = false;
+  std::string local_etag;
   if (want_md5) {  // the ETag CompleteMultipartUpload would return, from the GPU MD5s
     try {
-      std::fprintf(stderr, "multipart etag: %s\n", md5::multipart_etag(md5w).c_str());
+      local_etag = md5::multipart_etag(md5w);
+      std::fprintf(stderr, "multipart etag: %s\n", local_etag.c_str());
     } catch (const std::exception& e) {
       std::fprintf(stderr, "multipart etag: %s\n", e.what());
       return 1;
     }
+  }
+  if (send_parts && multipart && !put_failed.load()) {
+    // the object's ETag from the server's CompleteMultipartUpload, checked against the one the
+    // local MD5s give: the server hashed what it received, so equality closes the loop
+    std::string lower(object_etag);
+    for (char& ch : lower) ch = char(std::tolower(static_cast<unsigned char>(ch)));
+    etag_mismatch = want_md5 && lower != local_etag;
+    std::fprintf(stderr, "complete: upload id %s, object etag %s%s\n", upload_id.c_str(),
+                 object_etag.c_str(),
+                 !want_md5 ? "" : etag_mismatch ? " != the local multipart etag (MISMATCH)"
+                                                : " == the local multipart etag");
   }
   if (send_parts && get_verify)
     std::fprintf(stderr, "download verify: %zu parts, %d GETs failed, %llu mismatches (GET %.3f s, %s check %.3f s)\n",
@@ -626,5 +776,5 @@ int main(int argc, char** argv) {
                  t_check);
   munmap(const_cast<uint8_t*>(data), size);
   close(fd);
-  return mismatches || put_failed.load() || get_failed || down_bad ? 1 : 0;
+  return mismatches || put_failed.load() || get_failed || down_bad || etag_mismatch ? 1 : 0;
 }

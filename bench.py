@@ -1038,9 +1038,13 @@ def _dual_on(s3, torch, dev, data, ids, lens, offs, cfg, stream, gd, info, steps
 def c5_loopback(data, offs, lens, gd, nparts: int = 128, jobs: int = 16, repeat: int = 2):
     """BASELINE config 5 without MinIO (absent here): C2 parts 0..nparts-1 written to a file,
     which apps/s3_upload_hash slices as `jobs` x nparts/jobs parts (upload.cpp geometry: the
-    same 8 MiB parts), hashes and PUTs with each digest signed into x-amz-content-sha256 to
-    tests/s3_mock_server.py, which re-hashes every body (hashlib) and verifies every SigV4
-    signature.  Wall-clock of the whole pass (hash + upload; --repeat: the last pass) for the
+    same 8 MiB parts) and uploads as the reference's UploadFile does (upload.cpp:113-149,
+    `--multipart`): CreateMultipartUpload, every part hashed and PUT with its digest signed
+    into x-amz-content-sha256, CompleteMultipartUpload with the parts' ETags -- to
+    tests/s3_mock_server.py, which re-hashes every body (hashlib), verifies every SigV4
+    signature and answers the object's multipart ETag; every pass's object ETag must equal the
+    one hashlib's part MD5s give.  Wall-clock of the whole pass (create + hash + upload +
+    complete; --repeat: the last pass) for the
     GPU batch (one call, and one call per job: merged on the device), the CPU SHA-NI drop-in
     and its scalar loop (lib/hash-like cost), the size-aware route (--route auto: the measured
     model picks the GPU or the CPU drop-in for the batch; `auto_route` says which), plus the
@@ -1054,8 +1058,9 @@ def c5_loopback(data, offs, lens, gd, nparts: int = 128, jobs: int = 16, repeat:
     if not os.path.exists(app) or int(offs[nparts - 1]) != (nparts - 1) * int(lens[0]):
         return {"error": "app not built or parts not contiguous"}
     res = {"workload": f"{nparts} x 8 MiB (C2 parts 0-{nparts - 1}) in one file, {jobs} jobs x "
-                       f"{nparts // jobs} parts; hash + signed UploadPart PUT per part to a "
-                       "loopback mock S3 endpoint that re-hashes bodies and verifies SigV4",
+                       f"{nparts // jobs} parts; CreateMultipartUpload, hash + signed UploadPart "
+                       "PUT per part, CompleteMultipartUpload, to a loopback mock S3 endpoint "
+                       "that re-hashes bodies, verifies SigV4 and answers the object ETag",
            "repeat": repeat, "seconds": {}}
     srv = None
     with tempfile.TemporaryDirectory(dir="/tmp") as td:
@@ -1067,11 +1072,23 @@ def c5_loopback(data, offs, lens, gd, nparts: int = 128, jobs: int = 16, repeat:
                                    stderr=subprocess.DEVNULL, text=True)
             url = f"http://127.0.0.1:{int(srv.stdout.readline())}"
             want = [s3_hex(gd[k]) for k in range(nparts)]
-            for name, extra, env in (("gpu", ["--send"], {}),
-                                     ("gpu_per_job", ["--send", "--per-job"], {}),
-                                     ("cpu_shani", ["--send", "--cpu"], {}),
-                                     ("cpu_scalar", ["--send", "--cpu"], {"S3H_CPU_SCALAR": "1"}),
-                                     ("auto", ["--send", "--route", "auto"], {}),
+            # the object ETag S3 computes: MD5 of the parts' binary MD5s + "-" + count (hashlib)
+            import hashlib
+            from concurrent.futures import ThreadPoolExecutor
+            host = np.fromfile(path, dtype=np.uint8)
+            pb = int(lens[0])
+            with ThreadPoolExecutor(16) as ex:
+                md5s = list(ex.map(lambda k: hashlib.md5(host[k * pb:(k + 1) * pb]).digest(),
+                                   range(nparts)))
+            del host
+            res["object_etag_expected"] = f"{hashlib.md5(b''.join(md5s)).hexdigest()}-{nparts}"
+            etags = {}
+            send = ["--send", "--multipart"]
+            for name, extra, env in (("gpu", send, {}),
+                                     ("gpu_per_job", send + ["--per-job"], {}),
+                                     ("cpu_shani", send + ["--cpu"], {}),
+                                     ("cpu_scalar", send + ["--cpu"], {"S3H_CPU_SCALAR": "1"}),
+                                     ("auto", send + ["--route", "auto"], {}),
                                      ("gpu_hash_only", [], {})):
                 r = subprocess.run([app, "-f", path, "-j", str(jobs), "-n", str(nparts // jobs),
                                     "--endpoint", url, "--repeat", str(repeat), *extra],
@@ -1083,11 +1100,18 @@ def c5_loopback(data, offs, lens, gd, nparts: int = 128, jobs: int = 16, repeat:
                     res["error"] = f"{name}: rc {r.returncode}, digests match {got == want}"
                     break
                 res["seconds"][name] = float(m.group(1))
+                if extra:
+                    me = re.search(r"object etag (\S+)", r.stderr)
+                    etags[name] = me.group(1) if me else None
                 if name == "auto":
                     ra = re.search(r"route auto -> (\w+)", r.stderr)
                     res["auto_route"] = ra.group(1) if ra else None
             with urllib.request.urlopen(url + "/stats", timeout=10) as f:
                 res["server"] = json.loads(f.read())
+            res["object_etags_match"] = bool(etags) and all(
+                e == res["object_etag_expected"] for e in etags.values())
+            if "error" not in res and not res["object_etags_match"]:
+                res["error"] = f"object ETags {etags} != {res['object_etag_expected']}"
         except (OSError, ValueError, subprocess.SubprocessError) as e:
             res["error"] = repr(e)
         finally:

@@ -22,12 +22,22 @@ lib/src/download.cpp:72-103); `--corrupt-get K` flips one byte of the K-th GET's
 uploader's retries, upload.cpp:55-87).  `--wrong-etag-part N` answers part N's PUTs with an
 ETag that is not the body's MD5 (a server-side corruption the uploader's ETag check must
 catch).  `GET /stats` returns JSON counts.  Run: `s3_mock_server.py --port 0 --port-file F` (prints
-the bound port).  Nothing is stored."""
+the bound port).
+
+Multipart uploads (`s3_upload_hash --send --multipart`, the reference's UploadFile flow,
+lib/src/upload.cpp:113-149): `POST ?uploads` (CreateMultipartUpload) answers an
+`<UploadId>`; parts PUT to that upload are recorded with their MD5s; `POST ?uploadId=ID`
+(CompleteMultipartUpload, multipart_upload.cpp:48-61 builds its XML) checks that every listed
+part was received with the listed ETag, in ascending part order (400 InvalidPart /
+InvalidPartOrder otherwise), and answers the object ETag S3 computes -- hex MD5 of the parts'
+binary MD5s + "-" + part count -- quoted as `&quot;`.  Both POSTs are checked like PUTs
+(body SHA-256 against x-amz-content-sha256, SigV4)."""
 import argparse
 import base64
 import hashlib
 import hmac
 import json
+import re
 import threading
 import urllib.parse
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
@@ -72,6 +82,7 @@ class Handler(BaseHTTPRequestHandler):
     corrupt_get = 0
     wrong_etag_part = 0
     objects = {}  # "/bucket/key" -> {part number: bytes}
+    uploads = {}  # upload id -> {"path": "/bucket/key", "parts": {part number: md5 hex}}
     gets = 0
     lock = threading.Lock()
 
@@ -162,17 +173,76 @@ class Handler(BaseHTTPRequestHandler):
                 self.stats["bad_signature"] += 1
             return self._reply(403, b"SignatureDoesNotMatch")
         path, _, query = self.path.partition("?")
-        pn = int(dict(urllib.parse.parse_qsl(query)).get("partNumber", "0"))
+        q = dict(urllib.parse.parse_qsl(query))
+        pn = int(q.get("partNumber", "0"))
         etag = hashlib.md5(body).hexdigest()
         with self.lock:
             self.stats["parts"] += 1
             self.stats["bytes"] += n
             if self.store:
                 self.objects.setdefault(path, {})[pn] = body
+            up = self.uploads.get(q.get("uploadId", ""))
+            if up is not None and up["path"] == path:
+                up["parts"][pn] = etag
             if pn == self.wrong_etag_part:
                 self.stats["wrong_etags"] = self.stats.get("wrong_etags", 0) + 1
                 etag = hashlib.md5(body + b"x").hexdigest()
         self._reply(200, etag=etag)
+
+
+    def _count(self, what):
+        with self.lock:
+            self.stats[what] = self.stats.get(what, 0) + 1
+
+    def do_POST(self):
+        n = int(self.headers.get("content-length", "0"))
+        body = self.rfile.read(n)
+        claimed = self.headers.get("x-amz-content-sha256", "")
+        if len(body) != n or claimed != hashlib.sha256(body).hexdigest():
+            self._count("bad_hash")
+            return self._reply(400, b"XAmzContentSHA256Mismatch")
+        if not self._signature_ok(claimed):
+            self._count("bad_signature")
+            return self._reply(403, b"SignatureDoesNotMatch")
+        path, _, query = self.path.partition("?")
+        q = dict(urllib.parse.parse_qsl(query, keep_blank_values=True))
+        bucket, _, key = path.lstrip("/").partition("/")
+        if "uploads" in q:  # CreateMultipartUpload
+            with self.lock:
+                uid = f"upload-{len(self.uploads) + 1}"
+                self.uploads[uid] = {"path": path, "parts": {}}
+                self.stats["creates"] = self.stats.get("creates", 0) + 1
+            return self._reply(200, (
+                '<?xml version="1.0" encoding="UTF-8"?>\n<InitiateMultipartUploadResult '
+                'xmlns="http://s3.amazonaws.com/doc/2006-03-01/">'
+                f"<Bucket>{bucket}</Bucket><Key>{key}</Key><UploadId>{uid}</UploadId>"
+                "</InitiateMultipartUploadResult>").encode())
+        uid = q.get("uploadId")
+        with self.lock:
+            up = self.uploads.get(uid)
+        if up is None or up["path"] != path:
+            self._count("bad_completes")
+            return self._reply(404, b"NoSuchUpload")
+        listed = re.findall(r"<Part>\s*<ETag>(.*?)</ETag>\s*<PartNumber>(\d+)</PartNumber>\s*</Part>",
+                            body.decode(errors="replace"), re.S)
+        numbers = [int(pn) for _, pn in listed]
+        if not listed or numbers != sorted(set(numbers)):
+            self._count("bad_completes")
+            return self._reply(400, b"InvalidPartOrder")
+        md5s = []
+        for etag, pn in listed:
+            etag = etag.strip().replace("&quot;", "").replace("&#34;", "").strip('"').lower()
+            if up["parts"].get(int(pn)) != etag:
+                self._count("bad_completes")
+                return self._reply(400, b"InvalidPart")
+            md5s.append(bytes.fromhex(etag))
+        final = f"{hashlib.md5(b''.join(md5s)).hexdigest()}-{len(md5s)}"
+        self._count("completes")
+        self._reply(200, (
+            '<?xml version="1.0" encoding="UTF-8"?>\n<CompleteMultipartUploadResult '
+            'xmlns="http://s3.amazonaws.com/doc/2006-03-01/">'
+            f"<Location>http://127.0.0.1{path}</Location><Bucket>{bucket}</Bucket><Key>{key}</Key>"
+            f"<ETag>&quot;{final}&quot;</ETag></CompleteMultipartUploadResult>").encode())
 
 
 def main():

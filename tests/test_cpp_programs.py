@@ -332,3 +332,49 @@ def test_upload_then_download_verify_gpu(programs, tmp_path, golden):
     finally:
         proc.kill()
         proc.wait()
+
+
+def _multipart_round(args, tmp_path, golden):
+    """--multipart: the reference's whole UploadFile flow (upload.cpp:113-149) against the
+    verifying endpoint -- CreateMultipartUpload (the upload ID from its XML), the six parts
+    PUT to that upload, CompleteMultipartUpload listing every part's ETag in order
+    (multipart_upload.cpp:48-61) -- and the object ETag the server computes from the MD5s of
+    what it received equals the local multipart ETag from the part MD5s (and the compiled
+    reference's md5 golden for this file).  Without MD5s the object ETag is reported only; a
+    part the server answered with a wrong ETag makes Complete fail (InvalidPart)."""
+    want = golden["md5"]["transfer_etag"]
+    proc, url, stats = _start_mock()
+    try:
+        r, _ = _upload(args + ["--multipart", "--content-md5", "--repeat", "2"], url, tmp_path, golden)
+        assert r.returncode == 0, r.stderr
+        assert f"object etag {want} == the local multipart etag" in r.stderr, r.stderr
+        assert "upload id upload-2" in r.stderr, r.stderr  # a fresh upload per pass
+        r, _ = _upload(args + ["--multipart"], url, tmp_path, golden)
+        assert r.returncode == 0 and f"object etag {want}" in r.stderr, r.stderr
+        s = stats()
+        assert s["creates"] == 3 and s["completes"] == 3 and s.get("bad_completes", 0) == 0, s
+        assert s["parts"] == 18 and s["bad_hash"] == 0 and s["bad_signature"] == 0, s
+        r, _ = _upload(args + ["--multipart", "--secret", "WRONG"], url, tmp_path, golden)
+        assert r.returncode == 1 and "CreateMultipartUpload: HTTP status 403" in r.stderr, r.stderr
+    finally:
+        proc.kill()
+        proc.wait()
+    proc, url, stats = _start_mock("--wrong-etag-part", "4")
+    try:
+        r, _ = _upload(args + ["--multipart"], url, tmp_path, golden)
+        assert r.returncode == 1 and "CompleteMultipartUpload: HTTP status 400" in r.stderr, r.stderr
+        assert "InvalidPart" in r.stderr and stats()["bad_completes"] == 1
+    finally:
+        proc.kill()
+        proc.wait()
+
+
+def test_upload_multipart_flow_cpu(programs, tmp_path, golden):
+    _multipart_round(["--cpu"], tmp_path, golden)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("source", ["file", "memory"])
+def test_upload_multipart_flow_gpu(programs, tmp_path, golden, source):
+    """The same with SHA-256 and MD5 from the GPU's dual pass."""
+    _multipart_round(["--source", source], tmp_path, golden)
