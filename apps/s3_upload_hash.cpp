@@ -49,6 +49,7 @@
 #include <sys/sendfile.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
+#include <sys/time.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -158,6 +159,10 @@ int open_conn(const std::string& host, const std::string& port) {
     if (sock >= 0) close(sock);
     return -1;
   }
+  // a stalled endpoint fails the request (and its retries) instead of hanging the upload
+  const timeval tv{120, 0};
+  (void)setsockopt(sock, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+  (void)setsockopt(sock, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
   return sock;
 }
 
