@@ -73,6 +73,9 @@ def parse(argv=None):
                          "appended chunk by chunk through s3h_stream_*; dual / host-dual: "
                          "SHA-256 + MD5 of every part in one pass (none of these is the metric)")
     ap.add_argument("--chunk-bytes", type=int, default=MIB, help="stream mode: bytes per append")
+    ap.add_argument("--stream-source", default="device", choices=["device", "pinned", "pageable"],
+                    help="stream mode: chunks already in HBM (update_device) or in host memory "
+                         "(update: pinned or pageable buffer, H2D included)")
     ap.add_argument("--no-host-resident", action="store_true",
                     help="skip the H2D-inclusive sub-measurement of the default C2 line")
     ap.add_argument("--no-c4", action="store_true",
@@ -1373,12 +1376,26 @@ def stream_mode(args, s3, torch, data, ids, lens, offs, rank, name, stream):
     out = torch.zeros((n, st.words), dtype=torch.int32, device=data.device)
     cb = args.chunk_bytes
     nupd = int((int(lens.max()) + cb - 1) // cb)
+    src = args.stream_source
+    host = None
+    if src != "device":  # the parts in host memory: each update copies its chunks (H2D included)
+        end = int(offs[-1] + lens[-1])
+        host = torch.empty(end, dtype=torch.uint8, pin_memory=(src == "pinned"))
+        host.copy_(data[:end])
+        host_out = np.zeros((n, st.words), dtype=np.uint32)
 
     def one_object_pass():
         for k in range(nupd):
             lk = np.minimum(np.maximum(lens.astype(np.int64) - k * cb, 0), cb).astype(np.uint64)
-            st.update_device(data, offs + np.uint64(k * cb), lk, stream)
-        st.final_device(out, stream)
+            if host is None:
+                st.update_device(data, offs + np.uint64(k * cb), lk, stream)
+            else:
+                st.update(s3.BufferParts(host, offs + np.uint64(k * cb), lk))
+        if host is None:
+            st.final_device(out, stream)
+        else:
+            host_out[:] = st.final()
+            out.copy_(torch.from_numpy(host_out.view(np.int32)))
 
     for _ in range(args.warmup):
         one_object_pass()
@@ -1400,7 +1417,7 @@ def stream_mode(args, s3, torch, data, ids, lens, offs, rank, name, stream):
                           "value": round(float(lens.sum()) / 2**30 / wall, 3), "unit": "GiB/s",
                           "n_gpus": 1, "steps": args.steps,
                           "config": {"workload": name, "objects": n, "chunk_bytes": cb,
-                                     "updates_per_object": nupd},
+                                     "updates_per_object": nupd, "chunks_from": src},
                           "parity": {"fixtures_checked": len(checked), "mismatches": int(bad)},
                           "ms_per_pass": round(wall * 1e3, 2)}))
     st.close()

@@ -350,8 +350,12 @@ int s3h_stream_create(int device, int algo, uint64_t n, int kernel, s3h_stream_t
 int s3h_stream_update_device(s3h_stream_t s, const void *d_base, const uint64_t *offsets,
                              const uint64_t *lengths, void *stream);
 int s3h_stream_final_device(s3h_stream_t s, uint32_t *d_digests, void *stream);
-/* Host-memory forms (blocking; they check the launches' device error word like
- * s3h_plan_status): chunks[i] may be null when lengths[i] == 0. */
+/* Host-memory forms: chunks[i] may be null when lengths[i] == 0.  update_host returns once
+ * the chunks have been copied out of the caller's memory (they may be reused on return); its
+ * hash runs on the device while the caller prepares the next update, whose copy overlaps it.
+ * Page-locked chunks are DMA'd directly; pageable ones go through pinned pieces filled by copy
+ * threads on the device's NUMA node.  final_host waits for every update and checks the
+ * launches' device error words like s3h_plan_status (a fault of any update fails it). */
 int s3h_stream_update_host(s3h_stream_t s, const uint8_t *const *chunks, const uint64_t *lengths);
 int s3h_stream_final_host(s3h_stream_t s, uint32_t *digests);
 /* Device forms: waits for `stream` and reports (and clears) a fault of any update / final

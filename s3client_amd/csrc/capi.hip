@@ -876,6 +876,15 @@ class CopyPool {
 // kKeepRingBytes is freed when the call returns, so a cached context holds at most
 // kKeepRingBytes of HBM plus its staging; s3h_trim() frees idle contexts.
 constexpr int kHostRing = 3;
+// Host-form stream updates (s3h_stream_update_host): pinned host pieces of the staged copy
+// (two, filled alternately); pinned ragged chunks DMA'd one by one only up to this many per
+// update (more: staged -- a DMA per 1 MiB chunk costs more than a memcpy); updates above
+// 2 x kStreamSubBytes are split into sub-updates of ~kStreamSubBytes (>= kStreamSubMin of
+// every chunk) whose copies overlap the hash of the one before.
+constexpr uint64_t kStreamPiece = 64ull << 20;
+constexpr uint64_t kStreamDmaChunks = 64;
+constexpr uint64_t kStreamSubBytes = 128ull << 20;
+constexpr uint64_t kStreamSubMin = 64ull << 10;
 constexpr int kHostMaxAlgo = 2;
 constexpr uint64_t kStageSlot = 32ull << 20;     // pinned staging bytes per ring slot
 constexpr uint64_t kKeepRingBytes = 1ull << 30;  // largest HBM ring kept between calls
@@ -1380,8 +1389,20 @@ struct s3h_stream_s {
   uint8_t* d_head = nullptr;
   s3h::SpliceJob* d_jobs = nullptr;
   uint64_t* d_bits = nullptr;
-  uint8_t* d_stage = nullptr;  // host-form updates: chunks staged here
-  uint64_t stage_cap = 0;
+  // Host-form updates (s3h_stream_update_host): each update's chunks are packed at 64-B
+  // aligned offsets into device staging set hb -- two sets, so update k+1's copy (on copy_s)
+  // overlaps update k's hash (on own) -- by DMA straight from pinned chunks, or, for pageable
+  // chunks, through pinned host pieces (two, kStreamPiece bytes) that copy threads on the
+  // device's NUMA node fill while the previous piece's DMA runs.
+  uint8_t* d_hs[2] = {nullptr, nullptr};
+  uint64_t d_hs_cap[2] = {0, 0};
+  uint8_t* h_piece[2] = {nullptr, nullptr};
+  uint64_t h_piece_cap = 0;
+  hipEvent_t hs_copied[2] = {nullptr, nullptr}, hs_hashed[2] = {nullptr, nullptr};
+  hipEvent_t piece_copied[2] = {nullptr, nullptr};
+  hipStream_t copy_s = nullptr;
+  unsigned hs_set = 0;
+  std::unique_ptr<CopyPool> pool;
   uint32_t* d_dig = nullptr;   // host-form final
   // Pinned staging of an update / final in two sets used alternately: set b is rewritten
   // only once the call that used it two calls ago has completed (staged[b]), so the host
@@ -1418,18 +1439,23 @@ namespace {
 void stream_free(s3h_stream_s* S) {
   DeviceGuard g(S->device);
   if (S->own) (void)hipStreamSynchronize(S->own);
+  if (S->copy_s) (void)hipStreamSynchronize(S->copy_s);
   for (hipEvent_t e : {S->staged[0], S->staged[1], S->done})
     if (e) (void)hipEventSynchronize(e);
   s3h_plan_destroy(S->head);
   s3h_plan_destroy(S->body);
   s3h_plan_destroy(S->fin);
   for (void* p : {(void*)S->d_state, (void*)S->d_carry, (void*)S->d_head, (void*)S->d_jobs,
-                  (void*)S->d_bits, (void*)S->d_stage, (void*)S->d_dig})
+                  (void*)S->d_bits, (void*)S->d_hs[0], (void*)S->d_hs[1], (void*)S->d_dig})
     (void)hipFree(p);
   pinned_free(S->h_pin);
-  for (hipEvent_t e : {S->staged[0], S->staged[1], S->done})
+  pinned_free(S->h_piece[0]);
+  pinned_free(S->h_piece[1]);
+  for (hipEvent_t e : {S->staged[0], S->staged[1], S->done, S->hs_copied[0], S->hs_copied[1],
+                       S->hs_hashed[0], S->hs_hashed[1], S->piece_copied[0], S->piece_copied[1]})
     if (e) (void)hipEventDestroy(e);
   if (S->own) (void)hipStreamDestroy(S->own);
+  if (S->copy_s) (void)hipStreamDestroy(S->copy_s);
   delete S;
 }
 
@@ -2400,32 +2426,130 @@ int s3h_stream_final_device(s3h_stream_t S, uint32_t* d_digests, void* stream) {
   return stream_final(S, d_digests, static_cast<hipStream_t>(stream));
 }
 
-int s3h_stream_update_host(s3h_stream_t S, const uint8_t* const* chunks, const uint64_t* lengths) {
-  if (!S || !chunks || !lengths) return fail(S3H_EINVAL, "stream update: null argument");
-  std::vector<uint64_t> offs(S->n);
-  uint64_t sum = 0;
-  for (uint64_t i = 0; i < S->n; ++i) {
-    if (lengths[i] && !chunks[i]) return fail(S3H_EINVAL, "stream update: chunk %llu is null", (unsigned long long)i);
+namespace {
+
+// One host-form update of at most a few hundred MiB (s3h_stream_update_host splits larger
+// ones): the chunks are packed at 64-B aligned offsets into device staging set b and hashed on
+// `own` once the set's copy has landed; the copy of the next update overlaps this hash.
+//   pinned chunks of equal length at a constant stride -> one 2-D DMA;
+//   a few other pinned chunks                          -> one DMA each;
+//   anything else (pageable, or many ragged pinned)    -> copy threads fill pinned pieces,
+//                                                         one DMA per piece.
+// Returns once the chunks may be released by the caller.
+int stream_host_update_one(s3h_stream_s* S, const uint8_t* const* chunks, const uint64_t* lengths) {
+  const uint64_t n = S->n;
+  std::vector<uint64_t> offs(n);
+  uint64_t sum = 0, L0 = 0;
+  bool equal = true;
+  for (uint64_t i = 0; i < n; ++i) {
     offs[i] = sum;
     sum += (lengths[i] + 63) & ~uint64_t(63);
+    if (i == 0) L0 = lengths[0];
+    equal = equal && lengths[i] == L0;
+  }
+  const unsigned b = S->hs_set;
+  S->hs_set ^= 1u;
+  if (sum > S->d_hs_cap[b]) {
+    HIP_TRY(hipEventSynchronize(S->hs_hashed[b]));  // the set's last hash has read it
+    (void)hipFree(S->d_hs[b]);
+    S->d_hs[b] = nullptr;
+    S->d_hs_cap[b] = 0;
+    HIP_TRY(hipMalloc(&S->d_hs[b], sum));
+    S->d_hs_cap[b] = sum;
+  }
+  bool wait_copy = false;  // the DMA reads the caller's memory: wait for it before returning
+  if (sum) {
+    // set b is rewritten only after the hash that read it (two updates ago) has run
+    HIP_TRY(hipStreamWaitEvent(S->copy_s, S->hs_hashed[b], 0));
+    std::vector<uint64_t> all(n);
+    std::iota(all.begin(), all.end(), uint64_t(0));
+    const bool pinned = all_pinned(chunks, lengths, all);
+    const uint64_t stride = n > 1 && chunks[1] >= chunks[0] ? uint64_t(chunks[1] - chunks[0]) : 0;
+    bool strided = pinned && equal && L0 > 0 && n > 1 && stride >= L0;
+    for (uint64_t i = 1; strided && i < n; ++i) strided = uint64_t(chunks[i] - chunks[0]) == i * stride;
+    if (strided) {
+      HIP_TRY(hipMemcpy2DAsync(S->d_hs[b], (L0 + 63) & ~uint64_t(63), chunks[0], stride, L0, n,
+                               hipMemcpyHostToDevice, S->copy_s));
+      wait_copy = true;
+    } else if (pinned && n <= kStreamDmaChunks) {
+      for (uint64_t i = 0; i < n; ++i)
+        if (lengths[i])
+          HIP_TRY(hipMemcpyAsync(S->d_hs[b] + offs[i], chunks[i], lengths[i], hipMemcpyHostToDevice, S->copy_s));
+      wait_copy = true;
+    } else {
+      // copy threads fill pinned piece q while piece q^1's DMA runs
+      const uint64_t P = std::min<uint64_t>(sum, kStreamPiece);
+      if (P > S->h_piece_cap) {
+        for (hipEvent_t e : {S->piece_copied[0], S->piece_copied[1]}) HIP_TRY(hipEventSynchronize(e));
+        pinned_free(S->h_piece[0]);
+        pinned_free(S->h_piece[1]);
+        S->h_piece[0] = S->h_piece[1] = nullptr;
+        S->h_piece_cap = 0;
+        const int node = device_place(S->device).node;
+        for (uint8_t*& h : S->h_piece)
+          HIP_TRY(pinned_alloc(reinterpret_cast<void**>(&h), P, node));
+        S->h_piece_cap = P;
+      }
+      if (!S->pool) S->pool.reset(new CopyPool(host_threads_per_device(1) - 1, device_place(S->device)));
+      for (uint64_t lo = 0, q = 0; lo < sum; lo += P, q ^= 1u) {
+        const uint64_t hi = std::min(sum, lo + P);
+        HIP_TRY(hipEventSynchronize(S->piece_copied[q]));  // its previous DMA has read it
+        // the chunks overlapping [lo, hi) of the packed layout (offs ascending)
+        const uint64_t i0 = uint64_t(std::upper_bound(offs.begin(), offs.end(), lo) - offs.begin()) - 1;
+        const uint64_t i1 = uint64_t(std::lower_bound(offs.begin(), offs.end(), hi) - offs.begin());
+        uint8_t* const dst = S->h_piece[q];
+        S->pool->run(i1 - i0, [&](uint64_t k) {
+          const uint64_t i = i0 + k, a = std::max(offs[i], lo), e = std::min(offs[i] + lengths[i], hi);
+          if (e > a) std::memcpy(dst + (a - lo), chunks[i] + (a - offs[i]), e - a);
+        });
+        HIP_TRY(hipMemcpyAsync(S->d_hs[b] + lo, dst, hi - lo, hipMemcpyHostToDevice, S->copy_s));
+        HIP_TRY(hipEventRecord(S->piece_copied[q], S->copy_s));
+      }
+    }
+    HIP_TRY(hipEventRecord(S->hs_copied[b], S->copy_s));
+    HIP_TRY(hipStreamWaitEvent(S->own, S->hs_copied[b], 0));
+  }
+  const int rc = stream_update(S, S->d_hs[b], offs.data(), lengths, S->own);
+  HIP_TRY(hipEventRecord(S->hs_hashed[b], S->own));
+  if (wait_copy) HIP_TRY(hipEventSynchronize(S->hs_copied[b]));
+  return rc;
+}
+
+}  // namespace
+
+// A large update is appended as consecutive sub-updates of at most `sl` bytes of every chunk
+// (64-B multiples: no carry between them), so the copy of one overlaps the hash of the one
+// before -- appending a chunk in pieces is the same as appending it whole.
+int s3h_stream_update_host(s3h_stream_t S, const uint8_t* const* chunks, const uint64_t* lengths) {
+  if (!S || !chunks || !lengths) return fail(S3H_EINVAL, "stream update: null argument");
+  if (!S->failed.empty())
+    return fail(S3H_EINVAL, "stream object failed earlier (%s): destroy it", S->failed.c_str());
+  const uint64_t n = S->n;
+  uint64_t sum = 0, longest = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (lengths[i] && !chunks[i]) return fail(S3H_EINVAL, "stream update: chunk %llu is null", (unsigned long long)i);
+    sum += (lengths[i] + 63) & ~uint64_t(63);
+    longest = std::max(longest, lengths[i]);
   }
   DeviceGuard g(S->device);
-  if (sum > S->stage_cap) {
-    HIP_TRY(hipStreamSynchronize(S->own));
-    (void)hipFree(S->d_stage);
-    S->d_stage = nullptr;
-    S->stage_cap = 0;
-    HIP_TRY(hipMalloc(&S->d_stage, sum));
-    S->stage_cap = sum;
+  if (!S->copy_s) {
+    HIP_TRY(hipStreamCreateWithFlags(&S->copy_s, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&S->hs_copied[0], &S->hs_copied[1], &S->hs_hashed[0], &S->hs_hashed[1],
+                          &S->piece_copied[0], &S->piece_copied[1]})
+      HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
-  for (uint64_t i = 0; i < S->n; ++i)
-    if (lengths[i])
-      HIP_TRY(hipMemcpyAsync(S->d_stage + offs[i], chunks[i], lengths[i], hipMemcpyHostToDevice, S->own));
-  int rc = stream_update(S, S->d_stage, offs.data(), lengths, S->own);
-  hipError_t e = hipStreamSynchronize(S->own);  // chunks may be released on return
-  if (!rc && e != hipSuccess) rc = fail(S3H_EHIP, "stream update: %s", hipGetErrorString(e));
-  if (!rc) rc = stream_check(S, S->own);
-  return rc;
+  const uint64_t sl = std::max<uint64_t>(kStreamSubMin, (kStreamSubBytes / std::max<uint64_t>(n, 1)) & ~uint64_t(63));
+  if (sum <= 2 * kStreamSubBytes || longest <= sl) return stream_host_update_one(S, chunks, lengths);
+  std::vector<const uint8_t*> p(n);
+  std::vector<uint64_t> l(n);
+  for (uint64_t at = 0; at < longest; at += sl) {
+    for (uint64_t i = 0; i < n; ++i) {
+      l[i] = lengths[i] > at ? std::min(sl, lengths[i] - at) : 0;
+      p[i] = l[i] ? chunks[i] + at : nullptr;
+    }
+    if (int rc = stream_host_update_one(S, p.data(), l.data())) return rc;
+  }
+  return S3H_OK;
 }
 
 int s3h_stream_final_host(s3h_stream_t S, uint32_t* digests) {

@@ -331,8 +331,10 @@ class Stream:
     sha256_next contract (lib/hash/sha256.h:73-89) at ``final()`` -- the digest of the
     concatenation of every chunk appended since the previous ``final()``.
 
-    ``update(chunks)`` takes one chunk per message: host ``bytes``/numpy arrays (blocking),
-    or, with ``update_device``, a device tensor plus offsets/lengths (asynchronous)."""
+    ``update(chunks)`` takes one chunk per message: host ``bytes``/numpy arrays or
+    ``BufferParts`` (returns once the chunks are copied; the hash overlaps the next update and
+    ``final()`` reports a device fault of any of them), or, with ``update_device``, a device
+    tensor plus offsets/lengths (asynchronous)."""
 
     def __init__(self, n: int, device: int = 0, algo: str = "sha256", kernel: str | int = "auto"):
         k = kernel if isinstance(kernel, int) else _native.KERNEL_IDS[kernel]

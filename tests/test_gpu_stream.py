@@ -282,3 +282,41 @@ def test_stream_equal_chunks_reuse_device_slots(torch_cuda, oracle, chunk, alter
     # multiple of 64: body slots reused on every update after the first of each final round;
     # otherwise the heads (64 B at 64*i in the splice buffer) reuse theirs
     assert stats["slot_reuses"] >= (finals * (rounds - 1) if chunk % 64 == 0 else rounds - 2), stats
+
+
+@pytest.mark.parametrize("pinned,equal,n", [(False, False, 64), (True, False, 64), (True, True, 64),
+                                           (True, False, 100), (False, True, 100)])
+def test_stream_host_updates_pipelined_and_buffer_reuse(torch_cuda, oracle, pinned, equal, n):
+    """Host-form updates copy the chunks out and return while the hash still runs; the next
+    update's copy overlaps it (two device staging sets).  Copy forms: pinned chunks of equal
+    length at one stride -> one 2-D DMA; up to 64 other pinned chunks -> one DMA each; more, or
+    pageable ones -> copy threads through two pinned 64 MiB pieces; updates above 256 MiB
+    (100 x 4 MiB) are appended as sub-updates.  The caller overwrites its one chunk buffer right
+    after every update returns -- as an uploader reusing its read buffer does -- and the
+    digests must still be those of the bytes it passed.  Empty and ragged chunks, staging
+    regrowth, and a final in between that restarts the messages."""
+    torch = torch_cuda
+    rng = np.random.default_rng(404 + 2 * pinned + equal + n)
+    cap = 4 << 20
+    buf = torch.empty(n * cap, dtype=torch.uint8, pin_memory=pinned)
+    view = buf.numpy()
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(cap)
+    with s3.Stream(n) as st:
+        for f, rounds in enumerate((3, 5)):
+            msgs = [bytearray() for _ in range(n)]
+            for k in range(rounds):
+                top = [4096, 300000, 3 << 20, 4 << 20, 1 << 20][k % 5]
+                if equal:
+                    lens = np.full(n, top - 7 * (k % 2))  # a 64-B multiple or not
+                else:
+                    lens = rng.integers(0, top + 1, n)
+                    lens[rng.integers(0, n, 3)] = 0
+                view[:] = rng.integers(0, 256, view.size, dtype=np.uint8)
+                for i in range(n):
+                    msgs[i] += view[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes()
+                st.update(s3.BufferParts(buf, offs, lens))
+                view[:] = 0xA5  # the caller reuses its buffer at once
+            got = st.final()
+            want = np.stack([oracle.sha256(bytes(m)) for m in msgs])
+            bad = [i for i in range(n) if not np.array_equal(got[i], want[i])]
+            assert not bad, (f, bad[:8])
