@@ -1401,7 +1401,7 @@ struct s3h_stream_s {
   hipEvent_t hs_copied[2] = {nullptr, nullptr}, hs_hashed[2] = {nullptr, nullptr};
   hipEvent_t piece_copied[2] = {nullptr, nullptr};
   hipStream_t copy_s = nullptr;
-  unsigned hs_set = 0;
+  unsigned hs_set = 0, piece_next = 0;
   std::unique_ptr<CopyPool> pool;
   uint32_t* d_dig = nullptr;   // host-form final
   // Pinned staging of an update / final in two sets used alternately: set b is rewritten
@@ -2491,7 +2491,9 @@ int stream_host_update_one(s3h_stream_s* S, const uint8_t* const* chunks, const 
         S->h_piece_cap = P;
       }
       if (!S->pool) S->pool.reset(new CopyPool(host_threads_per_device(1) - 1, device_place(S->device)));
-      for (uint64_t lo = 0, q = 0; lo < sum; lo += P, q ^= 1u) {
+      for (uint64_t lo = 0; lo < sum; lo += P) {
+        const unsigned q = S->piece_next;  // alternates across updates too
+        S->piece_next ^= 1u;
         const uint64_t hi = std::min(sum, lo + P);
         HIP_TRY(hipEventSynchronize(S->piece_copied[q]));  // its previous DMA has read it
         // the chunks overlapping [lo, hi) of the packed layout (offs ascending)
