@@ -30,6 +30,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <numeric>
 #include <string>
 #include <thread>
@@ -1402,7 +1403,6 @@ struct s3h_stream_s {
   hipEvent_t piece_copied[2] = {nullptr, nullptr};
   hipStream_t copy_s = nullptr;
   unsigned hs_set = 0, piece_next = 0;
-  std::unique_ptr<CopyPool> pool;
   uint32_t* d_dig = nullptr;   // host-form final
   // Pinned staging of an update / final in two sets used alternately: set b is rewritten
   // only once the call that used it two calls ago has completed (staged[b]), so the host
@@ -2426,7 +2426,40 @@ int s3h_stream_final_device(s3h_stream_t S, uint32_t* d_digests, void* stream) {
   return stream_final(S, d_digests, static_cast<hipStream_t>(stream));
 }
 
+}  // extern "C"
+
 namespace {
+
+// The copy threads of host-form stream updates: one pool per device, shared by every stream
+// object on it (their copy phases take turns; each pool is as wide as the CPUs the process may
+// use, on the device's NUMA node), created on first use and kept for the process.
+struct StreamPools {
+  std::mutex m;
+  std::map<int, std::pair<std::unique_ptr<CopyPool>, std::unique_ptr<std::mutex>>> by_device;
+};
+StreamPools& stream_pools() {
+  static auto* p = new StreamPools();  // never destroyed: threads may outlive static teardown
+  return *p;
+}
+
+// fn(i) for i in [0, n) on `device`'s stream copy pool (exclusive while it runs)
+void stream_pool_run(int device, uint64_t n, const std::function<void(uint64_t)>& fn) {
+  StreamPools& P = stream_pools();
+  CopyPool* pool;
+  std::mutex* run_mu;
+  {
+    std::lock_guard<std::mutex> l(P.m);
+    auto& e = P.by_device[device];
+    if (!e.first) {
+      e.first.reset(new CopyPool(host_threads_per_device(1) - 1, device_place(device)));
+      e.second.reset(new std::mutex());
+    }
+    pool = e.first.get();
+    run_mu = e.second.get();
+  }
+  std::lock_guard<std::mutex> l(*run_mu);
+  pool->run(n, fn);
+}
 
 // One host-form update of at most a few hundred MiB (s3h_stream_update_host splits larger
 // ones): the chunks are packed at 64-B aligned offsets into device staging set b and hashed on
@@ -2490,7 +2523,6 @@ int stream_host_update_one(s3h_stream_s* S, const uint8_t* const* chunks, const 
           HIP_TRY(pinned_alloc(reinterpret_cast<void**>(&h), P, node));
         S->h_piece_cap = P;
       }
-      if (!S->pool) S->pool.reset(new CopyPool(host_threads_per_device(1) - 1, device_place(S->device)));
       for (uint64_t lo = 0; lo < sum; lo += P) {
         const unsigned q = S->piece_next;  // alternates across updates too
         S->piece_next ^= 1u;
@@ -2500,7 +2532,7 @@ int stream_host_update_one(s3h_stream_s* S, const uint8_t* const* chunks, const 
         const uint64_t i0 = uint64_t(std::upper_bound(offs.begin(), offs.end(), lo) - offs.begin()) - 1;
         const uint64_t i1 = uint64_t(std::lower_bound(offs.begin(), offs.end(), hi) - offs.begin());
         uint8_t* const dst = S->h_piece[q];
-        S->pool->run(i1 - i0, [&](uint64_t k) {
+        stream_pool_run(S->device, i1 - i0, [&](uint64_t k) {
           const uint64_t i = i0 + k, a = std::max(offs[i], lo), e = std::min(offs[i] + lengths[i], hi);
           if (e > a) std::memcpy(dst + (a - lo), chunks[i] + (a - offs[i]), e - a);
         });
@@ -2518,6 +2550,8 @@ int stream_host_update_one(s3h_stream_s* S, const uint8_t* const* chunks, const 
 }
 
 }  // namespace
+
+extern "C" {
 
 // A large update is appended as consecutive sub-updates of at most `sl` bytes of every chunk
 // (64-B multiples: no carry between them), so the copy of one overlaps the hash of the one
