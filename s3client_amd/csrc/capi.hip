@@ -1436,6 +1436,44 @@ struct s3h_stream_s {
 
 namespace {
 
+// Host-form staging of destroyed stream objects, kept per device for the next object (an
+// uploader creates one per batch of objects: allocating, first-touching and registering 2 x 64
+// MiB of pinned pieces plus the device sets cost ~35 ms per object, ~20 % of a C2-sized batch;
+// profiles/r05_stream_vs_batch_ab.json).  At most kStagingKeep entries per device; s3h_trim
+// frees them.
+struct StreamStaging {
+  uint8_t* d_hs[2] = {nullptr, nullptr};
+  uint64_t d_hs_cap[2] = {0, 0};
+  uint8_t* h_piece[2] = {nullptr, nullptr};
+  uint64_t h_piece_cap = 0;
+};
+constexpr size_t kStagingKeep = 2;
+struct StagingCache {
+  std::mutex m;
+  std::map<int, std::vector<StreamStaging>> free;
+};
+StagingCache& staging_cache() {
+  static auto* c = new StagingCache();
+  return *c;
+}
+
+void staging_release(int device, const StreamStaging& st) {
+  DeviceGuard g(device);
+  for (uint8_t* p : st.d_hs) (void)hipFree(p);
+  pinned_free(st.h_piece[0]);
+  pinned_free(st.h_piece[1]);
+}
+
+void staging_trim() {
+  std::map<int, std::vector<StreamStaging>> all;
+  {
+    std::lock_guard<std::mutex> l(staging_cache().m);
+    all.swap(staging_cache().free);
+  }
+  for (auto& kv : all)
+    for (auto& st : kv.second) staging_release(kv.first, st);
+}
+
 void stream_free(s3h_stream_s* S) {
   DeviceGuard g(S->device);
   if (S->own) (void)hipStreamSynchronize(S->own);
@@ -1446,11 +1484,26 @@ void stream_free(s3h_stream_s* S) {
   s3h_plan_destroy(S->body);
   s3h_plan_destroy(S->fin);
   for (void* p : {(void*)S->d_state, (void*)S->d_carry, (void*)S->d_head, (void*)S->d_jobs,
-                  (void*)S->d_bits, (void*)S->d_hs[0], (void*)S->d_hs[1], (void*)S->d_dig})
+                  (void*)S->d_bits, (void*)S->d_dig})
     (void)hipFree(p);
   pinned_free(S->h_pin);
-  pinned_free(S->h_piece[0]);
-  pinned_free(S->h_piece[1]);
+  if (S->d_hs[0] || S->d_hs[1] || S->h_piece[0]) {  // idle now: keep it for the next object
+    StreamStaging st;
+    std::copy(S->d_hs, S->d_hs + 2, st.d_hs);
+    std::copy(S->d_hs_cap, S->d_hs_cap + 2, st.d_hs_cap);
+    std::copy(S->h_piece, S->h_piece + 2, st.h_piece);
+    st.h_piece_cap = S->h_piece_cap;
+    bool kept = false;
+    {
+      std::lock_guard<std::mutex> l(staging_cache().m);
+      auto& v = staging_cache().free[S->device];
+      if (v.size() < kStagingKeep) {
+        v.push_back(st);
+        kept = true;
+      }
+    }
+    if (!kept) staging_release(S->device, st);
+  }
   for (hipEvent_t e : {S->staged[0], S->staged[1], S->done, S->hs_copied[0], S->hs_copied[1],
                        S->hs_hashed[0], S->hs_hashed[1], S->piece_copied[0], S->piece_copied[1]})
     if (e) (void)hipEventDestroy(e);
@@ -1832,6 +1885,7 @@ int s3h_api_version(void) { return S3H_API_VERSION; }
 
 int s3h_trim(void) {
   host_ctx_cache().trim();
+  staging_trim();
   return S3H_OK;
 }
 
@@ -2569,6 +2623,18 @@ int s3h_stream_update_host(s3h_stream_t S, const uint8_t* const* chunks, const u
   }
   DeviceGuard g(S->device);
   if (!S->copy_s) {
+    {  // staging left by an earlier object on this device, if any
+      std::lock_guard<std::mutex> l(staging_cache().m);
+      auto& v = staging_cache().free[S->device];
+      if (!v.empty()) {
+        const StreamStaging st = v.back();
+        v.pop_back();
+        std::copy(st.d_hs, st.d_hs + 2, S->d_hs);
+        std::copy(st.d_hs_cap, st.d_hs_cap + 2, S->d_hs_cap);
+        std::copy(st.h_piece, st.h_piece + 2, S->h_piece);
+        S->h_piece_cap = st.h_piece_cap;
+      }
+    }
     HIP_TRY(hipStreamCreateWithFlags(&S->copy_s, hipStreamNonBlocking));
     for (hipEvent_t* e : {&S->hs_copied[0], &S->hs_copied[1], &S->hs_hashed[0], &S->hs_hashed[1],
                           &S->piece_copied[0], &S->piece_copied[1]})
