@@ -2551,9 +2551,13 @@ int stream_host_update_one(s3h_stream_s* S, const uint8_t* const* chunks, const 
     std::vector<uint64_t> all(n);
     std::iota(all.begin(), all.end(), uint64_t(0));
     const bool pinned = all_pinned(chunks, lengths, all);
-    const uint64_t stride = n > 1 && chunks[1] >= chunks[0] ? uint64_t(chunks[1] - chunks[0]) : 0;
-    bool strided = pinned && equal && L0 > 0 && n > 1 && stride >= L0;
-    for (uint64_t i = 1; strided && i < n; ++i) strided = uint64_t(chunks[i] - chunks[0]) == i * stride;
+    // equal non-empty chunks at one positive stride (ranges of one buffer): one 2-D DMA
+    bool strided = pinned && equal && L0 > 0 && n > 1;
+    const uintptr_t c0 = reinterpret_cast<uintptr_t>(chunks[0]);
+    const uint64_t stride = strided ? uint64_t(reinterpret_cast<uintptr_t>(chunks[1]) - c0) : 0;
+    strided = strided && stride >= L0 && stride < (uint64_t(1) << 62);
+    for (uint64_t i = 2; strided && i < n; ++i)
+      strided = uint64_t(reinterpret_cast<uintptr_t>(chunks[i]) - c0) == i * stride;
     if (strided) {
       HIP_TRY(hipMemcpy2DAsync(S->d_hs[b], (L0 + 63) & ~uint64_t(63), chunks[0], stride, L0, n,
                                hipMemcpyHostToDevice, S->copy_s));
