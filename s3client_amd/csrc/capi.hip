@@ -888,6 +888,12 @@ constexpr uint64_t kStreamSubBytes = 128ull << 20;
 constexpr uint64_t kStreamSubMin = 64ull << 10;
 constexpr int kHostMaxAlgo = 2;
 constexpr uint64_t kStageSlot = 32ull << 20;     // pinned staging bytes per ring slot
+// Group mode (run_host_groups) for many small parts: parts of at most kGroupMaxPart; a group's
+// copy must outlast its longest part's chain (~69 MB/s per chain vs ~52 GB/s of PCIe: 750 x),
+// groups between kGroupMin and kGroupMax bytes.
+constexpr uint64_t kGroupMaxPart = 1ull << 20;
+constexpr uint64_t kGroupCopyPerChain = 768;
+constexpr uint64_t kGroupMin = 64ull << 20, kGroupMax = 1ull << 30;
 constexpr uint64_t kKeepRingBytes = 1ull << 30;  // largest HBM ring kept between calls
 // File ranges stage with one pread per part per slice, whose syscall costs more than it moves
 // below ~32 KiB: their slices are at least 32 KiB up to 4,096 parts per device (slots of up
@@ -945,6 +951,11 @@ struct HostCtx {
   uint64_t ring_bytes = 0;
   uint8_t* stage = nullptr;  // pinned staging ring (pageable and file sources)
   uint64_t stage_bytes = 0;
+  // group mode (run_host_groups): two plans per algorithm (group k uses set k & 1) and their
+  // pinned geometry staging
+  s3h_plan_s* gplan[2][kHostMaxAlgo] = {};
+  uint8_t* gpin = nullptr;
+  uint64_t gpin_bytes = 0;
 
   hipError_t ensure_streams() {
     hipError_t e = hipSuccess;
@@ -1000,6 +1011,24 @@ struct HostCtx {
            uint64_t(a) * pin_cap();
   }
   uint64_t pin_cap() const { return pin_bytes / (kHostMaxAlgo * (sizeof(s3h::Slot) + 4)); }
+  int ensure_gplan(int q, int a, int algo, uint64_t n) {
+    s3h_plan_s*& P = gplan[q][a];
+    if (P && P->algo == algo && P->cap >= n) return S3H_OK;
+    s3h_plan_destroy(P);
+    P = nullptr;
+    return plan_alloc(device, algo, std::max<uint64_t>(n, 1024), &P);
+  }
+  uint64_t gpin_cap() const { return gpin_bytes / (2 * kHostMaxAlgo * (sizeof(s3h::Slot) + 4)); }
+  hipError_t ensure_gpin(uint64_t n) {
+    return grow_pinned(&gpin, &gpin_bytes, 2 * kHostMaxAlgo * std::max<uint64_t>(n, 1024) * (sizeof(s3h::Slot) + 4));
+  }
+  s3h::Slot* gslots(int q, int a) {
+    return reinterpret_cast<s3h::Slot*>(gpin) + uint64_t(q * kHostMaxAlgo + a) * gpin_cap();
+  }
+  uint32_t* gorder(int q, int a) {
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<s3h::Slot*>(gpin) + 2 * kHostMaxAlgo * gpin_cap()) +
+           uint64_t(q * kHostMaxAlgo + a) * gpin_cap();
+  }
   hipError_t ensure_pin(uint64_t n) {
     return grow_pinned(&pin, &pin_bytes, kHostMaxAlgo * std::max<uint64_t>(n, 1024) * (sizeof(s3h::Slot) + 4));
   }
@@ -1036,9 +1065,13 @@ struct HostCtx {
       if (d) (void)hipFree(d);
     for (s3h_plan_s* p : plan)
       if (p) s3h_plan_destroy(p);
+    for (auto& row : gplan)
+      for (s3h_plan_s* p : row)
+        if (p) s3h_plan_destroy(p);
     if (ring) (void)hipFree(ring);
     pinned_free(stage);
     pinned_free(pin);
+    pinned_free(gpin);
   }
 };
 
@@ -1146,6 +1179,158 @@ struct HostShard {
   std::vector<uint64_t> parts;  // global part indices on this device
 };
 
+// Many small parts: slicing every part (run_host_shard) would cut them into slices of a few
+// hundred bytes (the staging slot holds n slices) or issue one DMA per part and slice, so
+// instead the parts go in GROUPS of consecutive parts (~kGroupCopyPerChain x the longest part,
+// in [kGroupMin, kGroupMax] bytes): each group is packed into pinned staging by the copy
+// threads (memcpy / pread; pinned parts that are one contiguous range of a buffer are DMA'd as
+// that range instead), copied by one DMA into one of two HBM group buffers, and hashed WHOLE
+// by one launch per algorithm while the next group is packed and copied.
+int run_host_groups(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
+                    const PartSource& src, const uint64_t* lengths, uint32_t* const* digests,
+                    bool pinned) {
+  const uint64_t n = sh.parts.size();
+  std::vector<uint64_t> lens(n), poff(n);
+  uint64_t longest = 0;
+  for (uint64_t j = 0; j < n; ++j) {
+    lens[j] = lengths[sh.parts[j]];
+    longest = std::max(longest, lens[j]);
+  }
+  const uint64_t G = std::min(kGroupMax, std::max(kGroupMin, kGroupCopyPerChain * ((longest + 63) & ~uint64_t(63))));
+  std::vector<uint64_t> gstart{0}, gbytes;
+  uint64_t acc = 0;
+  for (uint64_t j = 0; j < n; ++j) {
+    const uint64_t a = (lens[j] + 63) & ~uint64_t(63);
+    if (acc + a > G && acc > 0) {
+      gbytes.push_back(acc);
+      gstart.push_back(j);
+      acc = 0;
+    }
+    poff[j] = acc;
+    acc += a;
+  }
+  gbytes.push_back(acc);
+  gstart.push_back(n);
+  const uint64_t ngroups = gbytes.size();
+  uint64_t maxb = 64, maxparts = 1;
+  for (uint64_t k = 0; k < ngroups; ++k) {
+    maxb = std::max(maxb, gbytes[k]);
+    maxparts = std::max(maxparts, gstart[k + 1] - gstart[k]);
+  }
+  // pinned parts that form one increasing range of a buffer with small gaps: DMA'd as is
+  const uint8_t* const* parts = src.parts;
+  auto contiguous = [&](uint64_t j0, uint64_t j1, uint64_t* span) {
+    if (!pinned || !parts) return false;
+    const uint8_t* lo = nullptr;
+    const uint8_t* hi = nullptr;
+    for (uint64_t j = j0; j < j1; ++j) {
+      if (!lens[j]) continue;
+      const uint8_t* p = parts[sh.parts[j]];
+      if (hi && p < hi) return false;
+      if (!lo) lo = p;
+      hi = p + lens[j];
+    }
+    *span = lo ? uint64_t(hi - lo) : 0;
+    return *span <= maxb;
+  };
+  HIP_TRY(C.ensure_streams());
+  hipError_t ce = HostCtx::grow_dev(&C.ring, &C.ring_bytes, 2 * maxb);
+  if (ce != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(S3H_ENOMEM, "host group buffers (2 x %llu B of HBM): %s", (unsigned long long)maxb,
+                hipGetErrorString(ce));
+  }
+  bool any_staged = false;
+  for (uint64_t k = 0; k < ngroups && !any_staged; ++k) {
+    uint64_t span = 0;
+    any_staged = !contiguous(gstart[k], gstart[k + 1], &span);
+  }
+  if (any_staged) {
+    ce = C.grow_pinned(&C.stage, &C.stage_bytes, 2 * maxb);
+    if (ce != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(S3H_ENOMEM, "pinned group staging (2 x %llu B): %s", (unsigned long long)maxb,
+                  hipGetErrorString(ce));
+    }
+  }
+  HIP_TRY(C.ensure_gpin(maxparts));
+  for (int q = 0; q < 2; ++q)
+    for (int a = 0; a < nalgo; ++a) {
+      if (int rc = C.ensure_gplan(q, a, algos[a], maxparts)) return rc;
+      HIP_TRY(hipMemsetAsync(C.gplan[q][a]->d_err, 0, sizeof(uint32_t), C.copy_s));
+    }
+  for (int a = 0; a < nalgo; ++a)
+    HIP_TRY(C.ensure_digests(a, n * digest_words(algos[a]) * sizeof(uint32_t)));
+  CopyPool* pool = any_staged ? C.ensure_pool(host_threads_per_device(sh.ndevices) - 1) : nullptr;
+  std::vector<uint64_t> offs;
+  for (uint64_t k = 0; k < ngroups; ++k) {
+    const int q = int(k & 1);
+    const uint64_t j0 = gstart[k], j1 = gstart[k + 1], ng = j1 - j0;
+    uint8_t* const dgrp = C.ring + uint64_t(q) * maxb;
+    // group k-2 used set q: its DMAs (host staging and geometry staging) must have run, and
+    // its hashes (the HBM group buffer and the plans' device slots) before the copy stream
+    // overwrites them
+    if (k >= 2) {
+      HIP_TRY(hipEventSynchronize(C.copied[q]));
+      for (int a = 0; a < nalgo; ++a) HIP_TRY(hipStreamWaitEvent(C.copy_s, C.hashed[q][a], 0));
+    }
+    uint64_t span = 0;
+    const bool direct = contiguous(j0, j1, &span);
+    offs.assign(ng, 0);
+    const uint8_t* base = nullptr;
+    for (uint64_t t = 0; t < ng && direct; ++t)
+      if (lens[j0 + t] && !base) base = parts[sh.parts[j0 + t]];
+    for (uint64_t t = 0; t < ng; ++t)
+      offs[t] = direct ? (lens[j0 + t] ? uint64_t(parts[sh.parts[j0 + t]] - base) : 0) : poff[j0 + t];
+    for (int a = 0; a < nalgo; ++a)
+      if (int rc = plan_geometry(C.gplan[q][a], offs.data(), lens.data() + j0, ng, S3H_KERNEL_AUTO,
+                                 C.gslots(q, a), C.gorder(q, a), C.copy_s))
+        return rc;
+    if (direct) {
+      if (span) HIP_TRY(hipMemcpyAsync(dgrp, base, span, hipMemcpyHostToDevice, C.copy_s));
+    } else {
+      uint8_t* const hst = C.stage + uint64_t(q) * maxb;
+      std::atomic<bool> bad{false};
+      pool->run(ng, [&](uint64_t t) {
+        const uint64_t j = j0 + t;
+        if (lens[j] && !src.fill(sh.parts[j], 0, lens[j], hst + poff[j]))
+          bad.store(true, std::memory_order_relaxed);
+      });
+      if (bad.load()) return fail(S3H_EINVAL, "reading a part failed (file shorter than a part?)");
+      HIP_TRY(hipMemcpyAsync(dgrp, hst, gbytes[k], hipMemcpyHostToDevice, C.copy_s));
+    }
+    HIP_TRY(hipEventRecord(C.copied[q], C.copy_s));
+    for (int a = 0; a < nalgo; ++a) {
+      s3h_plan_s* P = C.gplan[q][a];
+      HIP_TRY(hipStreamWaitEvent(C.hash_s[a], C.copied[q], 0));
+      if (int rc = plan_launch(P, dgrp, C.d_dig[a] + j0 * digest_words(algos[a]), 0, P->max_blocks, 0,
+                               C.hash_s[a], false))
+        return rc;
+      HIP_TRY(hipEventRecord(C.hashed[q][a], C.hash_s[a]));
+    }
+  }
+  int rc = S3H_OK;
+  for (int a = 0; a < nalgo && rc == S3H_OK; ++a) {
+    const uint32_t dw = digest_words(algos[a]);
+    std::vector<uint32_t> local(n * dw);
+    hipError_t e = hipMemcpyAsync(local.data(), C.d_dig[a], n * dw * 4, hipMemcpyDeviceToHost, C.hash_s[a]);
+    if (e == hipSuccess) e = hipStreamSynchronize(C.hash_s[a]);
+    if (e != hipSuccess) {
+      rc = fail(S3H_EHIP, "D2H digests: %s", hipGetErrorString(e));
+      break;
+    }
+    for (int q = 0; q < 2 && rc == S3H_OK; ++q) rc = plan_check(C.gplan[q][a], C.hash_s[a]);
+    if (rc) break;
+    for (uint64_t j = 0; j < n; ++j) std::memcpy(digests[a] + dw * sh.parts[j], &local[dw * j], dw * 4);
+  }
+  C.sync();
+  if (trace_host())
+    std::fprintf(stderr, "[s3h host] dev %d: %llu parts in %llu groups of <= %llu B (%s)\n", sh.device,
+                 (unsigned long long)n, (unsigned long long)ngroups, (unsigned long long)maxb,
+                 any_staged ? "staged" : "pinned ranges");
+  return rc;
+}
+
 // Streams one device's parts through a 3-slot HBM ring; every slice is copied ONCE and
 // hashed by each requested algorithm (SHA-256 and/or MD5) on its own stream, so a dual
 // digest costs one PCIe pass.  digests[a] receives algo[a]'s digests (global part order).
@@ -1172,6 +1357,20 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
     uniform = stride >= intptr_t(lens[0]) && lens[0] > 0;
     for (uint64_t j = 1; j < n && uniform; ++j)
       uniform = lens[j] == lens[0] && parts[sh.parts[j]] - parts[sh.parts[j - 1]] == stride;
+  }
+  // Many small parts: whole parts in groups instead of slices of every part (run_host_groups)
+  // -- when staging would cut slices below 16 KiB (> 2,048 parts), or pinned ragged parts would
+  // each take their own DMA per slice (> 64 parts averaging < 256 KiB).  A caller's explicit
+  // slice size keeps the slice pipeline.
+  if (slice == 0) {
+    uint64_t longest = 0, total = 0;
+    for (uint64_t j = 0; j < n; ++j) {
+      longest = std::max(longest, lens[j]);
+      total += lens[j];
+    }
+    if (longest <= kGroupMaxPart &&
+        ((staged && n > 2048) || (!staged && !uniform && n > 64 && total < n * (256ull << 10))))
+      return run_host_groups(C, sh, algos, nalgo, src, lengths, digests, !staged);
   }
   // Too many pageable parts for the staging cap even at 64 B per slice: pageable DMAs.
 #ifdef S3H_EXP_PAGEABLE_DIRECT  // tools/ experiment builds only: pageable DMAs, no staging

@@ -581,3 +581,40 @@ def test_buffer_parts_match_views(torch_cuda, oracle):
         got, taken = s3.sha256_batch_routed(bp, route="gpu")
         assert np.array_equal(got, want) and taken == "gpu"
     del pinned
+
+
+@pytest.mark.parametrize("layout", ["pinned_range", "pinned_shuffled", "pageable", "file", "dual"])
+def test_many_small_parts_in_groups(torch_cuda, oracle, tmp_path, layout):
+    """Thousands of small ragged parts (0 - 128 KiB, ~300 MiB: several groups of whole parts,
+    run_host_groups) instead of slices of every part: pinned parts that are one increasing
+    range of a buffer (DMA'd as the range), pinned parts in shuffled order (packed by the copy
+    threads), pageable parts, file ranges (pread) and both digests at once; every digest vs
+    the oracle."""
+    torch = torch_cuda
+    rng = np.random.default_rng(808 + len(layout))
+    n = 4000
+    lens = rng.integers(0, 128 << 10, n).astype(np.uint64)
+    lens[rng.integers(0, n, 20)] = 0
+    gaps = rng.integers(0, 16, n).astype(np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens + gaps)[:-1]]).astype(np.uint64)
+    total = int(offs[-1] + lens[-1]) + 64
+    src = rng.integers(0, 256, total, dtype=np.uint8)
+    want = oracle.batch(src, offs, lens, threads=16)
+    if layout == "file":
+        path = tmp_path / "small.bin"
+        src.tofile(path)
+        got = s3.sha256_file_parts(str(path), offs, lens)
+    else:
+        buf = torch.empty(total, dtype=torch.uint8, pin_memory=layout.startswith("pinned") or layout == "dual")
+        buf.numpy()[:] = src
+        if layout == "pinned_shuffled":
+            perm = rng.permutation(n)
+            got = np.empty_like(want)
+            got[perm] = s3.sha256_batch_host(s3.BufferParts(buf, offs[perm], lens[perm]))
+        elif layout == "dual":
+            got, m5 = s3.sha256_md5_batch_host(s3.BufferParts(buf, offs, lens))
+            assert np.array_equal(m5, oracle.md5_batch(src, offs, lens))
+        else:
+            got = s3.sha256_batch_host(s3.BufferParts(buf, offs, lens))
+    bad = np.flatnonzero((got != want).any(axis=1))
+    assert bad.size == 0, (layout, bad[:8])
