@@ -1196,7 +1196,13 @@ int run_host_groups(HostCtx& C, const HostShard& sh, const int* algos, int nalgo
     lens[j] = lengths[sh.parts[j]];
     longest = std::max(longest, lens[j]);
   }
-  const uint64_t G = std::min(kGroupMax, std::max(kGroupMin, kGroupCopyPerChain * ((longest + 63) & ~uint64_t(63))));
+  // the two group buffers stay within a quarter of the free HBM, as the slice ring does
+  size_t free_b = 0, total_b = 0;
+  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  const uint64_t budget = std::min<uint64_t>(16ull << 30, (free_b + C.ring_bytes) / 4);
+  const uint64_t longest64 = std::max<uint64_t>(64, (longest + 63) & ~uint64_t(63));
+  const uint64_t G = std::max(longest64, std::min({kGroupMax, std::max(kGroupMin, kGroupCopyPerChain * longest64),
+                                                   budget / 2 / 64 * 64}));
   std::vector<uint64_t> gstart{0}, gbytes;
   uint64_t acc = 0;
   for (uint64_t j = 0; j < n; ++j) {
@@ -1362,15 +1368,23 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
   // -- when staging would cut slices below 16 KiB (> 2,048 parts), or pinned ragged parts would
   // each take their own DMA per slice (> 64 parts averaging < 256 KiB).  A caller's explicit
   // slice size keeps the slice pipeline.
+  // Large parts beside them (an object's parts batched with many small objects) run through
+  // the slice pipeline afterwards, on their own.
   if (slice == 0) {
-    uint64_t longest = 0, total = 0;
+    std::vector<uint64_t> small, large;
+    uint64_t small_total = 0;
     for (uint64_t j = 0; j < n; ++j) {
-      longest = std::max(longest, lens[j]);
-      total += lens[j];
+      (lens[j] <= kGroupMaxPart ? small : large).push_back(sh.parts[j]);
+      if (lens[j] <= kGroupMaxPart) small_total += lens[j];
     }
-    if (longest <= kGroupMaxPart &&
-        ((staged && n > 2048) || (!staged && !uniform && n > 64 && total < n * (256ull << 10))))
-      return run_host_groups(C, sh, algos, nalgo, src, lengths, digests, !staged);
+    const uint64_t ns = small.size();
+    if ((staged && ns > 2048) || (!staged && !uniform && ns > 64 && small_total < ns * (256ull << 10))) {
+      if (large.empty()) return run_host_groups(C, sh, algos, nalgo, src, lengths, digests, !staged);
+      const HostShard hs{sh.device, sh.ndevices, std::move(small)};
+      const HostShard hl{sh.device, sh.ndevices, std::move(large)};
+      if (int rc = run_host_groups(C, hs, algos, nalgo, src, lengths, digests, !staged)) return rc;
+      return run_host_shard(C, hl, algos, nalgo, src, lengths, digests, 0);
+    }
   }
   // Too many pageable parts for the staging cap even at 64 B per slice: pageable DMAs.
 #ifdef S3H_EXP_PAGEABLE_DIRECT  // tools/ experiment builds only: pageable DMAs, no staging

@@ -10,8 +10,10 @@ is free, and the entry points are driven into their allocation failures:
   * the host path on C2-sized parts (768 MiB ring at full size) with < 512 MiB free: the ring
     is sized to a quarter of the free HBM (capi.hip run_host_shard), so the call SUCCEEDS with
     smaller slices and bit-exact digests -- by design, a busy GPU still hashes;
-  * the host path when even its smallest ring (3 x n x 64 B) cannot fit (1M parts, < 48 MiB
-    free)                                          -> S3H_ENOMEM "host ring" / "plan alloc"
+  * the host path on 4M parts of 64 B with < 48 MiB free: they go in groups (capi.hip
+    run_host_groups, whose two group buffers also shrink to a quarter of the free HBM), but
+    their 128 MiB of digests cannot fit           -> S3H_ENOMEM "ensure_digests" (or the
+    group buffers / plans when those fail first)
 
 After every failure a small device batch on the remaining memory must still be bit-exact (a
 failed allocation must not leak into a later launch's error check), and once the memory is
@@ -75,7 +77,7 @@ def test_out_of_hbm_fails_cleanly_and_recovers(torch_cuda, oracle):
     torch.from_numpy(host.array).copy_(data)
     del data
     parts = s3.BufferParts(host.array, offs, lens)
-    tiny_n = 1 << 20
+    tiny_n = 4 << 20
     tiny = rng.integers(0, 256, tiny_n * 64, dtype=np.uint8)
     tiny_offs = np.arange(tiny_n, dtype=np.uint64) * np.uint64(64)
     tiny_lens = np.full(tiny_n, 64, dtype=np.uint64)
@@ -100,10 +102,10 @@ def test_out_of_hbm_fails_cleanly_and_recovers(torch_cuda, oracle):
         free = _fill(torch, dev, 48 * MIB, hog)
         assert free < 48 * MIB, free
         msgs["host"] = _enomem(lambda: s3.sha256_batch_host(tiny_parts, ndevices=1),
-                               "host ring", "plan alloc", "ensure_digests")
+                               "host ring", "host group", "plan alloc", "ensure_digests")
         _small_batch_ok(torch, dev, oracle, rng)
         msgs["host_again"] = _enomem(lambda: s3.sha256_batch_host(tiny_parts, ndevices=1),
-                                     "host ring", "plan alloc", "ensure_digests")
+                                     "host ring", "host group", "plan alloc", "ensure_digests")
     finally:
         del hog
         torch.cuda.empty_cache()

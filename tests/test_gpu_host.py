@@ -583,18 +583,23 @@ def test_buffer_parts_match_views(torch_cuda, oracle):
     del pinned
 
 
-@pytest.mark.parametrize("layout", ["pinned_range", "pinned_shuffled", "pageable", "file", "dual"])
+@pytest.mark.parametrize("layout", ["pinned_range", "pinned_shuffled", "pageable", "file", "dual",
+                                    "pageable_mixed", "pinned_mixed"])
 def test_many_small_parts_in_groups(torch_cuda, oracle, tmp_path, layout):
     """Thousands of small ragged parts (0 - 128 KiB, ~300 MiB: several groups of whole parts,
     run_host_groups) instead of slices of every part: pinned parts that are one increasing
     range of a buffer (DMA'd as the range), pinned parts in shuffled order (packed by the copy
-    threads), pageable parts, file ranges (pread) and both digests at once; every digest vs
-    the oracle."""
+    threads), pageable parts, file ranges (pread) and both digests at once; `mixed`: a few
+    large parts (2 - 24 MiB) among them go through the slice pipeline afterwards.  Every
+    digest vs the oracle."""
     torch = torch_cuda
     rng = np.random.default_rng(808 + len(layout))
     n = 4000
     lens = rng.integers(0, 128 << 10, n).astype(np.uint64)
     lens[rng.integers(0, n, 20)] = 0
+    if layout.endswith("_mixed"):
+        lens[rng.integers(0, n, 5)] = rng.integers(2 << 20, 24 << 20, 5)
+        layout = layout[:-len("_mixed")]
     gaps = rng.integers(0, 16, n).astype(np.uint64)
     offs = np.concatenate([[0], np.cumsum(lens + gaps)[:-1]]).astype(np.uint64)
     total = int(offs[-1] + lens[-1]) + 64
