@@ -862,9 +862,33 @@ def host_resident(s3, torch, data, ids, lens, offs, gd, reps: int = 3):
                    "(s3h_sha256_batch_host)",
            "fixture_mismatches": _fixture_mismatches(s3, ids, out),
            "digests_match_device_run": bool(np.array_equal(out, gd))}
+    res["split"] = split_from_host(s3, parts, lens, gd)
     res["stream"] = stream_from_host(s3, host, offs, lens, gd)
     del host, parts, rhost, rparts, local_buf, remote
     return res
+
+
+def split_from_host(s3, parts, lens, gd, reps: int = 3) -> dict:
+    """The same pinned C2 parts on S3H_ROUTE_SPLIT: the CPU drop-in (SHA-NI on the host
+    threads) hashes the model's share of the parts while the GPU host path hashes the rest, at
+    once -- the upload path's rate when the host's cores help; NOT a GPU-only number (`value`
+    above is).  What AUTO takes for this batch is reported beside it."""
+    gib = float(lens.sum()) / 2**30
+    s3.sha256_batch_routed(parts, ndevices=1, route="split")  # warm
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out, taken = s3.sha256_batch_routed(parts, ndevices=1, route="split")
+        times.append(time.perf_counter() - t0)
+    model = s3.route_model()
+    k, est = s3.route_split_estimate(lens, model, ndevices=1)
+    auto_out, auto_taken = s3.sha256_batch_routed(parts, ndevices=1, route="auto")
+    return {"metric": "host-resident SHA-256 GiB/s, GPU host path and CPU drop-in at once (S3H_ROUTE_SPLIT)",
+            "GiBps": round(gib / float(np.mean(times)), 3), "ms_per_batch": round(1e3 * float(np.mean(times)), 2),
+            "reps": reps, "taken": taken, "cpu_parts": k, "gpu_parts": int(len(lens) - k),
+            "cpu_threads": model["cpu_threads"], "cpu_backend": s3.cpu_backend(),
+            "model_s": round(est, 4), "auto_takes": auto_taken,
+            "digests_match_device_run": bool(np.array_equal(out, gd) and np.array_equal(auto_out, gd))}
 
 
 def stream_from_host(s3, host, offs, lens, gd, chunk: int = MIB, reps: int = 2) -> dict:

@@ -281,12 +281,17 @@ int s3h_sha256_md5_batch_device(int device, const void *d_base, const uint64_t *
  * the drop-in on one thread and on all of them, the threads' staging memcpy).  AUTO needs a
  * visible GPU (S3H_ENODEV otherwise): it chooses between two paths with identical digests and
  * is never a fallback for a missing device.
- * *taken (if non-null) receives the route that ran (S3H_ROUTE_GPU or S3H_ROUTE_CPU).
+ * S3H_ROUTE_SPLIT = both at once: the CPU drop-in hashes the m longest parts on its threads
+ * while the GPU host path hashes the rest (m from the model, s3h_route_split_estimate; a single
+ * part goes to the GPU); AUTO also splits parts that are all in pinned memory when the split
+ * is estimated at least 5 % faster than the better single route (a pageable or file GPU side
+ * needs the host threads for staging, so AUTO does not split those).
+ * *taken (if non-null) receives the route that ran (S3H_ROUTE_GPU, _CPU or _SPLIT).
  *   gpu_s = call_s + max(longest part / chain rate, bytes per device / feed rate)
  *           feed = h2d (pinned parts) or min(h2d, staged) (pageable parts, file ranges)
  *   cpu_s = (longest-first schedule of the parts on k = min(n, threads) threads) / (rate(k) / k)
  *           rate(k) = min(k x cpu_bytes_per_s, cpu_all_bytes_per_s) */
-enum s3h_route { S3H_ROUTE_GPU = 0, S3H_ROUTE_CPU = 1, S3H_ROUTE_AUTO = 2 };
+enum s3h_route { S3H_ROUTE_GPU = 0, S3H_ROUTE_CPU = 1, S3H_ROUTE_AUTO = 2, S3H_ROUTE_SPLIT = 3 };
 typedef struct {
   double cpu_bytes_per_s;   /* one host thread on the lib/hash drop-in (s3h_cpu_backend) */
   double chain_bytes_per_s; /* one part's chain on the GPU (the skew kernel, a lone part) */
@@ -311,6 +316,15 @@ int s3h_route_estimate(const s3h_route_model_t *m, const uint64_t *lengths, uint
 enum s3h_source { S3H_SOURCE_PINNED = 0, S3H_SOURCE_PAGEABLE = 1, S3H_SOURCE_FILE = 2 };
 int s3h_route_estimate_ex(const s3h_route_model_t *m, const uint64_t *lengths, uint64_t n,
                           int ndevices, int source, double *gpu_s, double *cpu_s);
+/* The split route's plan under model *m (pure host arithmetic): with the parts ordered by length
+ * (descending, ties by index), the first *cpu_parts go to the CPU and the rest to the GPU, and
+ *   split_s(m) = max(gpu_s(the n - m shorter parts), cpu_s(the m longest)),  m = 1 .. n-1
+ * (gpu_s / cpu_s as above on each side's parts); of the m with split_s(m) within 0.5 % of the
+ * minimum (the GPU side's longest chain makes ranges of m tie), *cpu_parts = the one with the
+ * smallest max(GPU side's bytes / devices / feed, cpu_s(m)), and *split_s = split_s(it)
+ * (*cpu_parts = 0 when n == 1). */
+int s3h_route_split_estimate(const s3h_route_model_t *m, const uint64_t *lengths, uint64_t n,
+                             int ndevices, int source, uint64_t *cpu_parts, double *split_s);
 int s3h_sha256_batch_routed(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                             uint32_t *digests, int ndevices, int route, int *taken);
 int s3h_sha256_file_parts_routed(const char *path, const uint64_t *offsets,

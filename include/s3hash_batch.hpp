@@ -46,9 +46,10 @@ inline void sha256_batch_device(int device, const void* d_base,
 }
 
 // Where a host batch is hashed (include/s3hash.h "size-aware routing"): gpu = the batched GPU
-// path (default), cpu = the lib/hash drop-in on host threads, automatic = whichever a model
-// measured once per process estimates to finish first (needs a GPU; never a fallback).
-enum class Route { gpu = S3H_ROUTE_GPU, cpu = S3H_ROUTE_CPU, automatic = S3H_ROUTE_AUTO };
+// path (default), cpu = the lib/hash drop-in on host threads, split = both at once (the
+// longest parts on the CPU, the rest on the GPU), automatic = whichever a model measured once
+// per process estimates to finish first (needs a GPU; never a fallback).
+enum class Route { gpu = S3H_ROUTE_GPU, cpu = S3H_ROUTE_CPU, automatic = S3H_ROUTE_AUTO, split = S3H_ROUTE_SPLIT };
 
 inline std::vector<std::string> to_hex(const std::vector<uint32_t>& d) {
   std::vector<std::string> out(d.size() / 8);

@@ -9,7 +9,7 @@ from .hashing import (Plan, device_count, digests_to_text, generate_parts, hash_
                       sha256_md5_batch_device, sha256_md5_batch_host, sha256_file_parts,
                       sha256_md5_file_parts,
                       trim, sha256_batch_host_on, host_threads, device_pci_bus_id,
-                      route_model, route_estimate, sha256_batch_routed,
+                      route_model, route_estimate, route_split_estimate, sha256_batch_routed,
                       sha256_file_parts_routed, BufferParts, pci_numa, device_numa,
                       host_numa, host_numa_info, mem_node, PinnedBuffer,
                       kernel_policy, dual_layout)
@@ -22,7 +22,7 @@ __all__ = ["BufferParts", "Plan", "device_count", "digests_to_text", "generate_p
            "verify_batch_device", "verify_batch_host", "Stream",
            "sha256_md5_batch_device", "sha256_md5_batch_host", "sha256_file_parts",
            "sha256_md5_file_parts", "trim", "sha256_batch_host_on", "host_threads",
-           "device_pci_bus_id", "route_model", "route_estimate", "sha256_batch_routed",
+           "device_pci_bus_id", "route_model", "route_estimate", "route_split_estimate", "sha256_batch_routed",
            "sha256_file_parts_routed", "pci_numa", "device_numa", "host_numa", "host_numa_info",
            "mem_node", "PinnedBuffer", "kernel_policy", "dual_layout",
            "upload_parts_geometry", "UploadPart", "S3HashError", "LIB_PATH"]

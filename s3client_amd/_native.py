@@ -42,14 +42,14 @@ C_ABI_SYMBOLS = (
     "s3h_sha256_file_parts_routed", "s3h_pci_numa", "s3h_device_numa_node", "s3h_host_numa",
     "s3h_host_numa_info", "s3h_host_alloc", "s3h_host_free", "s3h_mem_node",
     "s3h_route_estimate_ex", "s3h_kernel_policy", "s3h_stream_stats", "s3h_plan_dual_layout",
-    "s3h_dual_layout",
+    "s3h_dual_layout", "s3h_route_split_estimate",
 )
 POLICY_IDS = {"throughput": 0, "efficiency": 1}
 POLICY_NAMES = {v: k for k, v in POLICY_IDS.items()}
 SOURCE_IDS = {"pinned": 0, "pageable": 1, "file": 2}
 NUMA_LOCAL, NUMA_OFF = -1, -2
-ROUTE_GPU, ROUTE_CPU, ROUTE_AUTO = 0, 1, 2
-ROUTE_IDS = {"gpu": ROUTE_GPU, "cpu": ROUTE_CPU, "auto": ROUTE_AUTO}
+ROUTE_GPU, ROUTE_CPU, ROUTE_AUTO, ROUTE_SPLIT = 0, 1, 2, 3
+ROUTE_IDS = {"gpu": ROUTE_GPU, "cpu": ROUTE_CPU, "auto": ROUTE_AUTO, "split": ROUTE_SPLIT}
 ROUTE_NAMES = {v: k for k, v in ROUTE_IDS.items()}
 
 
@@ -198,6 +198,10 @@ def lib() -> ctypes.CDLL:
                                                 ctypes.c_int, ctypes.c_int,
                                                 ctypes.POINTER(ctypes.c_double),
                                                 ctypes.POINTER(ctypes.c_double)]
+            L.s3h_route_split_estimate.argtypes = [ctypes.POINTER(RouteModel), u64p, ctypes.c_uint64,
+                                                   ctypes.c_int, ctypes.c_int,
+                                                   ctypes.POINTER(ctypes.c_uint64),
+                                                   ctypes.POINTER(ctypes.c_double)]
             L.s3h_sha256_batch_routed.argtypes = [ctypes.POINTER(ctypes.c_void_p), u64p,
                                                   ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
                                                   ctypes.c_int, ctypes.POINTER(ctypes.c_int)]

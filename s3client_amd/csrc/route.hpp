@@ -288,6 +288,79 @@ int route_choose(const s3h_route_model_t& m, const uint64_t* lengths, uint64_t n
   return c < g ? S3H_ROUTE_CPU : S3H_ROUTE_GPU;
 }
 
+// S3H_ROUTE_SPLIT: the CPU drop-in hashes the m LONGEST parts on its threads while the GPU
+// host path hashes the rest, both at once (the calling thread drives the GPU side).  A part's
+// GPU chain runs ~30x slower than one SHA-NI core, so the long parts go to the CPU and the
+// GPU keeps the many shorter ones it needs to fill its lanes; for C2 from pinned memory the
+// GPU alone is fed at the PCIe rate and the CPU alone at its threads' rate, together faster
+// than either until the GPU side reaches its chain time:
+//   split_s(m) = max(gpu_s(the n - m shorter parts), cpu_s(the m longest))   m = 1 .. n-1
+// with gpu_s / cpu_s the estimates above on each side's parts; among the m within 0.5 % of the
+// minimum, the one with the smallest max(GPU side's bytes / feed, cpu_s).  Parts are ordered by length,
+// descending (ties: lower index first); the CPU side's longest-first schedule is built
+// incrementally as m grows (exact LPT).
+constexpr double kSplitTie = 0.005;  // estimates within 0.5 % of the minimum tie
+
+struct Split {
+  uint64_t m = 0;   // parts on the CPU: order[0, m) (0 only for a single part)
+  double s = 0, g = 0, c = 0;
+};
+
+std::vector<uint64_t> longest_first(const uint64_t* lengths, uint64_t n) {
+  std::vector<uint64_t> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return lengths[a] > lengths[b]; });
+  return order;
+}
+
+Split split_choose(const s3h_route_model_t& M, const uint64_t* lengths, uint64_t n, int ndevices,
+                   int source, const std::vector<uint64_t>& order) {
+  Split best;
+  if (n < 2) return best;
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < n; ++i) total += lengths[i];
+  const double feed = source == S3H_SOURCE_PINNED || !(M.staged_bytes_per_s > 0)
+                          ? M.h2d_bytes_per_s : std::min(M.h2d_bytes_per_s, M.staged_bytes_per_s);
+  const uint64_t kmax = std::min<uint64_t>(n, uint64_t(std::max(1, M.cpu_threads)));
+  const int dev_cap = ndevices > 0 ? std::min(ndevices, M.devices) : M.devices;
+  std::vector<double> load(kmax, 0.0);  // min-heap of the CPU threads' loads (bytes)
+  std::vector<double> G(n), C(n), F(n);  // per m: gpu_s, cpu_s, the GPU side's feed time
+  double makespan = 0, smin = 1e300;
+  uint64_t cpu_bytes = 0;
+  for (uint64_t m = 1; m < n; ++m) {
+    const uint64_t x = lengths[order[m - 1]];
+    std::pop_heap(load.begin(), load.end(), std::greater<double>());
+    load.back() += double(x);
+    makespan = std::max(makespan, load.back());
+    std::push_heap(load.begin(), load.end(), std::greater<double>());
+    cpu_bytes += x;
+    const uint64_t k = std::min(m, kmax);
+    const double c = makespan / (cpu_rate(M, double(k)) / double(k));
+    const int devs = std::max(1, int(std::min<uint64_t>(n - m, uint64_t(std::max(1, dev_cap)))));
+    F[m] = double(total - cpu_bytes) / devs / feed;
+    G[m] = M.call_s + std::max(double(lengths[order[m]]) / M.chain_bytes_per_s, F[m]);
+    C[m] = c;
+    smin = std::min(smin, std::max(G[m], C[m]));
+  }
+  // Where the GPU side's longest chain sets its time, a range of m ties: take the one that
+  // balances the GPU side's feed against the CPU side, leaving both slack.
+  double key = 1e300;
+  for (uint64_t m = 1; m < n; ++m) {
+    if (std::max(G[m], C[m]) > smin * (1 + kSplitTie)) continue;
+    const double k2 = std::max(F[m], C[m]);
+    if (k2 < key) {
+      key = k2;
+      best = Split{m, std::max(G[m], C[m]), G[m], C[m]};
+    }
+  }
+  return best;
+}
+
+// AUTO splits only parts in pinned memory, and only when the split is estimated at least this
+// much faster than the better single route: the GPU side of pinned parts needs no host
+// threads, so the CPU side has them all; a pageable or file GPU side needs them for staging.
+constexpr double kSplitGain = 0.95;
+
 // every non-empty part in page-locked host memory (hipPointerGetAttributes): the GPU route
 // DMAs them directly instead of staging
 bool all_pinned_parts(const uint8_t* const* parts, const uint64_t* lengths, uint64_t n) {
@@ -301,6 +374,57 @@ bool trace_route() {
   return on;
 }
 
+// Opens `path` for the CPU route and checks every range lies inside it.
+int open_ranges(const char* path, const uint64_t* offsets, const uint64_t* lengths, uint64_t n, int* fd_out) {
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return fail(S3H_EINVAL, "cpu route: cannot open %s", path);
+  struct stat st {};
+  int rc = fstat(fd, &st) == 0 ? S3H_OK : fail(S3H_EINVAL, "cpu route: cannot stat %s", path);
+  for (uint64_t i = 0; rc == S3H_OK && i < n; ++i)
+    if (lengths[i] > uint64_t(st.st_size) || offsets[i] > uint64_t(st.st_size) - lengths[i])
+      rc = fail(S3H_EINVAL, "cpu route: part %llu ends past the end of %s", (unsigned long long)i, path);
+  if (rc) close(fd);
+  else *fd_out = fd;
+  return rc;
+}
+
+// The split route: order[0, m) on the CPU drop-in (a thread of its own starting the CPU
+// route's threads), order[m, n) on the GPU host path from this thread; digests scattered back.
+int split_run(const uint8_t* const* parts, const char* path, const uint64_t* offsets,
+              const uint64_t* lengths, uint64_t n, uint32_t* digests, int ndevices,
+              const std::vector<uint64_t>& order, uint64_t m) {
+  const uint64_t ng = n - m;
+  std::vector<const uint8_t*> cp(parts ? m : 0), gp(parts ? ng : 0);
+  std::vector<uint64_t> co(path ? m : 0), go(path ? ng : 0), cl(m), gl(ng);
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint64_t i = order[k];
+    const bool cpu = k < m;
+    const uint64_t j = cpu ? k : k - m;
+    (cpu ? cl : gl)[j] = lengths[i];
+    if (parts) (cpu ? cp : gp)[j] = parts[i];
+    else (cpu ? co : go)[j] = offsets[i];
+  }
+  int fd = -1;
+  if (path)
+    if (int rc = open_ranges(path, co.data(), cl.data(), m, &fd)) return rc;
+  std::vector<uint32_t> cd(8 * m), gd(8 * ng);
+  int crc = S3H_OK;
+  std::string cerr;
+  std::thread cpu([&] {
+    crc = cpu_batch(parts ? cp.data() : nullptr, fd, co.data(), cl.data(), m, cd.data(), host_cpus());
+    if (crc) cerr = g_err;
+  });
+  const int grc = path ? s3h_sha256_file_parts(path, go.data(), gl.data(), ng, gd.data(), ndevices, 0)
+                       : s3h_sha256_batch_host(gp.data(), gl.data(), ng, gd.data(), ndevices, 0);
+  cpu.join();
+  if (fd >= 0) close(fd);
+  if (grc) return grc;  // this thread's last error already names it
+  if (crc) return fail(crc, "split route, cpu side: %s", cerr.c_str());
+  for (uint64_t k = 0; k < n; ++k)
+    std::memcpy(digests + 8 * order[k], (k < m ? cd.data() + 8 * k : gd.data() + 8 * (k - m)), 32);
+  return S3H_OK;
+}
+
 // The routed entry points: parts (fd < 0) or file ranges (fd >= 0, `path` for the GPU form).
 int routed(const uint8_t* const* parts, const char* path, const uint64_t* offsets,
            const uint64_t* lengths, uint64_t n, uint32_t* digests, int ndevices, int route,
@@ -308,39 +432,48 @@ int routed(const uint8_t* const* parts, const char* path, const uint64_t* offset
   if (taken) *taken = -1;
   if (!lengths || !digests || n == 0 || (!path && !parts) || (path && !offsets))
     return fail(S3H_EINVAL, "routed batch: null argument or n == 0");
-  if (route != S3H_ROUTE_GPU && route != S3H_ROUTE_CPU && route != S3H_ROUTE_AUTO)
+  if (route != S3H_ROUTE_GPU && route != S3H_ROUTE_CPU && route != S3H_ROUTE_AUTO && route != S3H_ROUTE_SPLIT)
     return fail(S3H_EINVAL, "routed batch: unknown route %d", route);
+  if (parts && route != S3H_ROUTE_GPU)
+    for (uint64_t i = 0; i < n; ++i)
+      if (!parts[i] && lengths[i]) return fail(S3H_EINVAL, "cpu route: part %llu is null", (unsigned long long)i);
   int use = route;
-  if (route == S3H_ROUTE_AUTO) {
+  std::vector<uint64_t> order;
+  Split sp;
+  if (route == S3H_ROUTE_AUTO || route == S3H_ROUTE_SPLIT) {
     const RouteModel& R = route_model();
     if (R.rc) return fail(R.rc, "%s", R.err.c_str());
     double g = 0, c = 0;
     const int source = path ? S3H_SOURCE_FILE : all_pinned_parts(parts, lengths, n) ? S3H_SOURCE_PINNED
                                                                                 : S3H_SOURCE_PAGEABLE;
-    use = route_choose(R.m, lengths, n, ndevices, source, &g, &c);
+    const int pick = route_choose(R.m, lengths, n, ndevices, source, &g, &c);
+    if (route == S3H_ROUTE_SPLIT || source == S3H_SOURCE_PINNED) {
+      order = longest_first(lengths, n);
+      sp = split_choose(R.m, lengths, n, ndevices, source, order);
+    }
+    if (route == S3H_ROUTE_SPLIT) use = sp.m ? S3H_ROUTE_SPLIT : S3H_ROUTE_GPU;  // one part: the GPU
+    else use = sp.m && sp.s < kSplitGain * std::min(g, c) ? S3H_ROUTE_SPLIT : pick;
     if (trace_route())
-      std::fprintf(stderr, "[s3h route] %llu parts (%s): gpu %.4f s, cpu %.4f s (%d threads) -> %s\n",
+      std::fprintf(stderr, "[s3h route] %llu parts (%s): gpu %.4f s, cpu %.4f s (%d threads), split %.4f s "
+                   "(%llu longest on the cpu) -> %s\n",
                    (unsigned long long)n, source == S3H_SOURCE_FILE ? "file" : source ? "pageable" : "pinned",
-                   g, c, R.m.cpu_threads, use == S3H_ROUTE_CPU ? "cpu" : "gpu");
+                   g, c, R.m.cpu_threads, sp.m ? sp.s : 0.0, (unsigned long long)sp.m,
+                   use == S3H_ROUTE_SPLIT ? "split" : use == S3H_ROUTE_CPU ? "cpu" : "gpu");
   }
   int rc;
-  if (use == S3H_ROUTE_GPU) {
+  if (use == S3H_ROUTE_SPLIT) {
+    rc = split_run(parts, path, offsets, lengths, n, digests, ndevices, order, sp.m);
+  } else if (use == S3H_ROUTE_GPU) {
     rc = path ? s3h_sha256_file_parts(path, offsets, lengths, n, digests, ndevices, 0)
               : s3h_sha256_batch_host(parts, lengths, n, digests, ndevices, 0);
   } else if (path) {
-    const int fd = open(path, O_RDONLY);
-    if (fd < 0) return fail(S3H_EINVAL, "cpu route: cannot open %s", path);
-    struct stat st {};
-    rc = fstat(fd, &st) == 0 ? S3H_OK : fail(S3H_EINVAL, "cpu route: cannot stat %s", path);
-    for (uint64_t i = 0; rc == S3H_OK && i < n; ++i)
-      if (lengths[i] > uint64_t(st.st_size) || offsets[i] > uint64_t(st.st_size) - lengths[i])
-        rc = fail(S3H_EINVAL, "cpu route: part %llu ends past the end of %s",
-                  (unsigned long long)i, path);
-    if (rc == S3H_OK) rc = cpu_batch(nullptr, fd, offsets, lengths, n, digests, host_cpus());
-    close(fd);
+    int fd = -1;
+    rc = open_ranges(path, offsets, lengths, n, &fd);
+    if (rc == S3H_OK) {
+      rc = cpu_batch(nullptr, fd, offsets, lengths, n, digests, host_cpus());
+      close(fd);
+    }
   } else {
-    for (uint64_t i = 0; i < n; ++i)
-      if (!parts[i] && lengths[i]) return fail(S3H_EINVAL, "cpu route: part %llu is null", (unsigned long long)i);
     rc = cpu_batch(parts, -1, nullptr, lengths, n, digests, host_cpus());
   }
   if (rc == S3H_OK && taken) *taken = use;
@@ -374,6 +507,21 @@ int s3h_route_estimate_ex(const s3h_route_model_t* m, const uint64_t* lengths, u
   if (!(m->cpu_bytes_per_s > 0 && m->chain_bytes_per_s > 0 && m->h2d_bytes_per_s > 0))
     return fail(S3H_EINVAL, "route estimate: the model's rates must be positive");
   return route_choose(*m, lengths, n, ndevices, source, gpu_s, cpu_s);
+}
+
+int s3h_route_split_estimate(const s3h_route_model_t* m, const uint64_t* lengths, uint64_t n,
+                             int ndevices, int source, uint64_t* cpu_parts, double* split_s) {
+  if (cpu_parts) *cpu_parts = 0;
+  if (split_s) *split_s = 0;
+  if (source < S3H_SOURCE_PINNED || source > S3H_SOURCE_FILE)
+    return fail(S3H_EINVAL, "route split estimate: unknown source %d", source);
+  if (!m || !lengths || n == 0) return fail(S3H_EINVAL, "route split estimate: bad argument");
+  if (!(m->cpu_bytes_per_s > 0 && m->chain_bytes_per_s > 0 && m->h2d_bytes_per_s > 0))
+    return fail(S3H_EINVAL, "route split estimate: the model's rates must be positive");
+  const Split sp = split_choose(*m, lengths, n, ndevices, source, longest_first(lengths, n));
+  if (cpu_parts) *cpu_parts = sp.m;
+  if (split_s) *split_s = sp.s;
+  return S3H_OK;
 }
 
 int s3h_sha256_batch_routed(const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,

@@ -479,10 +479,22 @@ def route_estimate(lengths, model: dict, ndevices: int = 0, pinned: bool = True,
     return _native.ROUTE_NAMES[r], g.value, c.value
 
 
+def route_split_estimate(lengths, model: dict, ndevices: int = 0, source: str = "pinned") -> tuple[int, float]:
+    """The split route's plan under ``model`` (s3h_route_split_estimate, pure host arithmetic):
+    (m, split_s) -- the m longest parts on the CPU, the rest on the GPU, estimated split_s s."""
+    m = _native.RouteModel(**model)
+    lens = _u64(lengths)
+    k, t = ctypes.c_uint64(), ctypes.c_double()
+    check(lib().s3h_route_split_estimate(ctypes.byref(m), _p64(lens), lens.size, ndevices,
+                                         _native.SOURCE_IDS[source], ctypes.byref(k), ctypes.byref(t)))
+    return k.value, t.value
+
+
 def sha256_batch_routed(parts: Sequence, ndevices: int = 0, route: str = "auto") -> tuple[np.ndarray, str]:
     """Host-resident parts hashed on the route given -- "gpu" (= sha256_batch_host), "cpu" (the
-    lib/hash drop-in on host threads) or "auto" (whichever the measured model says finishes
-    first; needs a GPU) -- s3h_sha256_batch_routed.  Returns ((n, 8) uint32, route taken)."""
+    lib/hash drop-in on host threads), "split" (the longest parts on the CPU, the rest on the
+    GPU, at once) or "auto" (whichever the measured model says finishes first; needs a GPU) --
+    s3h_sha256_batch_routed.  Returns ((n, 8) uint32, route taken)."""
     arrs, ptrs, lens = _host_parts(parts)
     out = np.zeros((len(arrs), DIGEST_WORDS), dtype=np.uint32)
     taken = ctypes.c_int(-1)

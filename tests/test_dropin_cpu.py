@@ -214,6 +214,9 @@ def test_route_auto_is_not_a_fallback():
         s3.sha256_batch_routed([b"abc"], route="auto")
     assert e.value.code == -2
     with pytest.raises(s3.S3HashError) as e:
+        s3.sha256_batch_routed([b"abc", b"de"], route="split")
+    assert e.value.code == -2
+    with pytest.raises(s3.S3HashError) as e:
         s3.route_model()
     assert e.value.code == -2
     from s3client_amd import _native

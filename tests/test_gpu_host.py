@@ -447,7 +447,8 @@ def test_device_queue_soak_mixed_calls(torch_cuda, tmp_path):
 
 def test_route_auto_by_batch_shape(torch_cuda, oracle, golden, tmp_path):
     """S3H_ROUTE_AUTO on a real GPU: the measured model is sane; 1,024 x 8 MiB C2 parts (pinned,
-    the bench metric's shape) go to the GPU and 8 x 8 MiB parts (a per-job batch of
+    the bench metric's shape) go to the GPU -- with the CPU drop-in beside it (the split
+    route) when the model says so -- and 8 x 8 MiB parts (a per-job batch of
     upload.cpp:89-110) go wherever the model estimates -- on a host with a few SHA-NI cores,
     the CPU.  Every digest equals the GPU-forced path's and the lib/hash fixtures."""
     torch = torch_cuda
@@ -469,8 +470,11 @@ def test_route_auto_by_batch_shape(torch_cuda, oracle, golden, tmp_path):
     fx = {e["p"]: e["digest"] for e in golden["c2_parts"]}
     want_route, g, c = s3.route_estimate([L] * n, m)
     assert want_route == "gpu", (g, c, m)
+    k, split_s = s3.route_split_estimate([L] * n, m)
     got, taken = s3.sha256_batch_routed(views, route="auto")
-    assert taken == "gpu"
+    # pinned C2 parts: the split (the CPU drop-in on part of them at once) when it is estimated
+    # 5 % faster than the GPU alone -- on the box's 16 SHA-NI threads it is
+    assert taken == ("split" if split_s < 0.95 * min(g, c) else "gpu"), (g, c, k, split_s)
     assert all(s3.hash_to_text(got[p]) == d for p, d in fx.items())
     small = views[:8]
     want_route, g, c = s3.route_estimate([L] * 8, m)
@@ -522,6 +526,40 @@ def test_route_auto_near_the_faster_route(torch_cuda):
         med = {r: float(np.median(v)) for r, v in t.items()}
         assert med["auto"] <= 1.10 * min(med["gpu"], med["cpu"]), (k, med, m)
     buf.close()
+
+
+@pytest.mark.parametrize("layout", ["pinned", "pageable", "file"])
+def test_route_split_vs_oracle(torch_cuda, oracle, tmp_path, layout):
+    """S3H_ROUTE_SPLIT: the longest parts on the CPU drop-in while the GPU host path hashes the
+    rest, at once -- ragged parts (empty, a few bytes, up to 6 MiB, in shuffled order),
+    pinned, pageable and file ranges: every digest vs the oracle, the route reported, and the
+    CPU side's share the model's plan (s3h_route_split_estimate).  One part is not split."""
+    torch = torch_cuda
+    rng = np.random.default_rng(4242 + len(layout))
+    n = 600
+    lens = rng.integers(0, 6 << 20, n).astype(np.uint64)
+    lens[:5] = [0, 1, 63, 64, 0]
+    lens = lens[rng.permutation(n)]
+    offs = np.concatenate([[0], np.cumsum(lens + 7)[:-1]]).astype(np.uint64)
+    total = int(offs[-1] + lens[-1]) + 64
+    src = rng.integers(0, 256, total, dtype=np.uint8)
+    want = oracle.batch(src, offs, lens, threads=16)
+    k, _ = s3.route_split_estimate(lens, s3.route_model(), source=layout)
+    assert 0 < k < n
+    if layout == "file":
+        path = tmp_path / "split.bin"
+        src.tofile(path)
+        got, taken = s3.sha256_file_parts_routed(str(path), offs, lens, route="split")
+        one, taken1 = s3.sha256_file_parts_routed(str(path), offs[:1], lens[:1], route="split")
+    else:
+        buf = torch.empty(total, dtype=torch.uint8, pin_memory=layout == "pinned")
+        buf.numpy()[:] = src
+        got, taken = s3.sha256_batch_routed(s3.BufferParts(buf, offs, lens), route="split")
+        one, taken1 = s3.sha256_batch_routed(s3.BufferParts(buf, offs[:1], lens[:1]), route="split")
+    assert taken == "split" and taken1 == "gpu"
+    bad = np.flatnonzero((got != want).any(axis=1))
+    assert bad.size == 0, (layout, bad[:8])
+    assert np.array_equal(one, want[:1])
 
 
 def test_dual_digest_host_beyond_one_grid(torch_cuda, oracle):

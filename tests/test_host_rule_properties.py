@@ -94,3 +94,61 @@ def test_route_estimate_is_monotone_in_the_batch(n, part):
     _, g1, c1 = s3.route_estimate([part] * n, MODEL)
     _, g2, c2 = s3.route_estimate([part] * (n + 1), MODEL)
     assert g2 >= g1 and c2 >= c1
+
+
+def split_ref(lengths, m, ndevices=1, source="pinned"):
+    """The split route's plan restated (include/s3hash.h s3h_route_split_estimate): parts by
+    length descending (ties by index), the first k on the CPU, the rest on the GPU."""
+    n = len(lengths)
+    order = sorted(range(n), key=lambda i: -lengths[i])
+    total = sum(lengths)
+    feed = m["h2d_bytes_per_s"] if source == "pinned" else min(m["h2d_bytes_per_s"], m["staged_bytes_per_s"])
+    kmax = min(n, m["cpu_threads"])
+    cap = min(ndevices, m["devices"]) if ndevices > 0 else m["devices"]
+    rows = []
+    for k in range(1, n):
+        cpu = [lengths[order[i]] for i in range(k)]
+        t = min(k, kmax)
+        per_thread = min(t * m["cpu_bytes_per_s"], m["cpu_all_bytes_per_s"]) / t
+        c = lpt(cpu, kmax) / per_thread
+        devs = max(1, min(n - k, cap))
+        f = (total - sum(cpu)) / devs / feed
+        g = m["call_s"] + max(lengths[order[k]] / m["chain_bytes_per_s"], f)
+        rows.append((k, max(g, c), max(f, c)))
+    smin = min(r[1] for r in rows)
+    k, s_, _ = min((r for r in rows if r[1] <= smin * 1.005), key=lambda r: r[2])
+    return s_, k
+
+
+@settings(max_examples=80, deadline=None)
+@given(st.lists(st.integers(0, 64 * MIB), min_size=1, max_size=60), st.integers(1, 24),
+       st.integers(1, 8), st.sampled_from(["pinned", "pageable", "file"]))
+def test_route_split_estimate_matches_its_formula(lengths, threads, devices, source):
+    """The split plan is exactly the documented rule (the balanced m among those within 0.5 %
+    of the minimum estimate), and a single part is not split."""
+    m = {**MODEL, "cpu_threads": threads, "devices": devices}
+    k, s_ = s3.route_split_estimate(lengths, m, source=source)
+    if len(lengths) == 1:
+        assert (k, s_) == (0, 0.0)
+        return
+    want_s, want_k = split_ref(lengths, m, source=source)
+    assert 1 <= k < len(lengths)
+    assert np.isclose(s_, want_s, rtol=1e-12, atol=1e-15)
+    assert k == want_k
+
+
+def test_route_split_on_c2_shapes():
+    """C2 from pinned memory under the box's measured rates (profiles/r05_route_sweep.json): the
+    split beats both single routes, bounded below by one 8 MiB chain; a batch of 8 parts (one
+    job of upload.cpp) gains nothing from the GPU side."""
+    m = dict(MODEL, cpu_bytes_per_s=2.4e9, cpu_all_bytes_per_s=39e9, chain_bytes_per_s=69e6,
+             h2d_bytes_per_s=56e9, cpu_threads=16)
+    lens = [8 * MIB] * 1024
+    route, g, c = s3.route_estimate(lens, m)
+    k, s_ = s3.route_split_estimate(lens, m)
+    assert route == "gpu" and s_ < 0.85 * min(g, c)
+    assert s_ >= 8 * MIB / m["chain_bytes_per_s"]
+    assert 350 < k < 500  # the feed balanced against the CPU side: 8 GiB x 39 / (39 + 56)
+    route, g, c = s3.route_estimate(lens[:8], m)
+    k, s_ = s3.route_split_estimate(lens[:8], m)
+    assert route == "cpu" and s_ >= c

@@ -15,6 +15,10 @@ for k in ("parity", "status", "fixture_mismatches"):
 for k in ("host_resident", "cpu_baseline"):
     if isinstance(line.get(k), dict):
         out.append(f"{k} {line[k].get('value')}")
+hr = line.get("host_resident") if isinstance(line.get("host_resident"), dict) else {}
+for k in ("split", "stream"):
+    if isinstance(hr.get(k), dict):
+        out.append(f"host_resident.{k} {hr[k].get('GiBps')}")
 if isinstance(line.get("configs"), dict):
     out.append("configs " + " ".join(f"{c}={v.get('GiBps')}" for c, v in line["configs"].items()))
 if isinstance(line.get("c4"), dict):

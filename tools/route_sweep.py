@@ -3,10 +3,11 @@
 
 For n in {8, 32, 64, 128, 256, 512, 1024} parts of 8 MiB (C2 parts 0..n-1, generator G), from
 pinned host memory (on the device's node) and from pageable memory, time
-s3h_sha256_batch_routed with route gpu, cpu and auto, round-robin (`--reps` timed calls each
-after one warm call), and record the model's two estimates and AUTO's choice beside the
-measured medians.  Every digest must equal the device-resident run's.  One JSON object on
-stdout; `auto_over_best` = AUTO's median / min(gpu, cpu) medians (the bar: <= 1.10).
+s3h_sha256_batch_routed with route gpu, cpu, split (the longest parts on the CPU while the
+GPU hashes the rest) and auto, round-robin (`--reps` timed calls each after one warm call),
+and record the model's estimates and AUTO's choice beside the measured medians.  Every digest
+must equal the device-resident run's.  One JSON object on stdout; `auto_over_best` = AUTO's
+median / the fastest forced route's (the bar: <= 1.10).
 
     python3 tools/route_sweep.py [--reps 3] [--ns 8,32,...]
 """
@@ -64,7 +65,8 @@ def main():
         for n in ns:
             parts = s3.BufferParts(arr, offs[:n], lens[:n])
             est_route, g_est, c_est = s3.route_estimate(lens[:n], model, pinned=src == "pinned")
-            times = {r: [] for r in ("gpu", "cpu", "auto")}
+            k_est, s_est = s3.route_split_estimate(lens[:n], model, source=src)
+            times = {r: [] for r in ("gpu", "cpu", "split", "auto")}
             taken = None
             for k in range(a.reps + 1):
                 for r in times:
@@ -77,17 +79,19 @@ def main():
                         taken = tk
                     out["mismatches"] += int(not np.array_equal(d, ref[:n]))
             med = {r: float(np.median(v)) for r, v in times.items()}
-            ratio = med["auto"] / min(med["gpu"], med["cpu"])
+            ratio = med["auto"] / min(med["gpu"], med["cpu"], med["split"])
             worst = max(worst, ratio)
             out["rows"].append({
                 "source": src, "n": n, "GiB": round(n * L / 2**30, 3),
                 "median_s": {r: round(v, 4) for r, v in med.items()},
                 "all_s": {r: [round(x, 4) for x in v] for r, v in times.items()},
-                "auto_taken": taken, "faster": min(("gpu", "cpu"), key=lambda r: med[r]),
+                "GiBps": {r: round(n * L / 2**30 / v, 2) for r, v in med.items()},
+                "auto_taken": taken, "faster": min(("gpu", "cpu", "split"), key=lambda r: med[r]),
                 "auto_over_best": round(ratio, 4),
-                "model": {"route": est_route, "gpu_s": round(g_est, 4), "cpu_s": round(c_est, 4)}})
-            print(f"[route_sweep] {src} n={n}: gpu {med['gpu']:.4f} cpu {med['cpu']:.4f} "
-                  f"auto {med['auto']:.4f} ({taken}) model gpu {g_est:.4f} cpu {c_est:.4f}",
+                "model": {"route": est_route, "gpu_s": round(g_est, 4), "cpu_s": round(c_est, 4),
+                          "split_s": round(s_est, 4), "split_cpu_parts": k_est}})
+            print(f"[route_sweep] {src} n={n}: gpu {med['gpu']:.4f} cpu {med['cpu']:.4f} split {med['split']:.4f} "
+                  f"auto {med['auto']:.4f} ({taken}) model gpu {g_est:.4f} cpu {c_est:.4f} split {s_est:.4f} ({k_est})",
                   file=sys.stderr, flush=True)
     out["worst_auto_over_best"] = round(worst, 4)
     print(json.dumps(out))
