@@ -881,7 +881,7 @@ def split_from_host(s3, parts, lens, gd, reps: int = 3) -> dict:
         out, taken = s3.sha256_batch_routed(parts, ndevices=1, route="split")
         times.append(time.perf_counter() - t0)
     model = s3.route_model()
-    k, est = s3.route_split_estimate(lens, model, ndevices=1)
+    k, _, est = s3.route_split_estimate(lens, model, ndevices=1)
     auto_out, auto_taken = s3.sha256_batch_routed(parts, ndevices=1, route="auto")
     return {"metric": "host-resident SHA-256 GiB/s, GPU host path and CPU drop-in at once (S3H_ROUTE_SPLIT)",
             "GiBps": round(gib / float(np.mean(times)), 3), "ms_per_batch": round(1e3 * float(np.mean(times)), 2),

@@ -283,9 +283,9 @@ int s3h_sha256_md5_batch_device(int device, const void *d_base, const uint64_t *
  * is never a fallback for a missing device.
  * S3H_ROUTE_SPLIT = both at once: the CPU drop-in hashes the m longest parts on its threads
  * while the GPU host path hashes the rest (m from the model, s3h_route_split_estimate; a single
- * part goes to the GPU); AUTO also splits parts that are all in pinned memory when the split
- * is estimated at least 5 % faster than the better single route (a pageable or file GPU side
- * needs the host threads for staging, so AUTO does not split those).
+ * part goes to the GPU; for pageable parts and file ranges the host threads are divided
+ * between the GPU side's staging and the CPU side, s3h_route_split_estimate); AUTO also
+ * splits when the split is estimated at least 5 % faster than the better single route.
  * *taken (if non-null) receives the route that ran (S3H_ROUTE_GPU, _CPU or _SPLIT).
  *   gpu_s = call_s + max(longest part / chain rate, bytes per device / feed rate)
  *           feed = h2d (pinned parts) or min(h2d, staged) (pageable parts, file ranges)
@@ -322,9 +322,14 @@ int s3h_route_estimate_ex(const s3h_route_model_t *m, const uint64_t *lengths, u
  * (gpu_s / cpu_s as above on each side's parts); of the m with split_s(m) within 0.5 % of the
  * minimum (the GPU side's longest chain makes ranges of m tie), *cpu_parts = the one with the
  * smallest max(GPU side's bytes / devices / feed, cpu_s(m)), and *split_s = split_s(it)
- * (*cpu_parts = 0 when n == 1). */
+ * (*cpu_parts = 0 when n == 1).  Pinned parts: the CPU side gets all cpu_threads threads
+ * (*stage_threads = 0).  Pageable parts / file ranges: each GPU shard stages with
+ * *stage_threads = tg threads, fed at min(H2D, staged rate x tg / threads), and the CPU side
+ * gets the rest at the all-threads rate per thread; tg is the best of threads x {1, 4, 6, 8, 9}
+ * / 12 (env S3H_SPLIT_STAGE_THREADS fixes it). */
 int s3h_route_split_estimate(const s3h_route_model_t *m, const uint64_t *lengths, uint64_t n,
-                             int ndevices, int source, uint64_t *cpu_parts, double *split_s);
+                             int ndevices, int source, uint64_t *cpu_parts, int *stage_threads,
+                             double *split_s);
 int s3h_sha256_batch_routed(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                             uint32_t *digests, int ndevices, int route, int *taken);
 int s3h_sha256_file_parts_routed(const char *path, const uint64_t *offsets,

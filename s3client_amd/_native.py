@@ -201,6 +201,7 @@ def lib() -> ctypes.CDLL:
             L.s3h_route_split_estimate.argtypes = [ctypes.POINTER(RouteModel), u64p, ctypes.c_uint64,
                                                    ctypes.c_int, ctypes.c_int,
                                                    ctypes.POINTER(ctypes.c_uint64),
+                                                   ctypes.POINTER(ctypes.c_int),
                                                    ctypes.POINTER(ctypes.c_double)]
             L.s3h_sha256_batch_routed.argtypes = [ctypes.POINTER(ctypes.c_void_p), u64p,
                                                   ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,

@@ -1177,7 +1177,18 @@ struct HostShard {
   int device;
   int ndevices;  // shards running concurrently (host threads are split between them)
   std::vector<uint64_t> parts;  // global part indices on this device
+  unsigned threads = 0;  // staging threads cap (0: host_threads_per_device); the split route's
+                         // GPU side leaves the rest of the CPUs to its CPU side
 };
+
+// The calling thread's staging-thread cap for the host batches it starts (the split route
+// sets it around its GPU side; batch_host_on copies it into the shards).
+thread_local unsigned g_stage_threads_cap = 0;
+
+unsigned shard_threads(const HostShard& sh) {
+  const unsigned t = host_threads_per_device(sh.ndevices);
+  return sh.threads ? std::max(1u, std::min(sh.threads, t)) : t;
+}
 
 // Many small parts: slicing every part (run_host_shard) would cut them into slices of a few
 // hundred bytes (the staging slot holds n slices) or issue one DMA per part and slice, so
@@ -1267,7 +1278,7 @@ int run_host_groups(HostCtx& C, const HostShard& sh, const int* algos, int nalgo
     }
   for (int a = 0; a < nalgo; ++a)
     HIP_TRY(C.ensure_digests(a, n * digest_words(algos[a]) * sizeof(uint32_t)));
-  CopyPool* pool = any_staged ? C.ensure_pool(host_threads_per_device(sh.ndevices) - 1) : nullptr;
+  CopyPool* pool = any_staged ? C.ensure_pool(shard_threads(sh) - 1) : nullptr;
   std::vector<uint64_t> offs;
   for (uint64_t k = 0; k < ngroups; ++k) {
     const int q = int(k & 1);
@@ -1380,8 +1391,8 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
     const uint64_t ns = small.size();
     if ((staged && ns > 2048) || (!staged && !uniform && ns > 64 && small_total < ns * (256ull << 10))) {
       if (large.empty()) return run_host_groups(C, sh, algos, nalgo, src, lengths, digests, !staged);
-      const HostShard hs{sh.device, sh.ndevices, std::move(small)};
-      const HostShard hl{sh.device, sh.ndevices, std::move(large)};
+      const HostShard hs{sh.device, sh.ndevices, std::move(small), sh.threads};
+      const HostShard hl{sh.device, sh.ndevices, std::move(large), sh.threads};
       if (int rc = run_host_groups(C, hs, algos, nalgo, src, lengths, digests, !staged)) return rc;
       return run_host_shard(C, hl, algos, nalgo, src, lengths, digests, 0);
     }
@@ -1435,7 +1446,7 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
     max_blocks = std::max(max_blocks, C.plan[a]->max_blocks);
   }
   CopyPool* pool = nullptr;
-  const unsigned threads = host_threads_per_device(sh.ndevices);  // the caller + workers
+  const unsigned threads = shard_threads(sh);  // the caller + workers
   if (staged) pool = C.ensure_pool(threads - 1);
   const uint64_t bps = slice / 64;  // blocks per slice
   s3h_plan_s* P0 = C.plan[0];
@@ -1564,7 +1575,7 @@ int run_host_shard_passes(HostCtx& C, const HostShard& sh, const int* algos, int
   for (uint64_t s = 0; s < sh.parts.size(); s += kMaxStagedRefs) {
     const uint64_t e = std::min<uint64_t>(sh.parts.size(), s + kMaxStagedRefs);
     HostShard sub{sh.device, sh.ndevices,
-                  std::vector<uint64_t>(sh.parts.begin() + s, sh.parts.begin() + e)};
+                  std::vector<uint64_t>(sh.parts.begin() + s, sh.parts.begin() + e), sh.threads};
     if (int rc = run_host_shard(C, sub, algos, nalgo, src, lengths, digests, slice)) return rc;
   }
   return S3H_OK;
@@ -1973,11 +1984,12 @@ int run_merged(HostCtx* C, const std::vector<HostReq*>& batch) {
   } else {
     uint64_t m = 0;
     bool mem = true;
-    HostShard sh{f.sh->device, 1, {}};
+    HostShard sh{f.sh->device, 1, {}, f.sh->threads};
     for (const HostReq* r : batch) {
       m += r->sh->parts.size();
       mem = mem && r->src->parts;
       sh.ndevices = std::max(sh.ndevices, r->sh->ndevices);
+      sh.threads = sh.threads && r->sh->threads ? std::max(sh.threads, r->sh->threads) : 0;  // 0 = no cap
     }
     std::vector<uint64_t> lens(m);
     std::vector<const uint8_t*> ptrs(mem ? m : 0);
@@ -2353,7 +2365,7 @@ static int batch_host_on(const int* algos, int nalgo, const PartSource& src,
       if (!src.parts[i] && lengths[i]) return fail(S3H_EINVAL, "batch_host: part %llu is null", (unsigned long long)i);
   const int nshards = int(std::min<uint64_t>(devs.size(), n));
   std::vector<HostShard> shards(nshards);
-  for (int k = 0; k < nshards; ++k) shards[k] = {devs[k], nshards, {}};
+  for (int k = 0; k < nshards; ++k) shards[k] = {devs[k], nshards, {}, g_stage_threads_cap};
   for (uint64_t i = 0; i < n; ++i) shards[i % nshards].parts.push_back(i);
   std::vector<int> rcs(nshards, S3H_OK);
   std::vector<std::string> errs(nshards);

@@ -298,47 +298,80 @@ int route_choose(const s3h_route_model_t& m, const uint64_t* lengths, uint64_t n
 // with gpu_s / cpu_s the estimates above on each side's parts; among the m within 0.5 % of the
 // minimum, the one with the smallest max(GPU side's bytes / feed, cpu_s).  Parts are ordered by length,
 // descending (ties: lower index first); the CPU side's longest-first schedule is built
-// incrementally as m grows (exact LPT).
+// incrementally as m grows (exact LPT; the fluid bound beyond 4,096 parts).
 constexpr double kSplitTie = 0.005;  // estimates within 0.5 % of the minimum tie
 
 struct Split {
-  uint64_t m = 0;   // parts on the CPU: order[0, m) (0 only for a single part)
+  uint64_t m = 0;   // parts on the CPU: order[0, m) (0: no split, e.g. a single part)
+  unsigned tg = 0;  // staging threads of each GPU shard (0: pinned parts, no staging)
   double s = 0, g = 0, c = 0;
 };
 
 std::vector<uint64_t> longest_first(const uint64_t* lengths, uint64_t n) {
   std::vector<uint64_t> order(n);
+  uint64_t longest = 0;
+  bool equal = true;
+  for (uint64_t i = 0; i < n; ++i) {
+    longest = std::max(longest, lengths[i]);
+    equal = equal && lengths[i] == lengths[0];
+  }
+  constexpr int kIdxBits = 24, kLenBits = 40;
+  if (!equal && n < (1ull << kIdxBits) && longest < (1ull << kLenBits)) {
+    // one key per part, (complemented length, index): a plain sort of integers
+    for (uint64_t i = 0; i < n; ++i) order[i] = (((1ull << kLenBits) - 1 - lengths[i]) << kIdxBits) | i;
+    std::sort(order.begin(), order.end());
+    for (uint64_t& x : order) x &= (1ull << kIdxBits) - 1;
+    return order;
+  }
   std::iota(order.begin(), order.end(), 0);
-  std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return lengths[a] > lengths[b]; });
+  if (!equal)
+    std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return lengths[a] > lengths[b]; });
   return order;
 }
 
-Split split_choose(const s3h_route_model_t& M, const uint64_t* lengths, uint64_t n, int ndevices,
-                   int source, const std::vector<uint64_t>& order) {
+// The best m for a given split of the host threads: pinned parts (tg = 0) leave all T threads
+// to the CPU side; staged parts give tg threads to each of the GPU side's device shards, which
+// feed it at min(H2D, staged rate x tg / T), and the rest to the CPU side, whose threads then
+// run at the all-threads rate per thread (every CPU busy).
+Split split_choose(const s3h_route_model_t& M, const uint64_t* sorted, uint64_t n, int ndevices,
+                   int source, unsigned tg, std::vector<double> (&ws)[3]) {
   Split best;
   if (n < 2) return best;
+  const unsigned T = unsigned(std::max(1, M.cpu_threads));
+  const int dev_cap = std::max(1, ndevices > 0 ? std::min(ndevices, M.devices) : M.devices);
+  const bool staged = source != S3H_SOURCE_PINNED;
+  if (!staged) tg = 0;
+  else if (tg == 0 || uint64_t(tg) * unsigned(dev_cap) >= T) return best;
+  const unsigned tc = staged ? T - tg * unsigned(dev_cap) : T;  // CPU side's threads
   uint64_t total = 0;
-  for (uint64_t i = 0; i < n; ++i) total += lengths[i];
-  const double feed = source == S3H_SOURCE_PINNED || !(M.staged_bytes_per_s > 0)
-                          ? M.h2d_bytes_per_s : std::min(M.h2d_bytes_per_s, M.staged_bytes_per_s);
-  const uint64_t kmax = std::min<uint64_t>(n, uint64_t(std::max(1, M.cpu_threads)));
-  const int dev_cap = ndevices > 0 ? std::min(ndevices, M.devices) : M.devices;
-  std::vector<double> load(kmax, 0.0);  // min-heap of the CPU threads' loads (bytes)
-  std::vector<double> G(n), C(n), F(n);  // per m: gpu_s, cpu_s, the GPU side's feed time
+  for (uint64_t i = 0; i < n; ++i) total += sorted[i];
+  const double feed = !staged || !(M.staged_bytes_per_s > 0)
+                          ? M.h2d_bytes_per_s : std::min(M.h2d_bytes_per_s, M.staged_bytes_per_s * tg / T);
+  const uint64_t kmax = std::min<uint64_t>(n, tc);
+  // exact longest-first schedule up to 4,096 parts, the fluid bound beyond (as route_choose)
+  const bool exact = n <= 4096;
+  std::vector<double> load(exact ? kmax : 0, 0.0);  // min-heap of the CPU threads' loads (bytes)
+  std::vector<double>& G = ws[0]; std::vector<double>& C = ws[1]; std::vector<double>& F = ws[2];
+  for (auto& v : ws) v.resize(n);  // per m: gpu_s, cpu_s, the GPU side's feed time
   double makespan = 0, smin = 1e300;
   uint64_t cpu_bytes = 0;
   for (uint64_t m = 1; m < n; ++m) {
-    const uint64_t x = lengths[order[m - 1]];
-    std::pop_heap(load.begin(), load.end(), std::greater<double>());
-    load.back() += double(x);
-    makespan = std::max(makespan, load.back());
-    std::push_heap(load.begin(), load.end(), std::greater<double>());
+    const uint64_t x = sorted[m - 1];
     cpu_bytes += x;
     const uint64_t k = std::min(m, kmax);
-    const double c = makespan / (cpu_rate(M, double(k)) / double(k));
-    const int devs = std::max(1, int(std::min<uint64_t>(n - m, uint64_t(std::max(1, dev_cap)))));
+    if (exact) {
+      std::pop_heap(load.begin(), load.end(), std::greater<double>());
+      load.back() += double(x);
+      makespan = std::max(makespan, load.back());
+      std::push_heap(load.begin(), load.end(), std::greater<double>());
+    } else {
+      makespan = std::max(double(cpu_bytes) / double(k), double(sorted[0]));
+    }
+    const double per_thread = staged ? cpu_rate(M, double(T)) / double(T) : cpu_rate(M, double(k)) / double(k);
+    const double c = makespan / per_thread;
+    const int devs = std::max(1, int(std::min<uint64_t>(n - m, uint64_t(dev_cap))));
     F[m] = double(total - cpu_bytes) / devs / feed;
-    G[m] = M.call_s + std::max(double(lengths[order[m]]) / M.chain_bytes_per_s, F[m]);
+    G[m] = M.call_s + std::max(double(sorted[m]) / M.chain_bytes_per_s, F[m]);
     C[m] = c;
     smin = std::min(smin, std::max(G[m], C[m]));
   }
@@ -350,15 +383,39 @@ Split split_choose(const s3h_route_model_t& M, const uint64_t* lengths, uint64_t
     const double k2 = std::max(F[m], C[m]);
     if (k2 < key) {
       key = k2;
-      best = Split{m, std::max(G[m], C[m]), G[m], C[m]};
+      best = Split{m, tg, std::max(G[m], C[m]), G[m], C[m]};
     }
   }
   return best;
 }
 
-// AUTO splits only parts in pinned memory, and only when the split is estimated at least this
-// much faster than the better single route: the GPU side of pinned parts needs no host
-// threads, so the CPU side has them all; a pageable or file GPU side needs them for staging.
+// The split plan: pinned parts need no staging threads; staged parts (pageable, file ranges)
+// try tg = T/4, T/3, T/2, 2T/3, 3T/4 staging threads per GPU shard and keep the fastest
+// estimate (S3H_SPLIT_STAGE_THREADS fixes tg, for measurements).
+Split split_plan(const s3h_route_model_t& M, const uint64_t* lengths, uint64_t n, int ndevices,
+                 int source, const std::vector<uint64_t>& order) {
+  std::vector<double> ws[3];
+  std::vector<uint64_t> sorted(n);  // the lengths in `order`
+  for (uint64_t k = 0; k < n; ++k) sorted[k] = lengths[order[k]];
+  if (source == S3H_SOURCE_PINNED) return split_choose(M, sorted.data(), n, ndevices, source, 0, ws);
+  const unsigned T = unsigned(std::max(1, M.cpu_threads));
+  std::vector<unsigned> cand;
+  if (const char* e = std::getenv("S3H_SPLIT_STAGE_THREADS")) cand.push_back(unsigned(std::max(1, std::atoi(e))));
+  else
+    for (unsigned num : {1u, 4u, 6u, 8u, 9u}) {  // x T / 12: T/12 ... 3T/4
+      const unsigned t = std::max(1u, T * num / 12);
+      if (std::find(cand.begin(), cand.end(), t) == cand.end()) cand.push_back(t);
+    }
+  Split best;
+  for (unsigned t : cand) {
+    const Split sp = split_choose(M, sorted.data(), n, ndevices, source, t, ws);
+    if (sp.m && (!best.m || sp.s < best.s)) best = sp;
+  }
+  return best;
+}
+
+// AUTO splits only when the split is estimated at least this much faster than the better
+// single route.
 constexpr double kSplitGain = 0.95;
 
 // every non-empty part in page-locked host memory (hipPointerGetAttributes): the GPU route
@@ -392,8 +449,8 @@ int open_ranges(const char* path, const uint64_t* offsets, const uint64_t* lengt
 // route's threads), order[m, n) on the GPU host path from this thread; digests scattered back.
 int split_run(const uint8_t* const* parts, const char* path, const uint64_t* offsets,
               const uint64_t* lengths, uint64_t n, uint32_t* digests, int ndevices,
-              const std::vector<uint64_t>& order, uint64_t m) {
-  const uint64_t ng = n - m;
+              const std::vector<uint64_t>& order, const Split& sp) {
+  const uint64_t m = sp.m, ng = n - m;
   std::vector<const uint8_t*> cp(parts ? m : 0), gp(parts ? ng : 0);
   std::vector<uint64_t> co(path ? m : 0), go(path ? ng : 0), cl(m), gl(ng);
   for (uint64_t k = 0; k < n; ++k) {
@@ -410,12 +467,19 @@ int split_run(const uint8_t* const* parts, const char* path, const uint64_t* off
   std::vector<uint32_t> cd(8 * m), gd(8 * ng);
   int crc = S3H_OK;
   std::string cerr;
+  int count = 1;
+  (void)hipGetDeviceCount(&count);
+  const unsigned T = host_cpus();
+  const unsigned devs = unsigned(std::max(1, ndevices > 0 ? std::min(ndevices, count) : count));
+  const unsigned tc = sp.tg && uint64_t(sp.tg) * devs < T ? T - sp.tg * devs : T;
   std::thread cpu([&] {
-    crc = cpu_batch(parts ? cp.data() : nullptr, fd, co.data(), cl.data(), m, cd.data(), host_cpus());
+    crc = cpu_batch(parts ? cp.data() : nullptr, fd, co.data(), cl.data(), m, cd.data(), tc);
     if (crc) cerr = g_err;
   });
+  g_stage_threads_cap = sp.tg;  // the GPU side's staging threads (0: uncapped)
   const int grc = path ? s3h_sha256_file_parts(path, go.data(), gl.data(), ng, gd.data(), ndevices, 0)
                        : s3h_sha256_batch_host(gp.data(), gl.data(), ng, gd.data(), ndevices, 0);
+  g_stage_threads_cap = 0;
   cpu.join();
   if (fd >= 0) close(fd);
   if (grc) return grc;  // this thread's last error already names it
@@ -447,22 +511,28 @@ int routed(const uint8_t* const* parts, const char* path, const uint64_t* offset
     const int source = path ? S3H_SOURCE_FILE : all_pinned_parts(parts, lengths, n) ? S3H_SOURCE_PINNED
                                                                                 : S3H_SOURCE_PAGEABLE;
     const int pick = route_choose(R.m, lengths, n, ndevices, source, &g, &c);
-    if (route == S3H_ROUTE_SPLIT || source == S3H_SOURCE_PINNED) {
+    // AUTO skips the plan when even a perfect split -- the GPU side fed at the H2D rate on every
+    // device, the CPU side at its all-threads rate -- could not beat the better route by 5 %
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i) total += lengths[i];
+    const int dev_cap = std::max(1, ndevices > 0 ? std::min(ndevices, R.m.devices) : R.m.devices);
+    const double bound = double(total) / (dev_cap * R.m.h2d_bytes_per_s + cpu_rate(R.m, R.m.cpu_threads));
+    if (route == S3H_ROUTE_SPLIT || bound < kSplitGain * std::min(g, c)) {
       order = longest_first(lengths, n);
-      sp = split_choose(R.m, lengths, n, ndevices, source, order);
+      sp = split_plan(R.m, lengths, n, ndevices, source, order);
     }
     if (route == S3H_ROUTE_SPLIT) use = sp.m ? S3H_ROUTE_SPLIT : S3H_ROUTE_GPU;  // one part: the GPU
     else use = sp.m && sp.s < kSplitGain * std::min(g, c) ? S3H_ROUTE_SPLIT : pick;
     if (trace_route())
       std::fprintf(stderr, "[s3h route] %llu parts (%s): gpu %.4f s, cpu %.4f s (%d threads), split %.4f s "
-                   "(%llu longest on the cpu) -> %s\n",
+                   "(%llu longest on the cpu, %u staging threads per gpu) -> %s\n",
                    (unsigned long long)n, source == S3H_SOURCE_FILE ? "file" : source ? "pageable" : "pinned",
-                   g, c, R.m.cpu_threads, sp.m ? sp.s : 0.0, (unsigned long long)sp.m,
+                   g, c, R.m.cpu_threads, sp.m ? sp.s : 0.0, (unsigned long long)sp.m, sp.tg,
                    use == S3H_ROUTE_SPLIT ? "split" : use == S3H_ROUTE_CPU ? "cpu" : "gpu");
   }
   int rc;
   if (use == S3H_ROUTE_SPLIT) {
-    rc = split_run(parts, path, offsets, lengths, n, digests, ndevices, order, sp.m);
+    rc = split_run(parts, path, offsets, lengths, n, digests, ndevices, order, sp);
   } else if (use == S3H_ROUTE_GPU) {
     rc = path ? s3h_sha256_file_parts(path, offsets, lengths, n, digests, ndevices, 0)
               : s3h_sha256_batch_host(parts, lengths, n, digests, ndevices, 0);
@@ -510,16 +580,19 @@ int s3h_route_estimate_ex(const s3h_route_model_t* m, const uint64_t* lengths, u
 }
 
 int s3h_route_split_estimate(const s3h_route_model_t* m, const uint64_t* lengths, uint64_t n,
-                             int ndevices, int source, uint64_t* cpu_parts, double* split_s) {
+                             int ndevices, int source, uint64_t* cpu_parts, int* stage_threads,
+                             double* split_s) {
   if (cpu_parts) *cpu_parts = 0;
+  if (stage_threads) *stage_threads = 0;
   if (split_s) *split_s = 0;
   if (source < S3H_SOURCE_PINNED || source > S3H_SOURCE_FILE)
     return fail(S3H_EINVAL, "route split estimate: unknown source %d", source);
   if (!m || !lengths || n == 0) return fail(S3H_EINVAL, "route split estimate: bad argument");
   if (!(m->cpu_bytes_per_s > 0 && m->chain_bytes_per_s > 0 && m->h2d_bytes_per_s > 0))
     return fail(S3H_EINVAL, "route split estimate: the model's rates must be positive");
-  const Split sp = split_choose(*m, lengths, n, ndevices, source, longest_first(lengths, n));
+  const Split sp = split_plan(*m, lengths, n, ndevices, source, longest_first(lengths, n));
   if (cpu_parts) *cpu_parts = sp.m;
+  if (stage_threads) *stage_threads = int(sp.tg);
   if (split_s) *split_s = sp.s;
   return S3H_OK;
 }

@@ -479,15 +479,18 @@ def route_estimate(lengths, model: dict, ndevices: int = 0, pinned: bool = True,
     return _native.ROUTE_NAMES[r], g.value, c.value
 
 
-def route_split_estimate(lengths, model: dict, ndevices: int = 0, source: str = "pinned") -> tuple[int, float]:
+def route_split_estimate(lengths, model: dict, ndevices: int = 0,
+                         source: str = "pinned") -> tuple[int, int, float]:
     """The split route's plan under ``model`` (s3h_route_split_estimate, pure host arithmetic):
-    (m, split_s) -- the m longest parts on the CPU, the rest on the GPU, estimated split_s s."""
+    (m, tg, split_s) -- the m longest parts on the CPU, the rest on the GPU with tg staging
+    threads per device (0 for pinned parts), estimated split_s seconds."""
     m = _native.RouteModel(**model)
     lens = _u64(lengths)
-    k, t = ctypes.c_uint64(), ctypes.c_double()
+    k, tg, t = ctypes.c_uint64(), ctypes.c_int(), ctypes.c_double()
     check(lib().s3h_route_split_estimate(ctypes.byref(m), _p64(lens), lens.size, ndevices,
-                                         _native.SOURCE_IDS[source], ctypes.byref(k), ctypes.byref(t)))
-    return k.value, t.value
+                                         _native.SOURCE_IDS[source], ctypes.byref(k), ctypes.byref(tg),
+                                         ctypes.byref(t)))
+    return k.value, tg.value, t.value
 
 
 def sha256_batch_routed(parts: Sequence, ndevices: int = 0, route: str = "auto") -> tuple[np.ndarray, str]:

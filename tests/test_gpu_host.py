@@ -470,7 +470,7 @@ def test_route_auto_by_batch_shape(torch_cuda, oracle, golden, tmp_path):
     fx = {e["p"]: e["digest"] for e in golden["c2_parts"]}
     want_route, g, c = s3.route_estimate([L] * n, m)
     assert want_route == "gpu", (g, c, m)
-    k, split_s = s3.route_split_estimate([L] * n, m)
+    k, _, split_s = s3.route_split_estimate([L] * n, m)
     got, taken = s3.sha256_batch_routed(views, route="auto")
     # pinned C2 parts: the split (the CPU drop-in on part of them at once) when it is estimated
     # 5 % faster than the GPU alone -- on the box's 16 SHA-NI threads it is
@@ -544,7 +544,7 @@ def test_route_split_vs_oracle(torch_cuda, oracle, tmp_path, layout):
     total = int(offs[-1] + lens[-1]) + 64
     src = rng.integers(0, 256, total, dtype=np.uint8)
     want = oracle.batch(src, offs, lens, threads=16)
-    k, _ = s3.route_split_estimate(lens, s3.route_model(), source=layout)
+    k, _, _ = s3.route_split_estimate(lens, s3.route_model(), source=layout)
     assert 0 < k < n
     if layout == "file":
         path = tmp_path / "split.bin"

@@ -96,20 +96,29 @@ def test_route_estimate_is_monotone_in_the_batch(n, part):
     assert g2 >= g1 and c2 >= c1
 
 
-def split_ref(lengths, m, ndevices=1, source="pinned"):
-    """The split route's plan restated (include/s3hash.h s3h_route_split_estimate): parts by
-    length descending (ties by index), the first k on the CPU, the rest on the GPU."""
+def split_ref_tg(lengths, m, tg, ndevices=0, source="pinned"):
+    """The split route's plan for one split of the host threads, restated (include/s3hash.h
+    s3h_route_split_estimate): parts by length descending (ties by index), the first k on the
+    CPU, the rest on the GPU; None when tg leaves the CPU side no thread."""
     n = len(lengths)
     order = sorted(range(n), key=lambda i: -lengths[i])
     total = sum(lengths)
-    feed = m["h2d_bytes_per_s"] if source == "pinned" else min(m["h2d_bytes_per_s"], m["staged_bytes_per_s"])
-    kmax = min(n, m["cpu_threads"])
-    cap = min(ndevices, m["devices"]) if ndevices > 0 else m["devices"]
+    T = m["cpu_threads"]
+    cap = max(1, min(ndevices, m["devices"]) if ndevices > 0 else m["devices"])
+    staged = source != "pinned"
+    if staged and tg * cap >= T:
+        return None
+    tc = T - tg * cap if staged else T
+    feed = min(m["h2d_bytes_per_s"], m["staged_bytes_per_s"] * tg / T) if staged else m["h2d_bytes_per_s"]
+    kmax = min(n, tc)
     rows = []
     for k in range(1, n):
         cpu = [lengths[order[i]] for i in range(k)]
         t = min(k, kmax)
-        per_thread = min(t * m["cpu_bytes_per_s"], m["cpu_all_bytes_per_s"]) / t
+        if staged:
+            per_thread = min(T * m["cpu_bytes_per_s"], m["cpu_all_bytes_per_s"]) / T
+        else:
+            per_thread = min(t * m["cpu_bytes_per_s"], m["cpu_all_bytes_per_s"]) / t
         c = lpt(cpu, kmax) / per_thread
         devs = max(1, min(n - k, cap))
         f = (total - sum(cpu)) / devs / feed
@@ -120,6 +129,20 @@ def split_ref(lengths, m, ndevices=1, source="pinned"):
     return s_, k
 
 
+def split_ref(lengths, m, ndevices=0, source="pinned"):
+    """The whole plan: tg = 0 for pinned parts, else the best of T x {1, 4, 6, 8, 9} / 12."""
+    if source == "pinned":
+        s_, k = split_ref_tg(lengths, m, 0, ndevices, source)
+        return s_, k, 0
+    T = m["cpu_threads"]
+    best = None
+    for t in dict.fromkeys(max(1, T * num // 12) for num in (1, 4, 6, 8, 9)):
+        r = split_ref_tg(lengths, m, t, ndevices, source)
+        if r and (best is None or r[0] < best[0]):
+            best = (r[0], r[1], t)
+    return best
+
+
 @settings(max_examples=80, deadline=None)
 @given(st.lists(st.integers(0, 64 * MIB), min_size=1, max_size=60), st.integers(1, 24),
        st.integers(1, 8), st.sampled_from(["pinned", "pageable", "file"]))
@@ -127,14 +150,15 @@ def test_route_split_estimate_matches_its_formula(lengths, threads, devices, sou
     """The split plan is exactly the documented rule (the balanced m among those within 0.5 %
     of the minimum estimate), and a single part is not split."""
     m = {**MODEL, "cpu_threads": threads, "devices": devices}
-    k, s_ = s3.route_split_estimate(lengths, m, source=source)
-    if len(lengths) == 1:
-        assert (k, s_) == (0, 0.0)
+    k, tg, s_ = s3.route_split_estimate(lengths, m, source=source)
+    want = split_ref(lengths, m, source=source) if len(lengths) > 1 else None
+    if want is None:  # one part, or no thread left for the CPU side
+        assert (k, tg, s_) == (0, 0, 0.0)
         return
-    want_s, want_k = split_ref(lengths, m, source=source)
+    want_s, want_k, want_tg = want
     assert 1 <= k < len(lengths)
     assert np.isclose(s_, want_s, rtol=1e-12, atol=1e-15)
-    assert k == want_k
+    assert (k, tg) == (want_k, want_tg)
 
 
 def test_route_split_on_c2_shapes():
@@ -145,10 +169,10 @@ def test_route_split_on_c2_shapes():
              h2d_bytes_per_s=56e9, cpu_threads=16)
     lens = [8 * MIB] * 1024
     route, g, c = s3.route_estimate(lens, m)
-    k, s_ = s3.route_split_estimate(lens, m)
-    assert route == "gpu" and s_ < 0.85 * min(g, c)
+    k, tg, s_ = s3.route_split_estimate(lens, m)
+    assert route == "gpu" and s_ < 0.85 * min(g, c) and tg == 0
     assert s_ >= 8 * MIB / m["chain_bytes_per_s"]
     assert 350 < k < 500  # the feed balanced against the CPU side: 8 GiB x 39 / (39 + 56)
     route, g, c = s3.route_estimate(lens[:8], m)
-    k, s_ = s3.route_split_estimate(lens[:8], m)
+    k, tg, s_ = s3.route_split_estimate(lens[:8], m)
     assert route == "cpu" and s_ >= c

@@ -65,7 +65,7 @@ def main():
         for n in ns:
             parts = s3.BufferParts(arr, offs[:n], lens[:n])
             est_route, g_est, c_est = s3.route_estimate(lens[:n], model, pinned=src == "pinned")
-            k_est, s_est = s3.route_split_estimate(lens[:n], model, source=src)
+            k_est, tg_est, s_est = s3.route_split_estimate(lens[:n], model, source=src)
             times = {r: [] for r in ("gpu", "cpu", "split", "auto")}
             taken = None
             for k in range(a.reps + 1):
@@ -89,7 +89,8 @@ def main():
                 "auto_taken": taken, "faster": min(("gpu", "cpu", "split"), key=lambda r: med[r]),
                 "auto_over_best": round(ratio, 4),
                 "model": {"route": est_route, "gpu_s": round(g_est, 4), "cpu_s": round(c_est, 4),
-                          "split_s": round(s_est, 4), "split_cpu_parts": k_est}})
+                          "split_s": round(s_est, 4), "split_cpu_parts": k_est,
+                          "split_stage_threads": tg_est}})
             print(f"[route_sweep] {src} n={n}: gpu {med['gpu']:.4f} cpu {med['cpu']:.4f} split {med['split']:.4f} "
                   f"auto {med['auto']:.4f} ({taken}) model gpu {g_est:.4f} cpu {c_est:.4f} split {s_est:.4f} ({k_est})",
                   file=sys.stderr, flush=True)
