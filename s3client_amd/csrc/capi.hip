@@ -1186,7 +1186,9 @@ struct HostShard {
 thread_local unsigned g_stage_threads_cap = 0;
 
 unsigned shard_threads(const HostShard& sh) {
-  const unsigned t = host_threads_per_device(sh.ndevices);
+  unsigned t = host_threads_per_device(sh.ndevices);
+  if (const char* e = std::getenv("S3H_STAGE_THREADS"))  // measurements: cap every shard
+    if (std::atoi(e) > 0) t = std::min(t, unsigned(std::atoi(e)));
   return sh.threads ? std::max(1u, std::min(sh.threads, t)) : t;
 }
 
