@@ -35,11 +35,13 @@
 //   --route R        gpu (default) | cpu | auto: where the SHA-256 hashing runs.  auto decides
 //                    once for the whole upload with the measured model (sha256::choose_route:
 //                    a few large parts go to the CPU drop-in, hundreds to the GPU); a CPU
-//                    decision hashes per job as --cpu does, overlapped with the PUTs.
+//                    decision hashes per job as --cpu does, overlapped with the PUTs; split
+//                    hashes each GPU call's longest parts on the CPU drop-in beside the GPU
+//                    (S3H_ROUTE_SPLIT).
 //
 //   s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory] [--per-job]
 //                  [--cpu] [--verify] [--print-headers] [--send] [--get-verify] [--retries N]
-//                  [--content-md5] [--check-etag] [--multipart] [--route gpu|cpu|auto]
+//                  [--content-md5] [--check-etag] [--multipart] [--route gpu|cpu|auto|split]
 //                  [--devices N]
 //                  [--repeat R] [--endpoint URL[,URL...] --bucket B --key K --access A
 //                  --secret S --upload-id ID]
@@ -312,7 +314,7 @@ void usage() {
   std::fprintf(stderr,
                "usage: s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory]\n"
                "       [--per-job] [--cpu] [--verify] [--print-headers] [--send] [--get-verify]\n"
-               "       [--retries N] [--content-md5] [--check-etag] [--multipart] [--route gpu|cpu|auto]\n"
+               "       [--retries N] [--content-md5] [--check-etag] [--multipart] [--route gpu|cpu|auto|split]\n"
                "       [--endpoint URL[,URL...] --bucket B --key K --access A --secret S --upload-id ID]\n"
                "       [--devices N] [--repeat R]\n");
 }
@@ -368,10 +370,14 @@ int main(int argc, char** argv) {
   std::signal(SIGPIPE, SIG_IGN);  // a closed connection fails its PUT (sendfile has no MSG_NOSIGNAL)
   if (file.empty() || jobs < 1 || ppj < 1 || repeat < 1 ||
       (source != "file" && source != "mmap" && source != "memory") ||
-      (route_name != "gpu" && route_name != "cpu" && route_name != "auto")) { usage(); return 2; }
-  const sha256::Route route = route_name == "cpu"    ? sha256::Route::cpu
-                              : route_name == "auto" ? sha256::Route::automatic
-                                                     : sha256::Route::gpu;
+      (route_name != "gpu" && route_name != "cpu" && route_name != "auto" && route_name != "split")) {
+    usage();
+    return 2;
+  }
+  const sha256::Route route = route_name == "cpu"     ? sha256::Route::cpu
+                              : route_name == "auto"  ? sha256::Route::automatic
+                              : route_name == "split" ? sha256::Route::split
+                                                      : sha256::Route::gpu;
   sha256::Route route_taken = route;
 
   const int fd = open(file.c_str(), O_RDONLY);
@@ -429,7 +435,7 @@ int main(int argc, char** argv) {
   // drop-in and PUTs them as it goes, so hashing overlaps the uploads -- and a GPU decision as
   // the default GPU path.
   double est_gpu = 0, est_cpu = 0;
-  if (!cpu && route != sha256::Route::gpu) {
+  if (!cpu && route != sha256::Route::gpu && route != sha256::Route::split) {
     try {
       route_taken = route == sha256::Route::cpu
                         ? sha256::Route::cpu
@@ -553,9 +559,11 @@ int main(int argc, char** argv) {
       }
       return;
     }
+    // --route split: each call's longest parts on the CPU drop-in while the GPU hashes the rest
+    const sha256::Route r = route_taken == sha256::Route::split ? sha256::Route::split : sha256::Route::gpu;
     const std::vector<std::string> h = source == "file"
-                                           ? sha256::file_part_hashes(file, o, l, devices)
-                                           : sha256::payload_hashes(p, l, devices);
+                                           ? sha256::file_part_hashes(file, o, l, devices, r)
+                                           : sha256::payload_hashes(p, l, devices, r);
     for (size_t k = 0; k < idx.size(); ++k) hex[idx[k]] = h[k];
   };
   // --multipart: the POSTs around the parts (S3Api::CreateMultipartUpload /
@@ -737,7 +745,9 @@ int main(int argc, char** argv) {
                                (per_job ? ", one call per job" : ", one call") +
                                (route == sha256::Route::gpu ? std::string()
                                 : std::string(", route ") + route_name + " -> " +
-                                      (route_taken == sha256::Route::cpu ? "cpu" : "gpu")) +
+                                      (route_taken == sha256::Route::cpu     ? "cpu"
+                                       : route_taken == sha256::Route::split ? "split"
+                                                                             : "gpu")) +
                                (route == sha256::Route::automatic
                                     ? " (model: gpu " + std::to_string(est_gpu) + " s, cpu " +
                                           std::to_string(est_cpu) + " s)"

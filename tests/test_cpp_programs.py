@@ -286,15 +286,16 @@ def test_upload_etag_check_gpu(programs, tmp_path, golden, source):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("route", ["cpu", "auto"])
+@pytest.mark.parametrize("route", ["cpu", "auto", "split"])
 def test_upload_send_routed_gpu(programs, tmp_path, golden, s3_mock, route):
     """--route: the transfer test's 6 small parts hashed on the chosen route (auto: the
-    measured model sends a batch this small to the CPU drop-in) and PUT to the verifying
-    endpoint; the digests are the lib/hash goldens either way."""
+    measured model sends a batch this small to the CPU drop-in; split: the longest parts on
+    the CPU beside the GPU) and PUT to the verifying endpoint; the digests are the lib/hash
+    goldens either way."""
     url, stats = s3_mock
     r, t = _upload(["--route", route, "--source", "file"], url, tmp_path, golden)
     assert r.returncode == 0, r.stderr
-    assert f"route {route} -> cpu" in r.stderr, r.stderr
+    assert f"route {route} -> {'split' if route == 'split' else 'cpu'}" in r.stderr, r.stderr
     assert [x[4] for x in _parse_parts(r.stdout)] == [p["digest"] for p in t["parts"]]
     assert stats()["parts"] == 6
 
