@@ -397,6 +397,11 @@ Split split_plan(const s3h_route_model_t& M, const uint64_t* lengths, uint64_t n
   std::vector<double> ws[3];
   std::vector<uint64_t> sorted(n);  // the lengths in `order`
   for (uint64_t k = 0; k < n; ++k) sorted[k] = lengths[order[k]];
+  // Many small pinned parts go through the group pipeline (capi.hip run_host_groups), which
+  // packs them with the copy threads once the CPU side has taken parts out of their range:
+  // plan them as staged parts.
+  const bool packed = source == S3H_SOURCE_PINNED && n > 64 && sorted[0] <= kGroupMaxPart;
+  if (packed) source = S3H_SOURCE_PAGEABLE;
   if (source == S3H_SOURCE_PINNED) return split_choose(M, sorted.data(), n, ndevices, source, 0, ws);
   const unsigned T = unsigned(std::max(1, M.cpu_threads));
   std::vector<unsigned> cand;

@@ -130,7 +130,10 @@ def split_ref_tg(lengths, m, tg, ndevices=0, source="pinned"):
 
 
 def split_ref(lengths, m, ndevices=0, source="pinned"):
-    """The whole plan: tg = 0 for pinned parts, else the best of T x {1, 4, 6, 8, 9} / 12."""
+    """The whole plan: tg = 0 for pinned parts, else the best of T x {1, 4, 6, 8, 9} / 12; many
+    small pinned parts (the group pipeline packs them) are planned as staged."""
+    if source == "pinned" and len(lengths) > 64 and max(lengths) <= MIB:
+        source = "pageable"
     if source == "pinned":
         s_, k = split_ref_tg(lengths, m, 0, ndevices, source)
         return s_, k, 0
@@ -176,3 +179,15 @@ def test_route_split_on_c2_shapes():
     route, g, c = s3.route_estimate(lens[:8], m)
     k, tg, s_ = s3.route_split_estimate(lens[:8], m)
     assert route == "cpu" and s_ >= c
+
+
+def test_route_split_plans_small_pinned_parts_as_staged():
+    """Many small pinned parts go through the group pipeline, whose copy threads pack them once
+    the CPU side has taken parts out of their range: the split plan gives them staging
+    threads, exactly as for pageable parts."""
+    lens = list(np.random.default_rng(3).integers(1, MIB, 500))
+    m = {**MODEL, "cpu_threads": 16}
+    assert s3.route_split_estimate(lens, m, source="pinned") == s3.route_split_estimate(lens, m, source="pageable")
+    assert s3.route_split_estimate(lens, m, source="pinned")[1] > 0
+    big = lens[:-1] + [2 * MIB]
+    assert s3.route_split_estimate(big, m, source="pinned")[1] == 0

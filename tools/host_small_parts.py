@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--hi", type=int, default=128 << 10)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--big", default="")
+    ap.add_argument("--routes", default="gpu", help="comma list of gpu / auto / split / cpu")
     a = ap.parse_args()
     import torch
 
@@ -45,19 +46,26 @@ def main():
             buf.numpy()[:] = src
             parts = s3.BufferParts(buf, offs, lens)
             ref = s3.sha256_batch_host(parts)
-            ts = []
-            for _ in range(a.reps):
-                t0 = time.perf_counter()
-                out = s3.sha256_batch_host(parts)
-                ts.append(time.perf_counter() - t0)
-            sample = rng.integers(0, n, 16)
-            ok = bool(np.array_equal(out, ref)) and all(
-                out[i].tobytes().hex() == hashlib.sha256(src[int(offs[i]):int(offs[i] + lens[i])]).hexdigest()
-                for i in sample)
-            rc |= not ok
-            print(json.dumps({"source": kind, "parts": n, "big": a.big or None, "GiB": round(total / 2**30, 3),
-                              "GiBps": round(total / 2**30 / float(np.median(ts)), 2),
-                              "ms": round(1e3 * float(np.median(ts)), 2), "digests_ok": ok}), flush=True)
+            for route in a.routes.split(","):
+                def call():
+                    if route == "gpu":
+                        return s3.sha256_batch_host(parts), "gpu"
+                    return s3.sha256_batch_routed(parts, route=route)
+                call()
+                ts = []
+                for _ in range(a.reps):
+                    t0 = time.perf_counter()
+                    out, taken = call()
+                    ts.append(time.perf_counter() - t0)
+                sample = rng.integers(0, n, 16)
+                ok = bool(np.array_equal(out, ref)) and all(
+                    out[i].tobytes().hex() == hashlib.sha256(src[int(offs[i]):int(offs[i] + lens[i])]).hexdigest()
+                    for i in sample)
+                rc |= not ok
+                print(json.dumps({"source": kind, "parts": n, "big": a.big or None, "route": route, "taken": taken,
+                                  "GiB": round(total / 2**30, 3),
+                                  "GiBps": round(total / 2**30 / float(np.median(ts)), 2),
+                                  "ms": round(1e3 * float(np.median(ts)), 2), "digests_ok": ok}), flush=True)
             del buf, parts
     return rc
 
