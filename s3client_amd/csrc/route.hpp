@@ -478,7 +478,11 @@ int split_run(const uint8_t* const* parts, const char* path, const uint64_t* off
   const unsigned devs = unsigned(std::max(1, ndevices > 0 ? std::min(ndevices, count) : count));
   const unsigned tc = sp.tg && uint64_t(sp.tg) * devs < T ? T - sp.tg * devs : T;
   std::thread cpu([&] {
-    crc = cpu_batch(parts ? cp.data() : nullptr, fd, co.data(), cl.data(), m, cd.data(), tc);
+    try {
+      crc = cpu_batch(parts ? cp.data() : nullptr, fd, co.data(), cl.data(), m, cd.data(), tc);
+    } catch (const std::exception&) {  // thread or buffer allocation
+      crc = fail(S3H_ENOMEM, "out of host resources");
+    }
     if (crc) cerr = g_err;
   });
   g_stage_threads_cap = sp.tg;  // the GPU side's staging threads (0: uncapped)
@@ -595,7 +599,12 @@ int s3h_route_split_estimate(const s3h_route_model_t* m, const uint64_t* lengths
   if (!m || !lengths || n == 0) return fail(S3H_EINVAL, "route split estimate: bad argument");
   if (!(m->cpu_bytes_per_s > 0 && m->chain_bytes_per_s > 0 && m->h2d_bytes_per_s > 0))
     return fail(S3H_EINVAL, "route split estimate: the model's rates must be positive");
-  const Split sp = split_plan(*m, lengths, n, ndevices, source, longest_first(lengths, n));
+  Split sp;
+  try {
+    sp = split_plan(*m, lengths, n, ndevices, source, longest_first(lengths, n));
+  } catch (const std::exception&) {
+    return fail(S3H_ENOMEM, "route split estimate: out of host memory");
+  }
   if (cpu_parts) *cpu_parts = sp.m;
   if (stage_threads) *stage_threads = int(sp.tg);
   if (split_s) *split_s = sp.s;
@@ -604,7 +613,11 @@ int s3h_route_split_estimate(const s3h_route_model_t* m, const uint64_t* lengths
 
 int s3h_sha256_batch_routed(const uint8_t* const* parts, const uint64_t* lengths, uint64_t n,
                             uint32_t* digests, int ndevices, int route, int* taken) {
-  return routed(parts, nullptr, nullptr, lengths, n, digests, ndevices, route, taken);
+  try {
+    return routed(parts, nullptr, nullptr, lengths, n, digests, ndevices, route, taken);
+  } catch (const std::exception&) {  // nothing escapes the C-ABI
+    return fail(S3H_ENOMEM, "routed batch: out of host resources");
+  }
 }
 
 // S3 multipart ETag (what CompleteMultipartUpload returns, multipart_upload.cpp:162-183):
@@ -625,7 +638,11 @@ int s3h_sha256_file_parts_routed(const char* path, const uint64_t* offsets,
                                  const uint64_t* lengths, uint64_t n, uint32_t* digests,
                                  int ndevices, int route, int* taken) {
   if (!path) return fail(S3H_EINVAL, "routed file parts: null path");
-  return routed(nullptr, path, offsets, lengths, n, digests, ndevices, route, taken);
+  try {
+    return routed(nullptr, path, offsets, lengths, n, digests, ndevices, route, taken);
+  } catch (const std::exception&) {
+    return fail(S3H_ENOMEM, "routed file parts: out of host resources");
+  }
 }
 
 }  // extern "C"
