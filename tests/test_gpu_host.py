@@ -562,6 +562,51 @@ def test_route_split_vs_oracle(torch_cuda, oracle, tmp_path, layout):
     assert np.array_equal(one, want[:1])
 
 
+def test_concurrent_split_and_auto_callers(torch_cuda, oracle, tmp_path):
+    """Six threads at once on the split and AUTO routes (each split starting its own CPU-side
+    threads beside GPU sides that meet in the device queue): pinned and pageable parts, file
+    ranges and a one-part batch, three rounds each; every digest vs the oracle."""
+    torch = torch_cuda
+    rng = np.random.default_rng(606)
+    n = 400
+    lens = rng.integers(0, 3 << 20, n).astype(np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    total = int(lens.sum()) + 64
+    src = rng.integers(0, 256, total, dtype=np.uint8)
+    want = oracle.batch(src, offs, lens, threads=16)
+    pinned = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+    pinned.numpy()[:] = src
+    path = tmp_path / "split.bin"
+    src.tofile(path)
+    cases = [("split", "pinned"), ("auto", "pinned"), ("split", "pageable"), ("auto", "pageable"),
+             ("split", "file"), ("split", "one")]
+    errors, bad = [], []
+
+    def job(k):
+        route, kind = cases[k]
+        sel = slice(k * 7, k * 7 + (1 if kind == "one" else n - 6 * 7))
+        o, ln = offs[sel], lens[sel]
+        try:
+            for _ in range(3):
+                if kind == "file":
+                    got, _ = s3.sha256_file_parts_routed(str(path), o, ln, route=route)
+                else:
+                    buf = pinned if kind == "pinned" else src
+                    got, _ = s3.sha256_batch_routed(s3.BufferParts(buf, o, ln), route=route)
+                if not np.array_equal(got, want[sel]):
+                    bad.append((route, kind))
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=job, args=(k,)) for k in range(len(cases))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    assert not bad, bad
+
+
 def test_dual_digest_host_beyond_one_grid(torch_cuda, oracle):
     """SHA-256 + MD5 from host memory for more parts than any one-grid dual form holds (9,000
     ragged pageable parts: the two plans per slice on the two hash streams) and, in another
