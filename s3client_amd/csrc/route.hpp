@@ -390,7 +390,7 @@ Split split_choose(const s3h_route_model_t& M, const uint64_t* sorted, uint64_t 
 }
 
 // The split plan: pinned parts need no staging threads; staged parts (pageable, file ranges)
-// try tg = T/4, T/3, T/2, 2T/3, 3T/4 staging threads per GPU shard and keep the fastest
+// try tg = T/12, T/3, T/2, 2T/3, 3T/4 staging threads per GPU shard and keep the fastest
 // estimate (S3H_SPLIT_STAGE_THREADS fixes tg, for measurements).
 Split split_plan(const s3h_route_model_t& M, const uint64_t* lengths, uint64_t n, int ndevices,
                  int source, const std::vector<uint64_t>& order) {
