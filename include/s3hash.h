@@ -347,6 +347,13 @@ int s3h_verify_batch_device(int device, int algo, const void *d_base, const uint
 int s3h_verify_batch_host(int algo, const uint8_t *const *parts, const uint64_t *lengths,
                           uint64_t n, const uint32_t *expected, uint8_t *mismatch,
                           uint64_t *mismatches, int ndevices);
+/* The host form on a route (size-aware routing below): S3H_ROUTE_GPU = s3h_verify_batch_host;
+ * CPU / SPLIT / AUTO hash SHA-256 as s3h_sha256_batch_routed does, then compare (the route
+ * model prices SHA-256 only, so MD5 takes S3H_ROUTE_GPU and any other route is S3H_EINVAL).
+ * *taken (if non-null) receives the route that ran. */
+int s3h_verify_batch_routed(int algo, const uint8_t *const *parts, const uint64_t *lengths,
+                            uint64_t n, const uint32_t *expected, uint8_t *mismatch,
+                            uint64_t *mismatches, int ndevices, int route, int *taken);
 
 /* ---------------------------------------------------------------- multi-object streams
  * n messages (objects) hashed incrementally as their bytes arrive in chunks: the batched,

@@ -5,7 +5,7 @@ Drop-in for uv-cpp/s3client's lib/hash on the payload-hashing path; see DESIGN.m
 from .hashing import (Plan, device_count, digests_to_text, generate_parts, hash_to_text,
                       hmac256, nblocks, sha256, sha256_batch_device, sha256_batch_host,
                       cpu_backend, md5, md5_batch_device, md5_batch_host, multipart_etag,
-                      verify_batch_device, verify_batch_host, Stream,
+                      verify_batch_device, verify_batch_host, verify_batch_routed, Stream,
                       sha256_md5_batch_device, sha256_md5_batch_host, sha256_file_parts,
                       sha256_md5_file_parts,
                       trim, sha256_batch_host_on, host_threads, device_pci_bus_id,
@@ -19,7 +19,7 @@ from ._native import S3HashError, LIB_PATH
 __all__ = ["BufferParts", "Plan", "device_count", "digests_to_text", "generate_parts", "hash_to_text",
            "hmac256", "nblocks", "sha256", "sha256_batch_device", "sha256_batch_host",
            "cpu_backend", "md5", "md5_batch_device", "md5_batch_host", "multipart_etag",
-           "verify_batch_device", "verify_batch_host", "Stream",
+           "verify_batch_device", "verify_batch_host", "verify_batch_routed", "Stream",
            "sha256_md5_batch_device", "sha256_md5_batch_host", "sha256_file_parts",
            "sha256_md5_file_parts", "trim", "sha256_batch_host_on", "host_threads",
            "device_pci_bus_id", "route_model", "route_estimate", "route_split_estimate", "sha256_batch_routed",

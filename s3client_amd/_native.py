@@ -42,7 +42,7 @@ C_ABI_SYMBOLS = (
     "s3h_sha256_file_parts_routed", "s3h_pci_numa", "s3h_device_numa_node", "s3h_host_numa",
     "s3h_host_numa_info", "s3h_host_alloc", "s3h_host_free", "s3h_mem_node",
     "s3h_route_estimate_ex", "s3h_kernel_policy", "s3h_stream_stats", "s3h_plan_dual_layout",
-    "s3h_dual_layout", "s3h_route_split_estimate",
+    "s3h_dual_layout", "s3h_route_split_estimate", "s3h_verify_batch_routed",
 )
 POLICY_IDS = {"throughput": 0, "efficiency": 1}
 POLICY_NAMES = {v: k for k, v in POLICY_IDS.items()}
@@ -203,6 +203,10 @@ def lib() -> ctypes.CDLL:
                                                    ctypes.POINTER(ctypes.c_uint64),
                                                    ctypes.POINTER(ctypes.c_int),
                                                    ctypes.POINTER(ctypes.c_double)]
+            L.s3h_verify_batch_routed.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), u64p,
+                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.POINTER(ctypes.c_uint64), ctypes.c_int,
+                                                  ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
             L.s3h_sha256_batch_routed.argtypes = [ctypes.POINTER(ctypes.c_void_p), u64p,
                                                   ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
                                                   ctypes.c_int, ctypes.POINTER(ctypes.c_int)]

@@ -634,6 +634,35 @@ int s3h_multipart_etag(const uint32_t* md5_digests, uint64_t n, char* out, uint6
   return S3H_OK;
 }
 
+int s3h_verify_batch_routed(int algo, const uint8_t* const* parts, const uint64_t* lengths,
+                            uint64_t n, const uint32_t* expected, uint8_t* mismatch,
+                            uint64_t* mismatches, int ndevices, int route, int* taken) {
+  if (taken) *taken = -1;
+  if (!expected || !mismatch || !mismatches) return fail(S3H_EINVAL, "verify routed: null argument");
+  if (algo != S3H_ALGO_SHA256 && algo != S3H_ALGO_MD5)
+    return fail(S3H_EINVAL, "verify routed: unknown algorithm %d", algo);
+  if (route == S3H_ROUTE_GPU) {
+    const int rc = s3h_verify_batch_host(algo, parts, lengths, n, expected, mismatch, mismatches, ndevices);
+    if (rc == S3H_OK && taken) *taken = S3H_ROUTE_GPU;
+    return rc;
+  }
+  if (algo != S3H_ALGO_SHA256)
+    return fail(S3H_EINVAL, "verify routed: route %d is SHA-256 only (MD5 verifies on the GPU route)", route);
+  try {
+    std::vector<uint32_t> got(8 * n);
+    if (int rc = routed(parts, nullptr, nullptr, lengths, n, got.data(), ndevices, route, taken)) return rc;
+    uint64_t c = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      mismatch[i] = std::memcmp(&got[8 * i], expected + 8 * i, 32) != 0;
+      c += mismatch[i];
+    }
+    *mismatches = c;
+    return S3H_OK;
+  } catch (const std::exception&) {
+    return fail(S3H_ENOMEM, "verify routed: out of host resources");
+  }
+}
+
 int s3h_sha256_file_parts_routed(const char* path, const uint64_t* offsets,
                                  const uint64_t* lengths, uint64_t n, uint32_t* digests,
                                  int ndevices, int route, int* taken) {

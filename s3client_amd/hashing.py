@@ -301,6 +301,29 @@ def verify_batch_host(parts: Sequence, expected, algo: str = "sha256",
     return mism.astype(bool)
 
 
+def verify_batch_routed(parts: Sequence, expected, algo: str = "sha256", ndevices: int = 0,
+                        route: str = "auto") -> tuple[np.ndarray, str]:
+    """verify_batch_host on a route (s3h_verify_batch_routed): "gpu", or for SHA-256 "cpu",
+    "split" or "auto" as sha256_batch_routed.  Returns (bool mismatch mask, route taken)."""
+    a = _native.ALGO_IDS[algo]
+    words = _native.DIGEST_WORDS[a]
+    if len(expected) and isinstance(expected[0], str):
+        expected = np.stack([np.frombuffer(bytes.fromhex(h), dtype=np.uint32) for h in expected])
+    exp = np.ascontiguousarray(expected, dtype=np.uint32).reshape(-1, words)
+    arrs, ptrs, lens = _host_parts(parts)
+    n = len(arrs)
+    if exp.shape[0] != n:
+        raise ValueError("expected digest count differs from part count")
+    mism = np.zeros(n, dtype=np.uint8)
+    cnt = ctypes.c_uint64(0)
+    taken = ctypes.c_int(-1)
+    check(lib().s3h_verify_batch_routed(a, ptrs, _p64(lens), n, exp.ctypes.data, mism.ctypes.data,
+                                        ctypes.byref(cnt), ndevices, _native.ROUTE_IDS[route],
+                                        ctypes.byref(taken)))
+    assert cnt.value == int(mism.sum())
+    return mism.astype(bool), _native.ROUTE_NAMES[taken.value]
+
+
 def verify_batch_device(data, offsets, lengths, expected, algo: str = "sha256", stream=None):
     """Device-resident verification: returns (mismatch count, bool mask on the device)."""
     import torch

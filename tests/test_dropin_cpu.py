@@ -216,6 +216,13 @@ def test_route_auto_is_not_a_fallback():
     with pytest.raises(s3.S3HashError) as e:
         s3.sha256_batch_routed([b"abc", b"de"], route="split")
     assert e.value.code == -2
+    exp = np.zeros((2, 8), dtype=np.uint32)
+    with pytest.raises(s3.S3HashError) as e:
+        s3.verify_batch_routed([b"abc", b"de"], exp, route="auto")
+    assert e.value.code == -2
+    with pytest.raises(s3.S3HashError) as e:  # MD5 verifies on the GPU route only
+        s3.verify_batch_routed([b"abc", b"de"], exp[:, :4], algo="md5", route="split")
+    assert e.value.code == -1
     with pytest.raises(s3.S3HashError) as e:
         s3.route_model()
     assert e.value.code == -2

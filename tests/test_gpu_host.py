@@ -562,6 +562,34 @@ def test_route_split_vs_oracle(torch_cuda, oracle, tmp_path, layout):
     assert np.array_equal(one, want[:1])
 
 
+@pytest.mark.parametrize("kind", ["pinned", "pageable"])
+def test_verify_routed(torch_cuda, oracle, kind):
+    """Download-side verification on every route (s3h_verify_batch_routed): ragged parts, about
+    3 % of the expected digests corrupted in one bit; the mismatch mask is exactly the
+    corrupted set on gpu / cpu / split / auto, and MD5 verifies on the GPU route."""
+    torch = torch_cuda
+    rng = np.random.default_rng(77 + len(kind))
+    n = 700
+    lens = rng.integers(0, 2 << 20, n).astype(np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    total = int(lens.sum()) + 64
+    src = rng.integers(0, 256, total, dtype=np.uint8)
+    buf = torch.empty(total, dtype=torch.uint8, pin_memory=kind == "pinned")
+    buf.numpy()[:] = src
+    parts = s3.BufferParts(buf, offs, lens)
+    exp = oracle.batch(src, offs, lens, threads=16).copy()
+    bad = rng.random(n) < 0.03
+    exp[bad, 3] ^= np.uint32(1 << 7)
+    for route in ("gpu", "cpu", "split", "auto"):
+        mask, taken = s3.verify_batch_routed(parts, exp, route=route)
+        assert np.array_equal(mask, bad), route
+        assert taken == route or route == "auto", (route, taken)
+    m5 = oracle.md5_batch(src, offs, lens).copy()
+    m5[bad, 0] ^= np.uint32(1)
+    mask, taken = s3.verify_batch_routed(parts, m5, algo="md5", route="gpu")
+    assert np.array_equal(mask, bad) and taken == "gpu"
+
+
 def test_concurrent_split_and_auto_callers(torch_cuda, oracle, tmp_path):
     """Six threads at once on the split and AUTO routes (each split starting its own CPU-side
     threads beside GPU sides that meet in the device queue): pinned and pageable parts, file
