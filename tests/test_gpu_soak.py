@@ -5,8 +5,9 @@ shape tests do (part counts across every AUTO kernel range, upload-like length s
 many small parts and small parts with a few large ones -- the group pipeline and its split
 from the slice pipeline) and sends each through the next entry point in turn: device SHA-256 /
 MD5 / both, host batches from numpy views, pinned and pageable BufferParts (SHA-256, MD5,
-both, verification with corrupted expectations), file ranges (SHA-256, both), the routed
-split and AUTO routes, and streamed objects fed in random pieces from host memory.  Every
+both, verification with corrupted expectations, also on the CPU / split / AUTO routes), file
+ranges (SHA-256, both), the routed split and AUTO routes, and streamed objects fed in random
+pieces from host memory.  Every
 result is checked whole against the oracle (lib/hash sha256.cpp:147-160, md5.cpp:71-116).
 
 S3H_SOAK_SECONDS sets how long it runs (default 20 s: every entry point at least once);
@@ -27,7 +28,8 @@ MIB = 1 << 20
 SOAK_S = float(os.environ.get("S3H_SOAK_SECONDS", "20"))
 SEED = int(os.environ.get("S3H_SOAK_SEED", "2024"))
 ENTRIES = ["device", "device_md5", "device_dual", "host_views", "host_pinned", "host_pageable",
-           "host_dual", "host_md5", "verify", "file", "file_dual", "split", "auto", "stream_host"]
+           "host_dual", "host_md5", "verify", "file", "file_dual", "split", "auto", "stream_host",
+           "verify_routed"]
 EXTRA_SHAPES = ["many_small", "small_and_large"]
 
 
@@ -121,6 +123,13 @@ def _run(entry, rng, torch, oracle, data, offs, lens, want_sha):
         assert taken in ("gpu", "cpu", "split"), taken
         assert entry == "auto" or taken == ("split" if len(lens) > 1 else "gpu"), taken
         out.append((f"sha256 ({taken})", got, want_sha()))
+    elif entry == "verify_routed":
+        exp = want_sha().copy()
+        bad = rng.random(len(lens)) < 0.01
+        exp[bad, int(rng.integers(0, 8))] ^= np.uint32(1 << int(rng.integers(0, 32)))
+        route = ("cpu", "split", "auto")[int(rng.integers(0, 3))]
+        mism, taken = s3.verify_batch_routed(s3.BufferParts(src, offs, lens), exp, route=route)
+        out.append((f"mismatch mask ({route} -> {taken})", mism[:, None], bad[:, None]))
     elif entry == "stream_host":
         with s3.Stream(len(lens)) as st:
             for po, pl in _stream_pieces(rng, offs, lens):
