@@ -892,9 +892,13 @@ constexpr uint64_t kStageSlot = 32ull << 20;     // pinned staging bytes per rin
 // copy must outlast its longest part's chain (~69 MB/s per chain vs ~52 GB/s of PCIe: 750 x),
 // groups between kGroupMin and kGroupMax bytes.
 constexpr uint64_t kGroupMaxPart = 1ull << 20;
-constexpr uint64_t kGroupCopyPerChain = 768;
+// Groups of 1,536 x the longest part where two of them fit the HBM ring a context keeps
+// between calls (release_large), else 768 x: 20,000 / 100,000 pinned parts of <= 128 KiB at
+// 768 x 40.9 / 46.8 GiB/s, at 1,536 x 46.7 / 49.6 (profiles/r05_group_sweep.log).
+constexpr uint64_t kGroupCopyPerChain = 1536, kGroupCopyPerChainMin = 768;
 constexpr uint64_t kGroupMin = 64ull << 20, kGroupMax = 1ull << 30;
 constexpr uint64_t kKeepRingBytes = 1ull << 30;  // largest HBM ring kept between calls
+constexpr uint64_t kGroupChunk = 64ull << 20;    // group mode: pinned staging per packed chunk
 // File ranges stage with one pread per part per slice, whose syscall costs more than it moves
 // below ~32 KiB: their slices are at least 32 KiB up to 4,096 parts per device (slots of up
 // to 128 MiB), 128 MiB / n beyond.
@@ -941,6 +945,7 @@ struct HostCtx {
   Place place;  // NUMA node of the pinned staging and CPUs of the copy threads (device_place)
   hipStream_t copy_s = nullptr, hash_s[kHostMaxAlgo] = {};
   hipEvent_t copied[kHostRing] = {}, hashed[kHostRing][kHostMaxAlgo] = {};
+  hipEvent_t chunk_copied[kHostRing] = {};  // group mode: a staging chunk's DMA has run
   std::unique_ptr<CopyPool> pool;
   s3h_plan_s* plan[kHostMaxAlgo] = {};
   uint32_t* d_dig[kHostMaxAlgo] = {};
@@ -964,6 +969,7 @@ struct HostCtx {
       if (e == hipSuccess && !st) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
     for (int r = 0; r < kHostRing && e == hipSuccess; ++r) {
       if (!copied[r]) e = hipEventCreateWithFlags(&copied[r], hipEventDisableTiming);
+      if (e == hipSuccess && !chunk_copied[r]) e = hipEventCreateWithFlags(&chunk_copied[r], hipEventDisableTiming);
       for (hipEvent_t& h : hashed[r])
         if (e == hipSuccess && !h) e = hipEventCreateWithFlags(&h, hipEventDisableTiming);
     }
@@ -1054,6 +1060,8 @@ struct HostCtx {
     sync();
     pool.reset();
     for (hipEvent_t e : copied)
+      if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : chunk_copied)
       if (e) (void)hipEventDestroy(e);
     for (auto& row : hashed)
       for (hipEvent_t e : row)
@@ -1214,8 +1222,14 @@ int run_host_groups(HostCtx& C, const HostShard& sh, const int* algos, int nalgo
   HIP_TRY(hipMemGetInfo(&free_b, &total_b));
   const uint64_t budget = std::min<uint64_t>(16ull << 30, (free_b + C.ring_bytes) / 4);
   const uint64_t longest64 = std::max<uint64_t>(64, (longest + 63) & ~uint64_t(63));
-  const uint64_t G = std::max(longest64, std::min({kGroupMax, std::max(kGroupMin, kGroupCopyPerChain * longest64),
-                                                   budget / 2 / 64 * 64}));
+  uint64_t per_chain = kGroupCopyPerChain;
+  if (const char* e = std::getenv("S3H_GROUP_COPY_PER_CHAIN"))  // measurements only
+    if (std::atoll(e) > 0) per_chain = uint64_t(std::atoll(e));
+  // beyond 768 x only while two groups fit the HBM ring a context keeps between calls
+  // (release_large) -- reallocating it per call costs more than the overlap gains
+  const uint64_t keep = kKeepRingBytes / 2;
+  const uint64_t want = std::max(kGroupCopyPerChainMin * longest64, std::min(per_chain * longest64, keep));
+  const uint64_t G = std::max(longest64, std::min({kGroupMax, std::max(kGroupMin, want), budget / 2 / 64 * 64}));
   std::vector<uint64_t> gstart{0}, gbytes;
   uint64_t acc = 0;
   for (uint64_t j = 0; j < n; ++j) {
@@ -1264,14 +1278,19 @@ int run_host_groups(HostCtx& C, const HostShard& sh, const int* algos, int nalgo
     uint64_t span = 0;
     any_staged = !contiguous(gstart[k], gstart[k + 1], &span);
   }
+  // packed groups go through kHostRing pinned chunks of kGroupChunk bytes (a part always fits
+  // one): the staging is sized for the copy in flight, not for the group the GPU hashes
+  const uint64_t chunk = std::max(kGroupChunk, longest64);
   if (any_staged) {
-    ce = C.grow_pinned(&C.stage, &C.stage_bytes, 2 * maxb);
+    ce = C.grow_pinned(&C.stage, &C.stage_bytes, kHostRing * chunk);
     if (ce != hipSuccess) {
       (void)hipGetLastError();
-      return fail(S3H_ENOMEM, "pinned group staging (2 x %llu B): %s", (unsigned long long)maxb,
-                  hipGetErrorString(ce));
+      return fail(S3H_ENOMEM, "pinned group staging (%d x %llu B): %s", kHostRing,
+                  (unsigned long long)chunk, hipGetErrorString(ce));
     }
   }
+  bool chunk_used[kHostRing] = {};
+  uint64_t chunk_next = 0;
   HIP_TRY(C.ensure_gpin(maxparts));
   for (int q = 0; q < 2; ++q)
     for (int a = 0; a < nalgo; ++a) {
@@ -1307,16 +1326,25 @@ int run_host_groups(HostCtx& C, const HostShard& sh, const int* algos, int nalgo
         return rc;
     if (direct) {
       if (span) HIP_TRY(hipMemcpyAsync(dgrp, base, span, hipMemcpyHostToDevice, C.copy_s));
-    } else {
-      uint8_t* const hst = C.stage + uint64_t(q) * maxb;
-      std::atomic<bool> bad{false};
-      pool->run(ng, [&](uint64_t t) {
-        const uint64_t j = j0 + t;
-        if (lens[j] && !src.fill(sh.parts[j], 0, lens[j], hst + poff[j]))
-          bad.store(true, std::memory_order_relaxed);
-      });
-      if (bad.load()) return fail(S3H_EINVAL, "reading a part failed (file shorter than a part?)");
-      HIP_TRY(hipMemcpyAsync(dgrp, hst, gbytes[k], hipMemcpyHostToDevice, C.copy_s));
+    } else {  // packed chunk by chunk: parts [ja, jb) whose packed bytes fit one chunk
+      for (uint64_t ja = j0, jb; ja < j1; ja = jb) {
+        jb = ja + 1;
+        while (jb < j1 && poff[jb] + ((lens[jb] + 63) & ~uint64_t(63)) - poff[ja] <= chunk) ++jb;
+        const uint64_t bytes = (jb < j1 ? poff[jb] : gbytes[k]) - poff[ja];
+        const int c = int(chunk_next++ % kHostRing);
+        if (chunk_used[c]) HIP_TRY(hipEventSynchronize(C.chunk_copied[c]));  // its last DMA ran
+        uint8_t* const hst = C.stage + uint64_t(c) * chunk;
+        std::atomic<bool> bad{false};
+        pool->run(jb - ja, [&](uint64_t t) {
+          const uint64_t j = ja + t;
+          if (lens[j] && !src.fill(sh.parts[j], 0, lens[j], hst + (poff[j] - poff[ja])))
+            bad.store(true, std::memory_order_relaxed);
+        });
+        if (bad.load()) return fail(S3H_EINVAL, "reading a part failed (file shorter than a part?)");
+        if (bytes) HIP_TRY(hipMemcpyAsync(dgrp + poff[ja], hst, bytes, hipMemcpyHostToDevice, C.copy_s));
+        HIP_TRY(hipEventRecord(C.chunk_copied[c], C.copy_s));
+        chunk_used[c] = true;
+      }
     }
     HIP_TRY(hipEventRecord(C.copied[q], C.copy_s));
     for (int a = 0; a < nalgo; ++a) {
@@ -1377,21 +1405,17 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
     for (uint64_t j = 1; j < n && uniform; ++j)
       uniform = lens[j] == lens[0] && parts[sh.parts[j]] - parts[sh.parts[j - 1]] == stride;
   }
-  // Many small parts: whole parts in groups instead of slices of every part (run_host_groups)
-  // -- when staging would cut slices below 16 KiB (> 2,048 parts), or pinned ragged parts would
-  // each take their own DMA per slice (> 64 parts averaging < 256 KiB).  A caller's explicit
-  // slice size keeps the slice pipeline.
-  // Large parts beside them (an object's parts batched with many small objects) run through
-  // the slice pipeline afterwards, on their own.
+  // Many small parts (<= kGroupMaxPart): whole parts in groups instead of slices of every part
+  // (run_host_groups) -- when staging would cut slices below 16 KiB (> 2,048 parts), or pinned
+  // ragged parts would each take their own DMA per slice (> 64 parts: 4,000 pinned parts of
+  // U[1 B, 1 MiB] spent 0.49 s draining 56,000 per-part DMAs for 1.9 GiB).  A caller's
+  // explicit slice size keeps the slice pipeline.  Large parts beside them (an object's parts
+  // batched with many small objects) run through the slice pipeline afterwards, on their own.
   if (slice == 0) {
     std::vector<uint64_t> small, large;
-    uint64_t small_total = 0;
-    for (uint64_t j = 0; j < n; ++j) {
-      (lens[j] <= kGroupMaxPart ? small : large).push_back(sh.parts[j]);
-      if (lens[j] <= kGroupMaxPart) small_total += lens[j];
-    }
+    for (uint64_t j = 0; j < n; ++j) (lens[j] <= kGroupMaxPart ? small : large).push_back(sh.parts[j]);
     const uint64_t ns = small.size();
-    if ((staged && ns > 2048) || (!staged && !uniform && ns > 64 && small_total < ns * (256ull << 10))) {
+    if ((staged && ns > 2048) || (!staged && !uniform && ns > 64)) {
       if (large.empty()) return run_host_groups(C, sh, algos, nalgo, src, lengths, digests, !staged);
       const HostShard hs{sh.device, sh.ndevices, std::move(small), sh.threads};
       const HostShard hl{sh.device, sh.ndevices, std::move(large), sh.threads};
