@@ -899,9 +899,11 @@ constexpr uint64_t kGroupCopyPerChain = 1536, kGroupCopyPerChainMin = 768;
 constexpr uint64_t kGroupMin = 64ull << 20, kGroupMax = 1ull << 30;
 constexpr uint64_t kKeepRingBytes = 1ull << 30;  // largest HBM ring kept between calls
 constexpr uint64_t kGroupChunk = 64ull << 20;    // group mode: pinned staging per packed chunk
-// File ranges stage with one pread per part per slice, whose syscall costs more than it moves
-// below ~32 KiB: their slices are at least 32 KiB up to 4,096 parts per device (slots of up
-// to 128 MiB), 128 MiB / n beyond.
+constexpr uint64_t kPinnedStageMin = 1024;       // ragged pinned parts beyond this are staged
+// Staged slices are at least 32 KiB up to 4,096 parts per device (slots of up to 128 MiB),
+// 128 MiB / n beyond: a file range's pread costs more than it moves below ~32 KiB, and each
+// slice of memory parts costs a copy-thread dispatch and a launch (4,000 parts of U[256 KiB,
+// 4 MiB] in 8 KiB slices: 512 slices, 26.6 GiB/s).
 constexpr uint64_t kFileStageSlot = 128ull << 20;
 
 // One part of a merged batch (concurrent callers, below): host memory or a file range.
@@ -1423,6 +1425,9 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
       return run_host_shard(C, hl, algos, nalgo, src, lengths, digests, 0);
     }
   }
+  // Many ragged pinned parts: packing them into staging (memcpy, one DMA per slice) beats one
+  // DMA per part per slice (4,000 parts of U[256 KiB, 4 MiB]: 18.0 GiB/s on per-part DMAs).
+  if (!staged && !uniform && n > kPinnedStageMin) staged = true;
   // Too many pageable parts for the staging cap even at 64 B per slice: pageable DMAs.
 #ifdef S3H_EXP_PAGEABLE_DIRECT  // tools/ experiment builds only: pageable DMAs, no staging
   bool direct_pageable = staged && parts;
@@ -1432,7 +1437,7 @@ int run_host_shard(HostCtx& C, const HostShard& sh, const int* algos, int nalgo,
   if (direct_pageable) staged = false;
   if (slice == 0)
     slice = staged ? std::max<uint64_t>(std::max<uint64_t>(64, kStageSlot / n / 64 * 64),
-                                        parts ? 0 : std::min<uint64_t>(32 << 10, kFileStageSlot / n / 64 * 64))
+                                        std::min<uint64_t>(32 << 10, kFileStageSlot / n / 64 * 64))
             : uniform ? (256ull << 10) : (2ull << 20);
   const uint64_t longest = *std::max_element(lens.begin(), lens.end());
   slice = std::min(slice, std::max<uint64_t>(64, (longest + 63) / 64 * 64));  // no idle slot bytes

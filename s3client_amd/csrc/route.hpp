@@ -400,7 +400,9 @@ Split split_plan(const s3h_route_model_t& M, const uint64_t* lengths, uint64_t n
   // Many small pinned parts go through the group pipeline (capi.hip run_host_groups), which
   // packs them with the copy threads once the CPU side has taken parts out of their range:
   // plan them as staged parts.
-  const bool packed = source == S3H_SOURCE_PINNED && n > 64 && sorted[0] <= kGroupMaxPart;
+  // So are more than kPinnedStageMin ragged pinned parts (the slice pipeline stages them).
+  const bool packed = source == S3H_SOURCE_PINNED && n > 64 &&
+                      (sorted[0] <= kGroupMaxPart || (n > kPinnedStageMin && sorted[0] != sorted[n - 1]));
   if (packed) source = S3H_SOURCE_PAGEABLE;
   if (source == S3H_SOURCE_PINNED) return split_choose(M, sorted.data(), n, ndevices, source, 0, ws);
   const unsigned T = unsigned(std::max(1, M.cpu_threads));

@@ -132,7 +132,8 @@ def split_ref_tg(lengths, m, tg, ndevices=0, source="pinned"):
 def split_ref(lengths, m, ndevices=0, source="pinned"):
     """The whole plan: tg = 0 for pinned parts, else the best of T x {1, 4, 6, 8, 9} / 12; many
     small pinned parts (the group pipeline packs them) are planned as staged."""
-    if source == "pinned" and len(lengths) > 64 and max(lengths) <= MIB:
+    if source == "pinned" and len(lengths) > 64 and (
+            max(lengths) <= MIB or (len(lengths) > 1024 and max(lengths) != min(lengths))):
         source = "pageable"
     if source == "pinned":
         s_, k = split_ref_tg(lengths, m, 0, ndevices, source)
