@@ -400,7 +400,7 @@ Split split_plan(const s3h_route_model_t& M, const uint64_t* lengths, uint64_t n
   // Many small pinned parts go through the group pipeline (capi.hip run_host_groups), which
   // packs them with the copy threads once the CPU side has taken parts out of their range:
   // plan them as staged parts.
-  // So are more than kPinnedStageMin ragged pinned parts (the slice pipeline stages them).
+  // So are more than kPinnedStageMin (256) ragged pinned parts (the slice pipeline stages them).
   const bool packed = source == S3H_SOURCE_PINNED && n > 64 &&
                       (sorted[0] <= kGroupMaxPart || (n > kPinnedStageMin && sorted[0] != sorted[n - 1]));
   if (packed) source = S3H_SOURCE_PAGEABLE;

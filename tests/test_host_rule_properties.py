@@ -133,7 +133,7 @@ def split_ref(lengths, m, ndevices=0, source="pinned"):
     """The whole plan: tg = 0 for pinned parts, else the best of T x {1, 4, 6, 8, 9} / 12; many
     small pinned parts (the group pipeline packs them) are planned as staged."""
     if source == "pinned" and len(lengths) > 64 and (
-            max(lengths) <= MIB or (len(lengths) > 1024 and max(lengths) != min(lengths))):
+            max(lengths) <= MIB or (len(lengths) > 256 and max(lengths) != min(lengths))):
         source = "pageable"
     if source == "pinned":
         s_, k = split_ref_tg(lengths, m, 0, ndevices, source)
@@ -184,11 +184,13 @@ def test_route_split_on_c2_shapes():
 
 def test_route_split_plans_small_pinned_parts_as_staged():
     """Many small pinned parts go through the group pipeline, whose copy threads pack them once
-    the CPU side has taken parts out of their range: the split plan gives them staging
-    threads, exactly as for pageable parts."""
+    the CPU side has taken parts out of their range, and more than 256 ragged pinned parts are
+    staged: the split plan gives both staging threads, exactly as for pageable parts.  Equal
+    large parts (DMA'd as they are) keep every thread for the CPU side."""
     lens = list(np.random.default_rng(3).integers(1, MIB, 500))
     m = {**MODEL, "cpu_threads": 16}
     assert s3.route_split_estimate(lens, m, source="pinned") == s3.route_split_estimate(lens, m, source="pageable")
     assert s3.route_split_estimate(lens, m, source="pinned")[1] > 0
-    big = lens[:-1] + [2 * MIB]
-    assert s3.route_split_estimate(big, m, source="pinned")[1] == 0
+    assert s3.route_split_estimate(lens[:-1] + [2 * MIB], m, source="pinned")[1] > 0
+    assert s3.route_split_estimate([2 * MIB] * 500, m, source="pinned")[1] == 0
+    assert s3.route_split_estimate(lens[:200] + [2 * MIB], m, source="pinned")[1] == 0
