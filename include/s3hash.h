@@ -29,7 +29,10 @@
 extern "C" {
 #endif
 
-#define S3H_API_VERSION 1
+/* 2: s3h_route_rates_t / s3h_route_choose (size-carrying, digest sets), s3h_host_plan,
+ * s3h_host_alloc_ex, MD5 and dual routed entry points.  s3h_route_model_t keeps its round-5
+ * layout (8 fields) for good: new rates go to s3h_route_rates_t, which carries its size. */
+#define S3H_API_VERSION 2
 
 enum s3h_status {
   S3H_OK = 0,
@@ -83,6 +86,42 @@ int s3h_kernel_policy(int policy, int *previous);
  * *cpus (if non-null) receives that CPU count.  Needs no GPU.  The reference's jobs run on
  * the cores the host grants (lib/src/upload.cpp:136-140, std::async). */
 int s3h_host_threads(int ndevices, int *cpus);
+/* The host path's thread plan for a call over `ndevices` devices at PCI addresses
+ * pci_bus_ids[k] (null entries or a null array: no NUMA record), with the CPUs of
+ * `affinity_cpulist` ("0-63,128-191"; null: this process's affinity) under a cgroup quota of
+ * `cpu_quota` CPUs (0: none; < 0: this process's quota) -- pure host arithmetic over sysfs
+ * (S3H_SYSFS_ROOT replaces /sys), the rules the host pipeline and the split route apply, so an
+ * N-GPU host can be checked before it runs:
+ *   staging threads per device = min(16, max(1, cpus / ndevices)), each device's threads bound
+ *   to its node's CPUs within the affinity; the split route from pinned parts gives the CPU side
+ *   every thread, from staged sources each device tg of its share (1, 4, 6, 8, 9 twelfths) and
+ *   the CPU side the rest.  devices (if non-null) receives ndevices records. */
+typedef struct {
+  int cpus;                       /* affinity capped by ceil(quota) */
+  int affinity_cpus;
+  double cpu_quota;               /* the quota applied (0: none) */
+  int devices;
+  int staging_threads_per_device; /* host threads staging one device's pageable parts / files */
+  int threads;                    /* staging threads of the whole call */
+  int oversubscribed;             /* threads > cpus (ndevices > cpus: one thread each anyway) */
+  int below_saturation;           /* per-device staging < 6 threads: pageable sources below the
+                                     H2D rate of one device (profiles/r05_stage_threads_sweep.json) */
+  int node_oversubscribed;        /* some node's bound threads exceed its bindable CPUs */
+  int split_cpu_threads_pinned;   /* split route, pinned parts: the CPU side's threads */
+  int split_candidates;           /* split route, staged sources: staging-thread choices (0: none fits) */
+  int split_stage_min, split_stage_max;            /* per device */
+  int split_cpu_threads_min, split_cpu_threads_max; /* the CPU side's threads at those choices */
+} s3h_host_plan_t;
+typedef struct {
+  int node;            /* sysfs numa_node (-1: unknown) */
+  int bind_node;       /* node its threads and staging go to (-1: unbound) */
+  int bind_cpus;       /* CPUs its shard / copy threads bind to (0: unbound) */
+  int bind_first_cpu;  /* lowest and highest of them (-1: none) */
+  int bind_last_cpu;
+  int staging_threads;
+} s3h_host_plan_device_t;
+int s3h_host_plan(const char *const *pci_bus_ids, int ndevices, const char *affinity_cpulist,
+                  double cpu_quota, s3h_host_plan_t *plan, s3h_host_plan_device_t *devices);
 /* Number of visible HIP devices; S3H_ENODEV (and *count = 0) when there is none. */
 int s3h_device_count(int *count);
 /* PCI address of HIP device `device` as "dddd:bb:dd.f" (lowercase, NUL-terminated; len >= 13):
@@ -128,6 +167,12 @@ int s3h_host_numa_info(int device, s3h_host_numa_t *info);
  * (-1: the runtime's placement): an uploader's read buffers on its device's node.  Needs a
  * HIP device.  Free with s3h_host_free. */
 int s3h_host_alloc(int node, uint64_t bytes, void **out);
+/* The same with flags.  Default (and s3h_host_alloc): the node is PREFERRED -- when it is short
+ * of free memory the pages go to another node instead of the process being OOM-killed within
+ * the node.  S3H_HOST_ALLOC_STRICT binds the pages to the node (MPOL_BIND) after checking that
+ * the node has the bytes free (S3H_ENOMEM otherwise). */
+#define S3H_HOST_ALLOC_STRICT 1
+int s3h_host_alloc_ex(int node, uint64_t bytes, int flags, void **out);
 int s3h_host_free(void *p);
 /* NUMA node of the page holding host address p (get_mempolicy). */
 int s3h_mem_node(const void *p, int *node);
@@ -262,6 +307,9 @@ int s3h_sha256_md5_batch_host(const uint8_t *const *parts, const uint64_t *lengt
 /* Both digests of (file, offset, size) parts, each slice read once (pread into pinned
  * staging) and crossing PCIe once: s3h_sha256_file_parts for uploads that also send
  * Content-MD5.  Same arguments and errors as s3h_sha256_file_parts. */
+/* Content-MD5 of (file, offset, size) parts, as s3h_sha256_file_parts. */
+int s3h_md5_file_parts(const char *path, const uint64_t *offsets, const uint64_t *lengths,
+                       uint64_t n, uint32_t *digests, int ndevices, uint64_t slice_bytes);
 int s3h_sha256_md5_file_parts(const char *path, const uint64_t *offsets, const uint64_t *lengths,
                               uint64_t n, uint32_t *sha256_digests, uint32_t *md5_digests,
                               int ndevices, uint64_t slice_bytes);
@@ -270,32 +318,35 @@ int s3h_sha256_md5_batch_device(int device, const void *d_base, const uint64_t *
                                 uint32_t *d_md5, void *stream);
 
 /* ---------------------------------------------------------------- size-aware routing
- * One part's chain runs at ~69 MB/s on the GPU and ~1.5 GB/s on one SHA-NI core, so a batch
+ * One part's chain runs at ~69 MB/s on the GPU and ~2.5 GB/s on one SHA-NI core, so a batch
  * of a few large parts -- the per-job batches of lib/src/upload.cpp:89-110, 136-140 -- is
  * faster on the CPU drop-in, and a batch of hundreds is faster on the GPU.  The routed entry
- * points take a route: S3H_ROUTE_GPU = s3h_sha256_batch_host / s3h_sha256_file_parts
- * unchanged (the default everywhere); S3H_ROUTE_CPU = the lib/hash drop-in (sha256::sha256)
- * on s3h_host_threads' CPU count, parts longest first; S3H_ROUTE_AUTO = whichever the model
- * below estimates to finish first.  The model's rates are measured once per process on the
- * first AUTO call (~0.1 s: a lone GPU chain, a pinned 32 MiB H2D copy, a one-block host call,
- * the drop-in on one thread and on all of them, the threads' staging memcpy).  AUTO needs a
- * visible GPU (S3H_ENODEV otherwise): it chooses between two paths with identical digests and
- * is never a fallback for a missing device.
- * S3H_ROUTE_SPLIT = both at once: the CPU drop-in hashes the m longest parts on its threads
- * while the GPU host path hashes the rest (m from the model, s3h_route_split_estimate; a single
- * part goes to the GPU; for pageable parts and file ranges the host threads are divided
- * between the GPU side's staging and the CPU side, s3h_route_split_estimate); AUTO also
- * splits when the split is estimated at least 5 % faster than the better single route.
- * *taken (if non-null) receives the route that ran (S3H_ROUTE_GPU, _CPU or _SPLIT).
+ * points take a route: S3H_ROUTE_GPU = the batched host path unchanged (the default
+ * everywhere); S3H_ROUTE_CPU = the lib/hash drop-in (sha256::sha256, md5::md5, both digests in
+ * one pass over each part) on s3h_host_threads' CPU count, parts longest first; S3H_ROUTE_AUTO
+ * = whichever the model below estimates to finish first; S3H_ROUTE_SPLIT = both at once: the
+ * CPU drop-in hashes the m longest parts on its threads while the GPU host path hashes the rest
+ * (m from the model; a single part goes to the GPU; for pageable parts and file ranges the host
+ * threads are divided between the GPU side's staging and the CPU side).  AUTO also splits when
+ * the split is estimated at least 5 % faster than the better single route.  AUTO needs a
+ * visible GPU (S3H_ENODEV otherwise): it chooses between paths with identical digests and is
+ * never a fallback for a missing device.  *taken (if non-null) receives the route that ran.
  *   gpu_s = call_s + max(longest part / chain rate, bytes per device / feed rate)
  *           feed = h2d (pinned parts) or min(h2d, staged) (pageable parts, file ranges)
  *   cpu_s = (longest-first schedule of the parts on k = min(n, threads) threads) / (rate(k) / k)
- *           rate(k) = min(k x cpu_bytes_per_s, cpu_all_bytes_per_s) */
+ *           rate(k) = min(k x one-thread rate, all-threads rate)
+ * each for the digest set the call computes (SHA-256, MD5, or both), times the observed /
+ * predicted ratio of earlier routed calls (the model is measured lazily per digest set and per
+ * device, re-measured when a call diverges from its prediction by more than 25 % and every
+ * s3h_route_refresh_calls calls). */
 enum s3h_route { S3H_ROUTE_GPU = 0, S3H_ROUTE_CPU = 1, S3H_ROUTE_AUTO = 2, S3H_ROUTE_SPLIT = 3 };
+/* Digest sets of the routing model: rate arrays are indexed by (set - 1). */
+enum s3h_digests { S3H_DIGESTS_SHA256 = 1, S3H_DIGESTS_MD5 = 2, S3H_DIGESTS_BOTH = 3 };
+/* The SHA-256 model (layout frozen at API version 1 + round 5's two trailing doubles). */
 typedef struct {
   double cpu_bytes_per_s;   /* one host thread on the lib/hash drop-in (s3h_cpu_backend) */
-  double chain_bytes_per_s; /* one part's chain on the GPU (the skew kernel, a lone part) */
-  double h2d_bytes_per_s;   /* pinned host -> device copy, one device */
+  double chain_bytes_per_s; /* one part's chain on the GPU (the slowest visible device) */
+  double h2d_bytes_per_s;   /* pinned host -> device copy (the slowest visible device) */
   double call_s;            /* fixed cost of one host-path GPU call (setup, launch, sync) */
   int cpu_threads;          /* host threads of the CPU route (affinity and cgroup quota) */
   int devices;              /* visible HIP devices */
@@ -325,16 +376,72 @@ int s3h_route_estimate_ex(const s3h_route_model_t *m, const uint64_t *lengths, u
  * (*cpu_parts = 0 when n == 1).  Pinned parts: the CPU side gets all cpu_threads threads
  * (*stage_threads = 0).  Pageable parts / file ranges: each GPU shard stages with
  * *stage_threads = tg threads, fed at min(H2D, staged rate x tg / threads), and the CPU side
- * gets the rest at the all-threads rate per thread; tg is the best of threads x {1, 4, 6, 8, 9}
- * / 12 (env S3H_SPLIT_STAGE_THREADS fixes it). */
+ * gets the rest at the all-threads rate per thread; tg is the best of (threads / devices) x
+ * {1, 4, 6, 8, 9} / 12 (env S3H_SPLIT_STAGE_THREADS fixes it). */
 int s3h_route_split_estimate(const s3h_route_model_t *m, const uint64_t *lengths, uint64_t n,
                              int ndevices, int source, uint64_t *cpu_parts, int *stage_threads,
                              double *split_s);
+/* The whole model, every digest set, with the observed corrections.  The caller sets `size`
+ * (sizeof(s3h_route_rates_t) as it was compiled); the library writes at most that many bytes,
+ * so a caller built against an older, shorter struct keeps working. */
+typedef struct {
+  uint32_t size;                  /* in: the struct size the caller knows; out: bytes written */
+  uint32_t version;               /* out: the library's S3H_API_VERSION */
+  int cpu_threads;                /* host threads of the CPU route */
+  int devices;                    /* visible HIP devices */
+  double cpu_bytes_per_s[3];      /* one host thread, per digest set (index = set - 1) */
+  double cpu_all_bytes_per_s[3];  /* all cpu_threads threads, aggregate */
+  double chain_bytes_per_s[3];    /* one GPU chain (the slowest device); [2]: both digests from one grid */
+  double h2d_bytes_per_s;         /* pinned host -> device (the slowest device) */
+  double staged_bytes_per_s;      /* staging memcpy of all cpu_threads threads */
+  double call_s;                  /* fixed cost of one host-path GPU call */
+  double gpu_factor, cpu_factor;  /* observed / predicted wall time of routed calls (EWMA; 1: none) */
+  uint64_t measurements;          /* times the model was (re)measured */
+  uint64_t routed_calls;          /* AUTO / SPLIT calls observed */
+  uint64_t divergences;           /* calls that differed from their prediction by > 25 % */
+  double age_s;                   /* seconds since the last measurement */
+} s3h_route_rates_t;
+int s3h_route_rates(s3h_route_rates_t *r);
+/* AUTO's decision for digest set `digests` under rates *r (pure host arithmetic; reads at most
+ * r->size bytes, missing fields = 0, factors 0 = 1). */
+typedef struct {
+  int route;           /* S3H_ROUTE_GPU, _CPU or _SPLIT */
+  int stage_threads;   /* split: staging threads per GPU shard (0: pinned parts / no split) */
+  uint64_t cpu_parts;  /* split: the longest parts on the CPU (0: no split plan) */
+  double gpu_s, cpu_s; /* estimates with the observed factors */
+  double split_s;      /* the split plan's estimate (0: none) */
+} s3h_route_choice_t;
+int s3h_route_choose(const s3h_route_rates_t *r, int digests, const uint64_t *lengths, uint64_t n,
+                     int ndevices, int source, s3h_route_choice_t *out);
+/* One device's lone-chain rate for a digest set and its pinned H2D rate (measured on first use). */
+int s3h_route_device_rates(int device, int digests, double *chain_bytes_per_s,
+                           double *h2d_bytes_per_s);
+/* Re-measure the model after this many AUTO / SPLIT calls (default 64, env
+ * S3H_ROUTE_REFRESH_CALLS; 0: only on divergence).  *previous (if non-null) gets the old value. */
+int s3h_route_refresh_calls(int calls, int *previous);
+/* Measurement / test hook: multiply one measured rate by `factor` until the model is next
+ * measured -- a model taken while the GPU or the host was busy (tests/test_gpu_route_adapt.py). */
+enum s3h_rate { S3H_RATE_CHAIN = 0, S3H_RATE_H2D = 1, S3H_RATE_CPU = 2, S3H_RATE_STAGED = 3 };
+int s3h_route_scale(int which, double factor);
 int s3h_sha256_batch_routed(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                             uint32_t *digests, int ndevices, int route, int *taken);
 int s3h_sha256_file_parts_routed(const char *path, const uint64_t *offsets,
                                  const uint64_t *lengths, uint64_t n, uint32_t *digests,
                                  int ndevices, int route, int *taken);
+/* Content-MD5 of host parts on a route (the CPU side: md5::md5). */
+int s3h_md5_batch_routed(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
+                         uint32_t *digests, int ndevices, int route, int *taken);
+/* Both upload headers on a route: the GPU side is s3h_sha256_md5_batch_host /
+ * _file_parts (one grid, one PCIe pass), the CPU side hashes each part with SHA-256 and MD5 in
+ * one pass over memory (64 KiB chunks while they sit in cache); the model prices both digests
+ * (a CPU MD5 runs at ~0.8 GB/s per thread: the dual CPU route is ~4x slower per thread than
+ * SHA-256 alone, so the GPU wins at far fewer parts). */
+int s3h_sha256_md5_batch_routed(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
+                                uint32_t *sha256_digests, uint32_t *md5_digests, int ndevices,
+                                int route, int *taken);
+int s3h_sha256_md5_file_parts_routed(const char *path, const uint64_t *offsets,
+                                     const uint64_t *lengths, uint64_t n, uint32_t *sha256_digests,
+                                     uint32_t *md5_digests, int ndevices, int route, int *taken);
 
 /* ---------------------------------------------------------------- verification
  * Download-side check of parts against known digests (ranged GETs of
@@ -347,10 +454,10 @@ int s3h_verify_batch_device(int device, int algo, const void *d_base, const uint
 int s3h_verify_batch_host(int algo, const uint8_t *const *parts, const uint64_t *lengths,
                           uint64_t n, const uint32_t *expected, uint8_t *mismatch,
                           uint64_t *mismatches, int ndevices);
-/* The host form on a route (size-aware routing below): S3H_ROUTE_GPU = s3h_verify_batch_host;
- * CPU / SPLIT / AUTO hash SHA-256 as s3h_sha256_batch_routed does, then compare (the route
- * model prices SHA-256 only, so MD5 takes S3H_ROUTE_GPU and any other route is S3H_EINVAL).
- * *taken (if non-null) receives the route that ran. */
+/* The host form on a route (size-aware routing above): S3H_ROUTE_GPU = s3h_verify_batch_host;
+ * CPU / SPLIT / AUTO hash as s3h_sha256_batch_routed / s3h_md5_batch_routed do (either
+ * algorithm, priced by its own rates), then compare.  *taken (if non-null) receives the route
+ * that ran. */
 int s3h_verify_batch_routed(int algo, const uint8_t *const *parts, const uint64_t *lengths,
                             uint64_t n, const uint32_t *expected, uint8_t *mismatch,
                             uint64_t *mismatches, int ndevices, int route, int *taken);

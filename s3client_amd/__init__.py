@@ -12,7 +12,9 @@ from .hashing import (Plan, device_count, digests_to_text, generate_parts, hash_
                       route_model, route_estimate, route_split_estimate, sha256_batch_routed,
                       sha256_file_parts_routed, BufferParts, pci_numa, device_numa,
                       host_numa, host_numa_info, mem_node, PinnedBuffer,
-                      kernel_policy, dual_layout)
+                      kernel_policy, dual_layout, md5_batch_routed, sha256_md5_batch_routed,
+                      sha256_md5_file_parts_routed, md5_file_parts, route_rates, route_choose,
+                      route_device_rates, route_refresh_calls, route_scale, host_plan)
 from .upload import upload_parts_geometry, UploadPart
 from ._native import S3HashError, LIB_PATH
 
@@ -24,5 +26,8 @@ __all__ = ["BufferParts", "Plan", "device_count", "digests_to_text", "generate_p
            "sha256_md5_file_parts", "trim", "sha256_batch_host_on", "host_threads",
            "device_pci_bus_id", "route_model", "route_estimate", "route_split_estimate", "sha256_batch_routed",
            "sha256_file_parts_routed", "pci_numa", "device_numa", "host_numa", "host_numa_info",
-           "mem_node", "PinnedBuffer", "kernel_policy", "dual_layout",
+           "mem_node", "PinnedBuffer", "kernel_policy", "dual_layout", "md5_batch_routed",
+           "sha256_md5_batch_routed", "sha256_md5_file_parts_routed", "md5_file_parts",
+           "route_rates", "route_choose", "route_device_rates", "route_refresh_calls",
+           "route_scale", "host_plan",
            "upload_parts_geometry", "UploadPart", "S3HashError", "LIB_PATH"]

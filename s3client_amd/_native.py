@@ -43,6 +43,11 @@ C_ABI_SYMBOLS = (
     "s3h_host_numa_info", "s3h_host_alloc", "s3h_host_free", "s3h_mem_node",
     "s3h_route_estimate_ex", "s3h_kernel_policy", "s3h_stream_stats", "s3h_plan_dual_layout",
     "s3h_dual_layout", "s3h_route_split_estimate", "s3h_verify_batch_routed",
+    # round 6: digest-set routing, adaptive model, host thread plan, strict pinned allocation
+    "s3h_route_rates", "s3h_route_choose", "s3h_route_device_rates", "s3h_route_refresh_calls",
+    "s3h_route_scale", "s3h_md5_batch_routed", "s3h_sha256_md5_batch_routed",
+    "s3h_sha256_md5_file_parts_routed", "s3h_md5_file_parts", "s3h_host_plan",
+    "s3h_host_alloc_ex",
 )
 POLICY_IDS = {"throughput": 0, "efficiency": 1}
 POLICY_NAMES = {v: k for k, v in POLICY_IDS.items()}
@@ -59,6 +64,52 @@ class RouteModel(ctypes.Structure):
                 ("h2d_bytes_per_s", ctypes.c_double), ("call_s", ctypes.c_double),
                 ("cpu_threads", ctypes.c_int), ("devices", ctypes.c_int),
                 ("cpu_all_bytes_per_s", ctypes.c_double), ("staged_bytes_per_s", ctypes.c_double)]
+
+
+DIGESTS_SHA256, DIGESTS_MD5, DIGESTS_BOTH = 1, 2, 3
+DIGESTS_IDS = {"sha256": DIGESTS_SHA256, "md5": DIGESTS_MD5, "both": DIGESTS_BOTH}
+RATE_IDS = {"chain": 0, "h2d": 1, "cpu": 2, "staged": 3}
+HOST_ALLOC_STRICT = 1
+
+
+class RouteRates(ctypes.Structure):
+    """s3h_route_rates_t (include/s3hash.h): size-carrying, every digest set."""
+    _fields_ = [("size", ctypes.c_uint32), ("version", ctypes.c_uint32),
+                ("cpu_threads", ctypes.c_int), ("devices", ctypes.c_int),
+                ("cpu_bytes_per_s", ctypes.c_double * 3),
+                ("cpu_all_bytes_per_s", ctypes.c_double * 3),
+                ("chain_bytes_per_s", ctypes.c_double * 3),
+                ("h2d_bytes_per_s", ctypes.c_double), ("staged_bytes_per_s", ctypes.c_double),
+                ("call_s", ctypes.c_double), ("gpu_factor", ctypes.c_double),
+                ("cpu_factor", ctypes.c_double), ("measurements", ctypes.c_uint64),
+                ("routed_calls", ctypes.c_uint64), ("divergences", ctypes.c_uint64),
+                ("age_s", ctypes.c_double)]
+
+
+class RouteChoice(ctypes.Structure):
+    """s3h_route_choice_t (include/s3hash.h)."""
+    _fields_ = [("route", ctypes.c_int), ("stage_threads", ctypes.c_int),
+                ("cpu_parts", ctypes.c_uint64), ("gpu_s", ctypes.c_double),
+                ("cpu_s", ctypes.c_double), ("split_s", ctypes.c_double)]
+
+
+class HostPlan(ctypes.Structure):
+    """s3h_host_plan_t (include/s3hash.h)."""
+    _fields_ = [("cpus", ctypes.c_int), ("affinity_cpus", ctypes.c_int),
+                ("cpu_quota", ctypes.c_double), ("devices", ctypes.c_int),
+                ("staging_threads_per_device", ctypes.c_int), ("threads", ctypes.c_int),
+                ("oversubscribed", ctypes.c_int), ("below_saturation", ctypes.c_int),
+                ("node_oversubscribed", ctypes.c_int), ("split_cpu_threads_pinned", ctypes.c_int),
+                ("split_candidates", ctypes.c_int), ("split_stage_min", ctypes.c_int),
+                ("split_stage_max", ctypes.c_int), ("split_cpu_threads_min", ctypes.c_int),
+                ("split_cpu_threads_max", ctypes.c_int)]
+
+
+class HostPlanDevice(ctypes.Structure):
+    """s3h_host_plan_device_t (include/s3hash.h)."""
+    _fields_ = [("node", ctypes.c_int), ("bind_node", ctypes.c_int), ("bind_cpus", ctypes.c_int),
+                ("bind_first_cpu", ctypes.c_int), ("bind_last_cpu", ctypes.c_int),
+                ("staging_threads", ctypes.c_int)]
 
 
 class HostNuma(ctypes.Structure):
@@ -214,6 +265,30 @@ def lib() -> ctypes.CDLL:
                                                        ctypes.c_uint64, ctypes.c_void_p,
                                                        ctypes.c_int, ctypes.c_int,
                                                        ctypes.POINTER(ctypes.c_int)]
+            L.s3h_route_rates.argtypes = [ctypes.POINTER(RouteRates)]
+            L.s3h_route_choose.argtypes = [ctypes.POINTER(RouteRates), ctypes.c_int, u64p,
+                                           ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                           ctypes.POINTER(RouteChoice)]
+            L.s3h_route_device_rates.argtypes = [ctypes.c_int, ctypes.c_int,
+                                                 ctypes.POINTER(ctypes.c_double),
+                                                 ctypes.POINTER(ctypes.c_double)]
+            L.s3h_route_refresh_calls.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+            L.s3h_route_scale.argtypes = [ctypes.c_int, ctypes.c_double]
+            L.s3h_md5_batch_routed.argtypes = L.s3h_sha256_batch_routed.argtypes
+            L.s3h_sha256_md5_batch_routed.argtypes = [ctypes.POINTER(ctypes.c_void_p), u64p,
+                                                      ctypes.c_uint64, ctypes.c_void_p,
+                                                      ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                      ctypes.POINTER(ctypes.c_int)]
+            L.s3h_sha256_md5_file_parts_routed.argtypes = [ctypes.c_char_p, u64p, u64p,
+                                                           ctypes.c_uint64, ctypes.c_void_p,
+                                                           ctypes.c_void_p, ctypes.c_int,
+                                                           ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+            L.s3h_md5_file_parts.argtypes = L.s3h_sha256_file_parts.argtypes
+            L.s3h_host_plan.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                                        ctypes.c_char_p, ctypes.c_double,
+                                        ctypes.POINTER(HostPlan), ctypes.POINTER(HostPlanDevice)]
+            L.s3h_host_alloc_ex.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_void_p)]
             L.s3h_multipart_etag.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p,
                                              ctypes.c_uint64]
             L.s3h_stream_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64,

@@ -11,6 +11,7 @@
 #include <cpuid.h>
 #include <immintrin.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -19,6 +20,8 @@
 
 #include "../../../include/s3hash.h"
 #include "../../../include/sha256.h"
+#include "../../../include/md5.h"
+#include "cpu_hash.hpp"
 
 namespace {
 
@@ -241,6 +244,32 @@ void hmac256(const uint8_t *data, size_t length, const uint8_t *key, size_t key_
     std::memcpy(hmac_hash + 4 * i, &be, 4);
   }
 }
+
+// ------------------------------------------------------------------ block-level (cpu_hash.hpp)
+namespace s3h::cpu {
+
+void sha256_blocks(uint32_t st[8], const uint8_t *p, uint64_t nblk) { g_compress(st, p, nblk); }
+
+void sha256_final(uint32_t st[8], const uint8_t *data, uint64_t len, uint64_t total) {
+  digest_native(data, len, 8ull * total, st);
+}
+
+void sha256_md5(const uint8_t *data, uint64_t len, uint32_t sha[8], uint32_t md5[4]) {
+  constexpr uint64_t kChunk = 64ull << 10;  // both passes over a chunk hit L1/L2
+  sha256::init_hash(sha);
+  md5::init_hash(md5);
+  const uint64_t whole = len / 64 * 64;
+  for (uint64_t at = 0; at < whole; at += kChunk) {
+    const uint64_t nb = std::min(kChunk, whole - at) / 64;
+    g_compress(sha, data + at, nb);
+    md5_blocks(md5, data + at, nb);
+  }
+  sha256_final(sha, data + whole, len - whole, len);
+  md5_final(md5, data + whole, len - whole, len);
+  sha256::to_little(sha);
+}
+
+}  // namespace s3h::cpu
 
 // ------------------------------------------------------------------ C view (s3hash.h)
 extern "C" {

@@ -1,18 +1,25 @@
 // lib_md5.cpp -- CPU side of the MD5 drop-in (include/md5.h).  RFC 1321 MD5 with the state
 // and output layout of /root/reference/lib/hash/md5.cpp (digest bytes = state words in
-// little-endian memory order).
+// little-endian memory order), and the S3 multipart ETag built on it.
+//
+// The 64 steps are expanded at compile time (step index, round function, message word and
+// shift are template constants), so each step is a handful of register operations with no
+// table lookups or branches: the routed CPU path prices a dual-digest part by this loop.
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <utility>
 #include <vector>
 
 #include "../../../include/md5.h"
 #include "../../../include/s3hash.h"
+#include "../status.hpp"
+#include "cpu_hash.hpp"
 
 namespace {
 
-const uint32_t kT[64] = {
+constexpr uint32_t kT[64] = {
     0xd76aa478u, 0xe8c7b756u, 0x242070dbu, 0xc1bdceeeu, 0xf57c0fafu, 0x4787c62au, 0xa8304613u,
     0xfd469501u, 0x698098d8u, 0x8b44f7afu, 0xffff5bb1u, 0x895cd7beu, 0x6b901122u, 0xfd987193u,
     0xa679438eu, 0x49b40821u, 0xf61e2562u, 0xc040b340u, 0x265e5a51u, 0xe9b6c7aau, 0xd62f105du,
@@ -23,28 +30,50 @@ const uint32_t kT[64] = {
     0x432aff97u, 0xab9423a7u, 0xfc93a039u, 0x655b59c3u, 0x8f0ccc92u, 0xffeff47du, 0x85845dd1u,
     0x6fa87e4fu, 0xfe2ce6e0u, 0xa3014314u, 0x4e0811a1u, 0xf7537e82u, 0xbd3af235u, 0x2ad7d2bbu,
     0xeb86d391u};
-const uint8_t kS[4][4] = {{7, 12, 17, 22}, {5, 9, 14, 20}, {4, 11, 16, 23}, {6, 10, 15, 21}};
 
-inline uint32_t rl(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+// per round (16 steps): the left-rotation of step i & 3, and message word of step i
+constexpr int shift_of(int i) {
+  constexpr int s[4][4] = {{7, 12, 17, 22}, {5, 9, 14, 20}, {4, 11, 16, 23}, {6, 10, 15, 21}};
+  return s[i / 16][i % 4];
+}
+constexpr int word_of(int i) {
+  return i < 16 ? i : i < 32 ? (5 * i + 1) % 16 : i < 48 ? (3 * i + 5) % 16 : (7 * i) % 16;
+}
+
+inline uint32_t rotl(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+
+// Step I updates `a` from b, c, d (the caller rotates the names).  Round functions in their
+// select forms: F = d ^ (b & (c ^ d)), G = c ^ (d & (b ^ c)), H = b ^ c ^ d, I = c ^ (b | ~d).
+template <int I>
+inline void step(uint32_t& a, uint32_t b, uint32_t c, uint32_t d, const uint32_t* m) {
+  uint32_t f;
+  if constexpr (I < 16) f = d ^ (b & (c ^ d));
+  else if constexpr (I < 32) f = c ^ (d & (b ^ c));
+  else if constexpr (I < 48) f = b ^ c ^ d;
+  else f = c ^ (b | ~d);
+  a = b + rotl(a + f + kT[I] + m[word_of(I)], shift_of(I));
+}
+
+template <int G>
+inline void group(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, const uint32_t* m) {
+  step<4 * G + 0>(a, b, c, d, m);
+  step<4 * G + 1>(d, a, b, c, m);
+  step<4 * G + 2>(c, d, a, b, m);
+  step<4 * G + 3>(b, c, d, a, m);
+}
+
+template <int... G>
+inline void all_groups(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, const uint32_t* m,
+                       std::integer_sequence<int, G...>) {
+  (group<G>(a, b, c, d, m), ...);
+}
 
 void compress(uint32_t st[4], const uint8_t *p, uint64_t nblk) {
   for (; nblk; --nblk, p += 64) {
     uint32_t m[16];
     std::memcpy(m, p, 64);  // little-endian words on x86
     uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
-    for (int i = 0; i < 64; ++i) {
-      const int q = i >> 4;
-      uint32_t f;
-      int g;
-      switch (q) {
-        case 0: f = (b & c) | (~b & d); g = i; break;
-        case 1: f = (d & b) | (~d & c); g = (5 * i + 1) & 15; break;
-        case 2: f = b ^ c ^ d; g = (3 * i + 5) & 15; break;
-        default: f = c ^ (b | ~d); g = (7 * i) & 15; break;
-      }
-      const uint32_t nb = b + rl(a + f + kT[i] + m[g], kS[q][i & 3]);
-      a = d; d = c; c = b; b = nb;
-    }
+    all_groups(a, b, c, d, m, std::make_integer_sequence<int, 16>());
     st[0] += a; st[1] += b; st[2] += c; st[3] += d;
   }
 }
@@ -63,6 +92,15 @@ void finish(uint32_t st[4], const uint8_t *data, uint64_t len, uint64_t total) {
 }
 
 }  // namespace
+
+namespace s3h::cpu {
+
+void md5_blocks(uint32_t st[4], const uint8_t *p, uint64_t nblk) { compress(st, p, nblk); }
+void md5_final(uint32_t st[4], const uint8_t *data, uint64_t len, uint64_t total) {
+  finish(st, data, len, total);
+}
+
+}  // namespace s3h::cpu
 
 namespace md5 {
 
@@ -112,6 +150,25 @@ void md5_file(const char *fname, uint32_t hash[4]) {
 
 }  // namespace md5
 
-extern "C" void s3h_cpu_md5(const uint8_t *data, uint64_t length, uint32_t hash[4]) {
+extern "C" {
+
+void s3h_cpu_md5(const uint8_t *data, uint64_t length, uint32_t hash[4]) {
   md5::md5(data, size_t(length), hash);
 }
+
+// S3 multipart ETag (what CompleteMultipartUpload returns, multipart_upload.cpp:162-183):
+// hex(MD5(binary part MD5s concatenated in part order)) + "-" + part count.  The outer MD5
+// covers 16 B per part, so it runs on the MD5 drop-in.
+int s3h_multipart_etag(const uint32_t *md5_digests, uint64_t n, char *out, uint64_t out_len) {
+  using s3h::host::fail;
+  if (out && out_len) out[0] = '\0';
+  if (!out || out_len < S3H_ETAG_MAX) return fail(S3H_EINVAL, "multipart etag: need %d output bytes", S3H_ETAG_MAX);
+  if (n == 0 || !md5_digests) return fail(S3H_EINVAL, "multipart etag: no part digests");
+  uint32_t h[4];
+  md5::md5(reinterpret_cast<const uint8_t *>(md5_digests), size_t(16 * n), h);
+  md5::hash_to_text(h, out);
+  std::snprintf(out + 32, size_t(out_len - 32), "-%llu", static_cast<unsigned long long>(n));
+  return S3H_OK;
+}
+
+}  // extern "C"

@@ -12,13 +12,9 @@
 #include <stdint.h>
 
 #include "exp_config.hpp"
+#include "kernel_abi.hpp"
 
 namespace s3h {
-
-struct Slot {        // one upload part in a plan, slots sorted by block count (descending)
-  uint64_t off;      // byte offset of the part relative to the launch's base pointer
-  uint64_t len;      // part length in bytes (the full part, also for resumed launches)
-};
 
 // Round constants as compile-time literals (folded into SGPR/literal operands).
 #define S3H_K(i) ((uint32_t)(                                                            \
@@ -60,8 +56,7 @@ __device__ __forceinline__ void init_state(uint32_t s[8]) {
   s[4] = 0x510e527fu; s[5] = 0x9b05688cu; s[6] = 0x1f83d9abu; s[7] = 0x5be0cd19u;
 }
 
-// Number of 64-byte compressions for a message of `len` bytes: ceil((len + 9) / 64).
-__host__ __device__ __forceinline__ uint64_t nblocks(uint64_t len) { return (len + 72) >> 6; }
+// Slot, nblocks: kernel_abi.hpp (shared with the host).
 
 // One round with the state held in rotating names: only d and h are written.
 #define S3H_RND(a, b, c, d, e, f, g, h, wk)            \

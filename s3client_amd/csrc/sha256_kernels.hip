@@ -50,35 +50,7 @@
 
 namespace s3h {
 
-// LaunchArgs::flags
-constexpr uint32_t kNoPad = 1;   // hash only the slot's whole 64-B blocks; never pad or emit
-constexpr uint32_t kResume = 2;  // load the chaining state even at blk_begin == 0
-
-// Bits of the device error word (LaunchArgs::err).  Every host entry point reads the word
-// after its launches complete and fails the call when it is non-zero (capi.hip plan_check):
-// a launch whose digests may be wrong never returns S3H_OK.
-constexpr uint32_t kErrSyncTimeout = 1;  // a producer/consumer flag wait timed out
-
-struct LaunchArgs {
-  const uint8_t* base;       // part p's block b is at base + slots[p].off + 64*(b - blk_origin)
-  const Slot* slots;         // sorted by nblocks descending
-  const uint32_t* out_idx;   // slot -> output part (message) index
-  uint32_t* state;           // n*8 words (message order); may be null for single-launch plans
-  uint32_t* digests;         // n*8 words (part order), bswap32(H_i) like lib/hash to_little
-  const uint8_t* zero;       // 256 zero bytes: target of the loads of out-of-range lanes
-  const uint64_t* bits;      // per-message bit length for the padding (null: 8 * slot length)
-  uint64_t blk_begin, blk_end, blk_origin;
-  uint32_t n;
-  uint32_t flags;
-  // Clock probe (s3h_plan_set_clock_probe; skew kernel): per consumer wave, shader-clock and
-  // 100 MHz real-time counters at the start and end of its chain loop.  Null: off.
-  uint64_t* clocks;
-  // sha256_skew_pairs_kernel: the first `solo` workgroups run one group each (the longest
-  // parts, on a CU of their own), the rest two.  0 elsewhere.
-  uint32_t solo;
-  // Device error word of the plan (kErr* bits OR-ed in by global atomics; cleared by the host).
-  uint32_t* err;
-};
+// LaunchArgs, its flags and the error-word bits: kernel_abi.hpp (shared with the host).
 
 // Compressions the launch sequence runs for a slot of `len` bytes.
 __device__ __forceinline__ uint64_t slot_blocks(const LaunchArgs& A, uint64_t len) {
@@ -192,8 +164,6 @@ __device__ __forceinline__ void produce_block(const RawBlock& r, uint32_t sel, c
     buf[q][lane] = make_uint4(wk[4 * q], wk[4 * q + 1], wk[4 * q + 2], wk[4 * q + 3]);
 }
 
-constexpr int kPcThreads = 128;  // wave 0 consumer, wave 1 producer; 64 parts per workgroup
-
 __global__ __launch_bounds__(kPcThreads) void sha256_pc_kernel(LaunchArgs A) {
   __shared__ uint4 lds_wk[2][16][64];  // [buffer][group of 4 rounds][lane]: 32 KiB
 
@@ -282,8 +252,6 @@ __global__ __launch_bounds__(kPcThreads) void sha256_pc_kernel(LaunchArgs A) {
 // whatever the op (profiles/r01_ubench_valu_issue.txt), each chain runs ~1.35x faster.
 // Workgroup = 128 threads: wave 0 consumes 32 parts (64 lanes), wave 1 produces W+K for
 // those 32 parts, two blocks per step (lanes 0-31 even blocks, 32-63 odd blocks).
-constexpr int kPairThreads = 128;
-constexpr int kPairParts = 32;
 
 __device__ __forceinline__ uint32_t pair_chain(uint32_t lane) {
   return (lane >> 4) * 8u + ((lane >> 3) & 1u) * 4u + (lane & 3u);
@@ -465,7 +433,6 @@ __global__ __launch_bounds__(kPairThreads) void sha256_pair_kernel(LaunchArgs A)
 // per chain matches the pair kernel's once NC = 4.
 // Hazards: the first xor_dpp reads the rotation 3 instructions after it is written (2 wait
 // states needed); the a-quad's exchange reads T1 two instructions after the add3.
-constexpr int kQuadChainsPerWave = 8;
 
 // One quad round.  W+K reaches the e-quad by DPP broadcast: lane L of every quad holds W+K
 // rows L, L+4, L+8, L+12 (4 ds_read_b128 per block instead of 16), and the h+W+K precompute
@@ -1924,7 +1891,6 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
 
 // kBps = kMd5Bps (128 KiB of LDS: one workgroup per CU) while the grid fits one workgroup per
 // CU (<= 64 x CUs parts); kBps = 1 (32 KiB, several per CU) for larger batches (capi.hip).
-constexpr int kMd5Bps = S3H_EXP_MD5_BPS;
 template <int kBps>
 __global__ __launch_bounds__(kPcThreads) void md5_pc_kernel(LaunchArgs A) {
   __shared__ Md5Lds<kBps> L;
@@ -2045,11 +2011,7 @@ __global__ __launch_bounds__(256) void compare_digests_kernel(const uint32_t* go
 //   kSpliceGrow : carry[i][c:c+h] = chunk[0:h]           (still < 64 B buffered)
 //   kSpliceReset: carry[i][0:r] = chunk[tail:tail+r]     (the new < 64-B remainder)
 // The head block is built before the carry is overwritten (same thread, program order).
-struct SpliceJob {
-  uint64_t src, tail;  // chunk start / new-remainder start, offsets from the update's base
-  uint32_t c, h, r, mode;
-};
-constexpr uint32_t kSpliceHead = 1, kSpliceGrow = 2, kSpliceReset = 4;
+// (SpliceJob and its modes: kernel_abi.hpp)
 
 __global__ __launch_bounds__(256) void stream_splice_kernel(const uint8_t* base,
                                                             const SpliceJob* jobs, uint8_t* carry,
@@ -2085,7 +2047,7 @@ __global__ __launch_bounds__(256) void stream_init_kernel(uint32_t* state, uint6
 // ------------------------------------------------------------- synthetic input generator
 // G(seed, p, L) of SURVEY.md 8(d): word j of part p is splitmix64(x0 + (j+1)*golden),
 // x0 = seed ^ p*0xD1B54A32D192ED03, serialised little-endian.  Parts must start 8-B aligned.
-struct GenPart { uint64_t off, len, id; };
+// (GenPart: kernel_abi.hpp)
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

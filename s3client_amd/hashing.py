@@ -303,8 +303,9 @@ def verify_batch_host(parts: Sequence, expected, algo: str = "sha256",
 
 def verify_batch_routed(parts: Sequence, expected, algo: str = "sha256", ndevices: int = 0,
                         route: str = "auto") -> tuple[np.ndarray, str]:
-    """verify_batch_host on a route (s3h_verify_batch_routed): "gpu", or for SHA-256 "cpu",
-    "split" or "auto" as sha256_batch_routed.  Returns (bool mismatch mask, route taken)."""
+    """verify_batch_host on a route (s3h_verify_batch_routed): "gpu", "cpu", "split" or "auto"
+    as sha256_batch_routed / md5_batch_routed, for either algorithm.  Returns (bool mismatch
+    mask, route taken)."""
     a = _native.ALGO_IDS[algo]
     words = _native.DIGEST_WORDS[a]
     if len(expected) and isinstance(expected[0], str):
@@ -543,6 +544,136 @@ def sha256_file_parts_routed(path: str, offsets, lengths, ndevices: int = 0,
     return out, _native.ROUTE_NAMES[taken.value]
 
 
+def md5_batch_routed(parts: Sequence, ndevices: int = 0, route: str = "auto") -> tuple[np.ndarray, str]:
+    """Content-MD5 of host parts on a route (s3h_md5_batch_routed): ((n, 4) uint32, taken)."""
+    arrs, ptrs, lens = _host_parts(parts)
+    out = np.zeros((len(arrs), 4), dtype=np.uint32)
+    taken = ctypes.c_int(-1)
+    check(lib().s3h_md5_batch_routed(ptrs, _p64(lens), len(arrs), out.ctypes.data, ndevices,
+                                     _native.ROUTE_IDS[route], ctypes.byref(taken)))
+    return out, _native.ROUTE_NAMES[taken.value]
+
+
+def sha256_md5_batch_routed(parts: Sequence, ndevices: int = 0,
+                            route: str = "auto") -> tuple[np.ndarray, np.ndarray, str]:
+    """x-amz-content-sha256 AND Content-MD5 of host parts on a route -- "gpu" (one grid, one
+    PCIe pass: sha256_md5_batch_host), "cpu" (both digests per part in one pass over memory),
+    "split" or "auto" (priced with the dual rates) -- s3h_sha256_md5_batch_routed.  Returns
+    ((n, 8) SHA-256 words, (n, 4) MD5 words, route taken)."""
+    arrs, ptrs, lens = _host_parts(parts)
+    sha = np.zeros((len(arrs), DIGEST_WORDS), dtype=np.uint32)
+    m5 = np.zeros((len(arrs), 4), dtype=np.uint32)
+    taken = ctypes.c_int(-1)
+    check(lib().s3h_sha256_md5_batch_routed(ptrs, _p64(lens), len(arrs), sha.ctypes.data,
+                                            m5.ctypes.data, ndevices, _native.ROUTE_IDS[route],
+                                            ctypes.byref(taken)))
+    return sha, m5, _native.ROUTE_NAMES[taken.value]
+
+
+def sha256_md5_file_parts_routed(path: str, offsets, lengths, ndevices: int = 0,
+                                 route: str = "auto") -> tuple[np.ndarray, np.ndarray, str]:
+    """Both digests of file ranges on a route (s3h_sha256_md5_file_parts_routed)."""
+    offs, lens = _u64(offsets), _u64(lengths)
+    if offs.shape != lens.shape or offs.ndim != 1 or offs.size == 0:
+        raise ValueError("offsets and lengths must be 1-D, equal length and non-empty")
+    sha = np.zeros((offs.size, DIGEST_WORDS), dtype=np.uint32)
+    m5 = np.zeros((offs.size, 4), dtype=np.uint32)
+    taken = ctypes.c_int(-1)
+    check(lib().s3h_sha256_md5_file_parts_routed(os.fsencode(path), _p64(offs), _p64(lens),
+                                                 offs.size, sha.ctypes.data, m5.ctypes.data,
+                                                 ndevices, _native.ROUTE_IDS[route],
+                                                 ctypes.byref(taken)))
+    return sha, m5, _native.ROUTE_NAMES[taken.value]
+
+
+def md5_file_parts(path: str, offsets, lengths, ndevices: int = 0, slice_bytes: int = 0) -> np.ndarray:
+    """Content-MD5 of file ranges on the GPU (s3h_md5_file_parts): (n, 4) uint32."""
+    offs, lens = _u64(offsets), _u64(lengths)
+    if offs.shape != lens.shape or offs.ndim != 1 or offs.size == 0:
+        raise ValueError("offsets and lengths must be 1-D, equal length and non-empty")
+    out = np.zeros((offs.size, 4), dtype=np.uint32)
+    check(lib().s3h_md5_file_parts(os.fsencode(path), _p64(offs), _p64(lens), offs.size,
+                                   out.ctypes.data, ndevices, slice_bytes))
+    return out
+
+
+def route_rates() -> dict:
+    """The whole routing model -- per digest set (index 0 SHA-256, 1 MD5, 2 both) the one-thread
+    and all-threads CPU rates and the GPU chain rate, H2D / staging rates, call cost, the
+    observed GPU / CPU factors, measurement and divergence counters (s3h_route_rates; measures
+    what is missing).  Lists for the per-digest-set arrays."""
+    r = _native.RouteRates()
+    r.size = ctypes.sizeof(r)
+    check(lib().s3h_route_rates(ctypes.byref(r)))
+    out = {}
+    for f, _ in r._fields_:
+        v = getattr(r, f)
+        out[f] = list(v) if isinstance(v, ctypes.Array) else v
+    return out
+
+
+def route_choose(lengths, rates: dict, digests: str = "sha256", ndevices: int = 0,
+                 source: str = "pinned") -> dict:
+    """AUTO's decision under ``rates`` (route_rates()'s dict, possibly edited; pure host
+    arithmetic, s3h_route_choose): route, gpu_s, cpu_s, split_s, cpu_parts, stage_threads."""
+    r = _native.RouteRates()
+    for f, _ in r._fields_:
+        if f in rates:
+            v = rates[f]
+            if isinstance(v, (list, tuple)):
+                arr = getattr(r, f)
+                for i, x in enumerate(v):
+                    arr[i] = x
+            else:
+                setattr(r, f, v)
+    r.size = ctypes.sizeof(r)
+    lens = _u64(lengths)
+    c = _native.RouteChoice()
+    check(lib().s3h_route_choose(ctypes.byref(r), _native.DIGESTS_IDS[digests], _p64(lens), lens.size,
+                                 ndevices, _native.SOURCE_IDS[source], ctypes.byref(c)))
+    return {"route": _native.ROUTE_NAMES[c.route], "gpu_s": c.gpu_s, "cpu_s": c.cpu_s,
+            "split_s": c.split_s, "cpu_parts": c.cpu_parts, "stage_threads": c.stage_threads}
+
+
+def route_device_rates(device: int, digests: str = "sha256") -> tuple[float, float]:
+    """(lone-chain bytes/s, pinned H2D bytes/s) of one device (s3h_route_device_rates)."""
+    ch, h = ctypes.c_double(), ctypes.c_double()
+    check(lib().s3h_route_device_rates(device, _native.DIGESTS_IDS[digests], ctypes.byref(ch),
+                                       ctypes.byref(h)))
+    return ch.value, h.value
+
+
+def route_refresh_calls(calls: int) -> int:
+    """Re-measure the routing model every ``calls`` AUTO/SPLIT calls (0: only on divergence);
+    returns the previous setting (s3h_route_refresh_calls)."""
+    prev = ctypes.c_int(0)
+    check(lib().s3h_route_refresh_calls(int(calls), ctypes.byref(prev)))
+    return prev.value
+
+
+def route_scale(rate: str, factor: float) -> None:
+    """Test hook: multiply one measured rate ("chain", "h2d", "cpu", "staged") by ``factor``
+    until the model is next measured (s3h_route_scale)."""
+    check(lib().s3h_route_scale(_native.RATE_IDS[rate], float(factor)))
+
+
+def host_plan(pci_bus_ids, affinity: str | None = None, cpu_quota: float = -1.0) -> dict:
+    """The host path's thread plan for a call over the devices at ``pci_bus_ids`` (None
+    entries: no NUMA record) -- per-device staging threads, bind node and CPUs, split-route
+    thread shares, oversubscription flags -- with the CPUs of ``affinity`` (a cpulist; None:
+    this process) under a ``cpu_quota`` (0: none; < 0: this process's cgroup): s3h_host_plan,
+    pure host arithmetic over sysfs (S3H_SYSFS_ROOT)."""
+    n = len(pci_bus_ids)
+    ids = (ctypes.c_char_p * n)(*[None if b is None else b.encode() for b in pci_bus_ids])
+    plan = _native.HostPlan()
+    devs = (_native.HostPlanDevice * n)()
+    check(lib().s3h_host_plan(ids, n, None if affinity is None else affinity.encode(),
+                              float(cpu_quota), ctypes.byref(plan), devs))
+    out = {f: getattr(plan, f) for f, _ in plan._fields_}
+    out["per_device"] = [{f: getattr(d, f) for f, _ in d._fields_} for d in devs]
+    return out
+
+
 def host_threads(ndevices: int = 1) -> tuple[int, int]:
     """(staging threads per device when ``ndevices`` device shards run at once, CPUs this
     process may use: affinity capped by the cgroup quota) -- s3h_host_threads."""
@@ -602,10 +733,11 @@ class PinnedBuffer:
     e.g. an uploader's read buffer on its device's node.  ``array`` is a uint8 numpy view (it
     keeps the buffer alive); the memory is freed when the last view is gone or on close()."""
 
-    def __init__(self, nbytes: int, node: int = -1):
+    def __init__(self, nbytes: int, node: int = -1, strict: bool = False):
         import weakref
         p = ctypes.c_void_p()
-        check(lib().s3h_host_alloc(int(node), int(nbytes), ctypes.byref(p)))
+        flags = _native.HOST_ALLOC_STRICT if strict else 0
+        check(lib().s3h_host_alloc_ex(int(node), int(nbytes), flags, ctypes.byref(p)))
         self.ptr, self.nbytes, self.node = p.value, int(nbytes), int(node)
         raw = (ctypes.c_uint8 * self.nbytes).from_address(self.ptr)
         # freed once the ctypes array -- held by this object and by every numpy view -- is gone
