@@ -32,12 +32,14 @@
 //                    is forwarded into the signature as DoUploadFilePart does (:81-86).
 //   --per-job        one batch call per job thread at the same time (std::async per job, as
 //                    upload.cpp:136-140 runs UploadParts), instead of one call for all parts.
-//   --route R        gpu (default) | cpu | auto: where the SHA-256 hashing runs.  auto decides
-//                    once for the whole upload with the measured model (sha256::choose_route:
-//                    a few large parts go to the CPU drop-in, hundreds to the GPU); a CPU
-//                    decision hashes per job as --cpu does, overlapped with the PUTs; split
-//                    hashes each GPU call's longest parts on the CPU drop-in beside the GPU
-//                    (S3H_ROUTE_SPLIT).
+//   --route R        gpu (default) | cpu | auto | split: where the hashing runs -- SHA-256, or
+//                    SHA-256 + MD5 with --content-md5 / --check-etag.  auto decides once for the
+//                    whole upload with the measured model, priced for the digests the upload
+//                    computes (sha256::choose_route: a few large parts go to the CPU drop-in,
+//                    hundreds to the GPU, the split in between); a CPU decision hashes per job as
+//                    --cpu does, overlapped with the PUTs; split hashes each GPU call's longest
+//                    parts on the CPU drop-in beside the GPU (S3H_ROUTE_SPLIT), both digests
+//                    there too.
 //
 //   s3-upload-hash -f FILE [-j JOBS] [-n PARTS_PER_JOB] [--source file|mmap|memory] [--per-job]
 //                  [--cpu] [--verify] [--print-headers] [--send] [--get-verify] [--retries N]
@@ -434,12 +436,17 @@ int main(int argc, char** argv) {
   // decision hashes exactly as --cpu does -- each job thread hashes its own parts with the
   // drop-in and PUTs them as it goes, so hashing overlaps the uploads -- and a GPU decision as
   // the default GPU path.
+  // The decision prices what this upload computes: with --content-md5 (or --check-etag) each
+  // part needs both digests, and the CPU side runs MD5 as well as SHA-256 (pricing
+  // only SHA-256 under-priced the CPU near the crossover).  AUTO may also pick the split.
   double est_gpu = 0, est_cpu = 0;
   if (!cpu && route != sha256::Route::gpu && route != sha256::Route::split) {
     try {
       route_taken = route == sha256::Route::cpu
                         ? sha256::Route::cpu
-                        : sha256::choose_route(lens, devices, &est_gpu, &est_cpu);
+                        : sha256::choose_route(lens, devices, &est_gpu, &est_cpu,
+                                               want_md5 ? S3H_DIGESTS_BOTH : S3H_DIGESTS_SHA256,
+                                               source == "file" ? S3H_SOURCE_FILE : S3H_SOURCE_PAGEABLE);
     } catch (const std::exception& e) {
       std::fprintf(stderr, "%s\n", e.what());
       return 1;
@@ -546,10 +553,14 @@ int main(int argc, char** argv) {
       l.push_back(lens[i]);
       o.push_back(offs[i]);
     }
-    if (want_md5) {  // both digests, each slice read and copied once
-      const sha256::DualDigests d = source == "file"
-                                        ? sha256::file_part_sha256_md5(file, o, l, devices)
-                                        : sha256::sha256_md5_batch(p, l, devices);
+    if (want_md5) {  // both digests, each slice read and copied once; --route split (or
+                     // AUTO's split) puts each call's longest parts on the CPU, both digests there too
+      const bool split = route_taken == sha256::Route::split;
+      const sha256::DualDigests d =
+          source == "file" ? (split ? sha256::file_part_sha256_md5_routed(file, o, l, devices, sha256::Route::split)
+                                    : sha256::file_part_sha256_md5(file, o, l, devices))
+                           : (split ? sha256::sha256_md5_routed(p, l, devices, sha256::Route::split)
+                                    : sha256::sha256_md5_batch(p, l, devices));
       for (size_t k = 0; k < idx.size(); ++k) {
         char t[65];
         sha256::hash_to_text(const_cast<uint32_t*>(&d.sha256[8 * k]), t);

@@ -1103,8 +1103,9 @@ def c5_loopback(data, offs, lens, gd, nparts: int = 128, jobs: int = 16, repeat:
     complete; --repeat: the last pass) for the
     GPU batch (one call, and one call per job: merged on the device), the CPU SHA-NI drop-in
     and its scalar loop (lib/hash-like cost), the size-aware route (--route auto: the measured
-    model picks the GPU or the CPU drop-in for the batch; `auto_route` says which), plus the
-    GPU hash alone."""
+    model picks the GPU, the CPU drop-in or the split for the batch; `auto_route` says which),
+    the same three with Content-MD5 as well (`*_md5`: both digests per part; AUTO priced for
+    both, `auto_md5_route`), plus the GPU hash alone."""
     import re
     import subprocess
     import tempfile
@@ -1145,6 +1146,11 @@ def c5_loopback(data, offs, lens, gd, nparts: int = 128, jobs: int = 16, repeat:
                                      ("cpu_shani", send + ["--cpu"], {}),
                                      ("cpu_scalar", send + ["--cpu"], {"S3H_CPU_SCALAR": "1"}),
                                      ("auto", send + ["--route", "auto"], {}),
+                                     # both upload headers (Content-MD5 + x-amz-content-sha256):
+                                     # AUTO prices the CPU side with MD5 too (round 6)
+                                     ("gpu_md5", send + ["--content-md5"], {}),
+                                     ("cpu_shani_md5", send + ["--cpu", "--content-md5"], {}),
+                                     ("auto_md5", send + ["--route", "auto", "--content-md5"], {}),
                                      ("gpu_hash_only", [], {})):
                 r = subprocess.run([app, "-f", path, "-j", str(jobs), "-n", str(nparts // jobs),
                                     "--endpoint", url, "--repeat", str(repeat), *extra],
@@ -1159,9 +1165,9 @@ def c5_loopback(data, offs, lens, gd, nparts: int = 128, jobs: int = 16, repeat:
                 if extra:
                     me = re.search(r"object etag (\S+)", r.stderr)
                     etags[name] = me.group(1) if me else None
-                if name == "auto":
+                if name in ("auto", "auto_md5"):
                     ra = re.search(r"route auto -> (\w+)", r.stderr)
-                    res["auto_route"] = ra.group(1) if ra else None
+                    res[f"{name}_route"] = ra.group(1) if ra else None
             with urllib.request.urlopen(url + "/stats", timeout=10) as f:
                 res["server"] = json.loads(f.read())
             res["object_etags_match"] = bool(etags) and all(

@@ -61,18 +61,25 @@ inline std::vector<std::string> to_hex(const std::vector<uint32_t>& d) {
   return out;
 }
 
-// AUTO's decision for a batch of parts of `lengths` without running it (s3h_route_model, measured
-// once per process, + s3h_route_estimate): Route::gpu or Route::cpu, and both estimates.  An
-// uploader that hashes per job decides once for the whole upload with this, then hashes each
-// job's parts on that route.
+// AUTO's decision for a batch of parts of `lengths` without running it (s3h_route_rates,
+// measured on first use and kept current by routed calls, + s3h_route_choose): Route::gpu,
+// Route::cpu or Route::split, and the GPU / CPU estimates.  `digests` is what the caller will
+// compute (S3H_DIGESTS_SHA256, or S3H_DIGESTS_BOTH for Content-MD5 + x-amz-content-sha256: the
+// CPU side is then priced at the MD5 + SHA-256 rate), `source` where the parts are
+// (S3H_SOURCE_PINNED / _PAGEABLE / _FILE).  An uploader that hashes per job decides once for
+// the whole upload with this, then hashes each job's parts on that route.
 inline Route choose_route(const std::vector<uint64_t>& lengths, int ndevices = 0,
-                          double* gpu_s = nullptr, double* cpu_s = nullptr) {
+                          double* gpu_s = nullptr, double* cpu_s = nullptr,
+                          int digests = S3H_DIGESTS_SHA256, int source = S3H_SOURCE_PINNED) {
   if (lengths.empty()) throw std::invalid_argument("choose_route: no parts");
-  s3h_route_model_t m;
-  batch_check(s3h_route_model(&m));
-  const int r = s3h_route_estimate(&m, lengths.data(), lengths.size(), ndevices, gpu_s, cpu_s);
-  if (r < 0) batch_check(r);
-  return Route(r);
+  s3h_route_rates_t r{};
+  r.size = sizeof r;
+  batch_check(s3h_route_rates(&r));
+  s3h_route_choice_t c{};
+  batch_check(s3h_route_choose(&r, digests, lengths.data(), lengths.size(), ndevices, source, &c));
+  if (gpu_s) *gpu_s = c.gpu_s;
+  if (cpu_s) *cpu_s = c.cpu_s;
+  return Route(c.route);
 }
 
 // 64-char lowercase hex per part: the `payloadHash` strings S3Api::UploadFilePart takes
@@ -144,6 +151,35 @@ inline DualDigests file_part_sha256_md5(const std::string& path, const std::vect
   if (!offsets.empty())
     batch_check(s3h_sha256_md5_file_parts(path.c_str(), offsets.data(), lengths.data(),
                                           offsets.size(), d.sha256.data(), d.md5.data(), ndevices, 0));
+  return d;
+}
+
+// Both digests on a route (s3h_sha256_md5_batch_routed / s3h_sha256_md5_file_parts_routed):
+// Route::gpu = the one-grid dual pass, Route::cpu = SHA-256 + MD5 per part in one pass over
+// memory on the host threads, Route::split = the longest parts on the CPU while the GPU hashes
+// the rest, Route::automatic = the model's pick for both digests.  *taken: the route that ran.
+inline DualDigests sha256_md5_routed(const std::vector<const uint8_t*>& parts,
+                                     const std::vector<uint64_t>& lengths, int ndevices = 0,
+                                     Route route = Route::automatic, Route* taken = nullptr) {
+  if (parts.size() != lengths.size()) throw std::invalid_argument("parts/lengths size mismatch");
+  DualDigests d{std::vector<uint32_t>(8 * parts.size()), std::vector<uint32_t>(4 * parts.size())};
+  int t = int(route);
+  if (!parts.empty())
+    batch_check(s3h_sha256_md5_batch_routed(parts.data(), lengths.data(), parts.size(), d.sha256.data(),
+                                            d.md5.data(), ndevices, int(route), &t));
+  if (taken) *taken = Route(t);
+  return d;
+}
+inline DualDigests file_part_sha256_md5_routed(const std::string& path, const std::vector<uint64_t>& offsets,
+                                               const std::vector<uint64_t>& lengths, int ndevices = 0,
+                                               Route route = Route::automatic, Route* taken = nullptr) {
+  if (offsets.size() != lengths.size()) throw std::invalid_argument("offsets/lengths size mismatch");
+  DualDigests d{std::vector<uint32_t>(8 * offsets.size()), std::vector<uint32_t>(4 * offsets.size())};
+  int t = int(route);
+  if (!offsets.empty())
+    batch_check(s3h_sha256_md5_file_parts_routed(path.c_str(), offsets.data(), lengths.data(), offsets.size(),
+                                                 d.sha256.data(), d.md5.data(), ndevices, int(route), &t));
+  if (taken) *taken = Route(t);
   return d;
 }
 

@@ -938,6 +938,16 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
 #pragma unroll
     for (uint32_t r = 0; r < kItems; ++r) S3H_PRODUCE(ra[r], za[r], r, p[r], bh[r], rows(0, h[r]));
     S3H_SYNC_PRODUCED(1u);
+#ifdef S3H_EXP_PRODUCER_IDLE  // experiment (power): after step 0 the shared-SIMD producer only
+                              // keeps the flag protocol; the consumers hash stale W+K
+    if constexpr (FLAGS && SIMPLE) {
+      for (uint64_t k = 1; k <= steps; ++k) {
+        if (k < steps && k >= 2) flag_wait_ge(&flags[1], uint32_t(k - 1), alive, A.err);
+        S3H_SYNC_PRODUCED(uint32_t(k + 1));
+      }
+      return;
+    }
+#endif
     // Step k goes into buffer k & 1, which held step k - 2: FLAGS waits until the consumer
     // has released that step (the barrier of the other mode orders the same thing).
     for (uint64_t k = 1; k <= steps; k += 2) {
@@ -974,6 +984,16 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
   // ------------------------------------------------------------------ consumer
 #ifdef S3H_EXP_LONE_CONSUMER  // experiment: only consumer wave 0 works (wrong digests)
   if (role != 0) return;
+#endif
+#ifdef S3H_EXP_CONSUMER_IDLE  // experiment (power): the shared-SIMD consumers only keep the
+                              // flag protocol; the producers run alone (wrong digests)
+  if constexpr (FLAGS && SIMPLE) {
+    for (uint32_t j = 0; j < uint32_t(steps); ++j) {
+      flag_wait_ge(&flags[0], j + 1, alive, A.err);
+      flag_publish(&flags[1], j + 1);
+    }
+    return;
+  }
 #endif
   __builtin_amdgcn_s_setprio(3);
   const bool ahalf = (lane >> 2) & 1u;

@@ -3,6 +3,7 @@
 // sha256_stream (lib/hash/sha256.cpp:84-144) for the appends and the DOCUMENTED contract of
 // sha256_next (sha256.h:73-89) for the finish.
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -87,12 +88,13 @@ constexpr uint64_t kStreamDmaChunks = 64;
 constexpr uint64_t kStreamSubBytes = 128ull << 20;
 constexpr uint64_t kStreamSubMin = 64ull << 10;
 
-// Test hook: S3H_TEST_STREAM_FAIL_SUB=k fails the k-th sub-update of every
-// s3h_stream_update_host call before its copy (tests/test_gpu_stream.py).
+// Test hook: S3H_TEST_STREAM_FAIL_SUB=k fails the k-th sub-update of the FIRST
+// s3h_stream_update_host call that reaches it, before its copy (tests/test_gpu_stream.py).
 const long g_fail_stream_sub = [] {
   const char* e = std::getenv("S3H_TEST_STREAM_FAIL_SUB");
   return e && *e ? std::atol(e) : -1L;
 }();
+std::atomic<bool> g_fail_stream_fired{false};
 
 // Host-form staging of destroyed stream objects, kept per device for the next object (an
 // uploader creates one per batch of objects: allocating, first-touching and registering 2 x 64
@@ -624,7 +626,8 @@ int s3h_stream_update_host(s3h_stream_t S, const uint8_t* const* chunks, const u
   bool queued = false;
   auto one = [&](const uint8_t* const* c, const uint64_t* l) {
     int rc;
-    if (g_fail_stream_sub >= 0 && sub == uint64_t(g_fail_stream_sub))  // test hook (env)
+    if (g_fail_stream_sub >= 0 && sub == uint64_t(g_fail_stream_sub) &&  // test hook (env)
+        !g_fail_stream_fired.exchange(true))
       rc = fail(S3H_ENOMEM, "stream update: injected failure of sub-update %llu", (unsigned long long)sub);
     else
       rc = stream_host_update_one(S, c, l, &queued);

@@ -566,7 +566,7 @@ def test_route_split_vs_oracle(torch_cuda, oracle, tmp_path, layout):
 def test_verify_routed(torch_cuda, oracle, kind):
     """Download-side verification on every route (s3h_verify_batch_routed): ragged parts, about
     3 % of the expected digests corrupted in one bit; the mismatch mask is exactly the
-    corrupted set on gpu / cpu / split / auto, and MD5 verifies on the GPU route."""
+    corrupted set on gpu / cpu / split / auto, for SHA-256 and (round 6) MD5 alike."""
     torch = torch_cuda
     rng = np.random.default_rng(77 + len(kind))
     n = 700
@@ -586,8 +586,10 @@ def test_verify_routed(torch_cuda, oracle, kind):
         assert taken == route or route == "auto", (route, taken)
     m5 = oracle.md5_batch(src, offs, lens).copy()
     m5[bad, 0] ^= np.uint32(1)
-    mask, taken = s3.verify_batch_routed(parts, m5, algo="md5", route="gpu")
-    assert np.array_equal(mask, bad) and taken == "gpu"
+    for route in ("gpu", "cpu", "split", "auto"):
+        mask, taken = s3.verify_batch_routed(parts, m5, algo="md5", route=route)
+        assert np.array_equal(mask, bad), route
+        assert taken == route or route == "auto", (route, taken)
 
 
 def test_concurrent_split_and_auto_callers(torch_cuda, oracle, tmp_path):
@@ -734,3 +736,53 @@ def test_many_small_parts_in_groups(torch_cuda, oracle, tmp_path, layout):
             got = s3.sha256_batch_host(s3.BufferParts(buf, offs, lens))
     bad = np.flatnonzero((got != want).any(axis=1))
     assert bad.size == 0, (layout, bad[:8])
+
+
+def test_group_dma_spans_one_pinned_allocation(torch_cuda, oracle, tmp_path):
+    """Advisor r5 (high): many small pinned parts that form one increasing address range are
+    DMA'd as that range -- only when the range lies inside ONE pinned allocation.  Parts taken
+    from 120 separately pinned buffers, passed in increasing address order, have unregistered
+    pages (or other allocations) between them: they must be packed like pageable parts, and
+    every digest must equal the oracle's.  The same parts inside one pinned buffer still go as
+    one range (S3H_TRACE_HOST reports which, in a child process)."""
+    import subprocess
+    import sys
+    torch = torch_cuda
+    rng = np.random.default_rng(911)
+    n = 120
+    lens = rng.integers(1, 60000, n)
+    bufs = [s3.PinnedBuffer(int(L) + 4096) for L in lens]
+    order = sorted(range(n), key=lambda i: bufs[i].ptr)
+    views = []
+    for i in order:
+        a = bufs[i].array[:int(lens[i])]
+        a[:] = rng.integers(0, 256, a.size, dtype=np.uint8)
+        views.append(a)
+    want = np.stack([oracle.sha256(v.tobytes()) for v in views])
+    got = s3.sha256_batch_host(views)
+    assert np.array_equal(got, want)
+    sha, m5 = s3.sha256_md5_batch_host(views)
+    assert np.array_equal(sha, want)
+    assert np.array_equal(m5, np.stack([oracle.md5(v.tobytes()) for v in views]))
+    code = f"""
+import sys; sys.path.insert(0, {repr(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))})
+import numpy as np, torch, s3client_amd as s3
+rng = np.random.default_rng(5)
+n = 120
+lens = rng.integers(1, 60000, n)
+bufs = [s3.PinnedBuffer(int(L) + 4096) for L in lens]
+order = sorted(range(n), key=lambda i: bufs[i].ptr)
+apart = [bufs[i].array[:int(lens[i])] for i in order]
+one = torch.empty(int(lens.sum()) + 64 * n, dtype=torch.uint8, pin_memory=True)
+offs = np.concatenate([[0], np.cumsum(lens + 64)[:-1]])
+s3.sha256_batch_host(apart)
+s3.sha256_batch_host(s3.BufferParts(one, offs, lens))
+print("ok")
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env={**os.environ, "S3H_TRACE_HOST": "1"})
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-3000:]
+    groups = [l for l in r.stderr.splitlines() if "groups of" in l]
+    assert len(groups) == 2, r.stderr[-3000:]
+    assert groups[0].endswith("(staged)"), groups  # separate allocations: packed
+    assert groups[1].endswith("(pinned ranges)"), groups  # one buffer: one DMA per group

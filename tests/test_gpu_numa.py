@@ -105,3 +105,25 @@ def test_registered_buffer_takes_the_pinned_path(torch_cuda):
                        env={**os.environ, "S3H_TRACE_HOST": "1"}, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "pinned 2-D" in r.stderr, r.stderr
+
+
+def test_strict_and_preferred_placement(torch_cuda, oracle):
+    """Advisor r5: staging and s3h_host_alloc PREFER their node (a short node spills to another
+    instead of OOM-killing the process); S3H_HOST_ALLOC_STRICT binds, after checking the node's
+    free memory -- a request beyond it fails cleanly with S3H_ENOMEM, before any page is touched."""
+    dn = s3.device_numa(0)["node"]
+    node = dn if dn >= 0 else 0
+    rng = np.random.default_rng(53)
+    data, offs, lens = _parts(rng, n=16, L=MIB)
+    for strict in (False, True):
+        buf = s3.PinnedBuffer(data.size, node, strict=strict)
+        buf.array[:] = data
+        assert s3.mem_node(buf.array) == node and s3.mem_node(buf.array[-1:]) == node
+        got = s3.sha256_batch_host(s3.BufferParts(buf.array, offs, lens), ndevices=1)
+        assert np.array_equal(got, oracle.batch(data, offs, lens))
+        buf.close()
+    with pytest.raises(s3.S3HashError) as e:  # 64 TiB on one node: refused, not OOM-killed
+        s3.PinnedBuffer(64 << 40, node, strict=True)
+    assert e.value.code == -4 and "strict" in str(e.value)
+    with pytest.raises(s3.S3HashError):
+        s3._native.check(s3._native.lib().s3h_host_alloc_ex(node, 4096, 8, None))

@@ -5,6 +5,8 @@ contract (lib/hash/sha256.h:73-89): the digest must equal the one-shot digest of
 concatenation of every chunk (oracle_sha256 / oracle_md5 over the joined bytes), bit-exact,
 for every chunk schedule -- empty chunks, chunks that stay inside one block, chunks that
 complete a carried block exactly, multi-block chunks at any alignment."""
+import os
+
 import numpy as np
 import pytest
 
@@ -320,3 +322,53 @@ def test_stream_host_updates_pipelined_and_buffer_reuse(torch_cuda, oracle, pinn
             want = np.stack([oracle.sha256(bytes(m)) for m in msgs])
             bad = [i for i in range(n) if not np.array_equal(got[i], want[i])]
             assert not bad, (f, bad[:8])
+
+
+_SUB_FAIL_CHILD = r"""
+import sys, json
+sys.path.insert(0, sys.argv[1])
+import os
+
+import numpy as np
+import s3client_amd as s3
+from tests.oracle_lib import Oracle
+rng = np.random.default_rng(31)
+big = [rng.integers(0, 256, 200 << 20, dtype=np.uint8) for _ in range(2)]  # 4 sub-updates each
+small = [rng.integers(0, 256, 1000 + i, dtype=np.uint8) for i in range(2)]
+out = {}
+st = s3.Stream(2)
+try:
+    st.update(big)
+    out["first"] = 0
+except s3.S3HashError as e:
+    out["first"], out["first_msg"] = e.code, str(e)
+try:
+    st.update(small)
+    out["second"] = 0
+    out["digests_ok"] = bool(np.array_equal(st.final(), np.stack([Oracle().sha256(s.tobytes()) for s in small])))
+except s3.S3HashError as e:
+    out["second"], out["second_msg"] = e.code, str(e)
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("fail_sub", [0, 1])
+def test_stream_update_fails_midway(torch_cuda, fail_sub):
+    """Advisor r5: a large host update is appended as sub-updates; when sub-update k fails
+    (S3H_TEST_STREAM_FAIL_SUB injects it before its copy), the call returns the error after the
+    copy stream has drained.  k > 0: the earlier sub-updates were appended, so the object is
+    failed -- the next call returns S3H_EINVAL instead of appending those pieces twice.  k = 0:
+    nothing was appended or queued, the object stays usable and its digests are right."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _SUB_FAIL_CHILD, root], capture_output=True, text=True,
+                       timeout=300, cwd=root, env={**os.environ, "S3H_TEST_STREAM_FAIL_SUB": str(fail_sub)})
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["first"] == -4 and f"injected failure of sub-update {fail_sub}" in out["first_msg"], out
+    if fail_sub == 0:
+        assert out["second"] == 0 and out["digests_ok"], out
+    else:
+        assert out["second"] == -1 and "failed earlier" in out["second_msg"], out

@@ -1,7 +1,9 @@
 """Differential fuzz against the REAL reference lib/hash (oracle/_ref/libref_hash.so, built from
-/root/reference by oracle/Makefile).  Runs where that library exists (the build container;
-it also travels to the GPU box).  Compares reference, oracle and the product CPU drop-in on
-random lengths 0..64 KiB, block-boundary lengths and a few large sizes."""
+/root/reference by oracle/Makefile).  Runs only where that library exists -- the build
+container: oracle/_ref is git-ignored AND listed in .gpurunignore, so the reference's compiled
+code never travels to the GPU box (and the test skips there).  Compares reference, oracle and
+the product CPU drop-in on random lengths 0..64 KiB, block-boundary lengths and a few large
+sizes."""
 import ctypes
 import hashlib
 import os

@@ -9,7 +9,12 @@ and record the model's estimates and AUTO's choice beside the measured medians. 
 must equal the device-resident run's.  One JSON object on stdout; `auto_over_best` = AUTO's
 median / the fastest forced route's (the bar: <= 1.10).
 
-    python3 tools/route_sweep.py [--reps 3] [--ns 8,32,...]
+`--dual` (round 6): both upload digests (Content-MD5 + x-amz-content-sha256)
+through s3h_sha256_md5_batch_routed, the model's estimates from s3h_route_choose for the dual
+digest set; every SHA-256 and MD5 digest vs the device-resident dual run.  The bar: AUTO within
+5 % of the fastest forced route for n = 8 ... 1,024.
+
+    python3 tools/route_sweep.py [--reps 3] [--ns 8,32,...] [--dual]
 """
 from __future__ import annotations
 
@@ -32,6 +37,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--ns", default="8,32,64,128,256,512,1024")
     ap.add_argument("--sources", default="pinned,pageable")
+    ap.add_argument("--dual", action="store_true", help="both digests (SHA-256 + MD5)")
     a = ap.parse_args()
     import torch
 
@@ -43,7 +49,11 @@ def main():
     dev = torch.device("cuda", 0)
     data = torch.empty(N * L, dtype=torch.uint8, device=dev)
     s3.generate_parts(data, offs, lens, np.arange(N), SEED)
-    ref = s3.sha256_batch_device(data, offs, lens).cpu().numpy().view(np.uint32)
+    if a.dual:
+        rs, rm = s3.sha256_md5_batch_device(data, offs, lens)
+        ref = (rs.cpu().numpy().view(np.uint32), rm.cpu().numpy().view(np.uint32))
+    else:
+        ref = s3.sha256_batch_device(data, offs, lens).cpu().numpy().view(np.uint32)
     bufs = {}
     if "pinned" in a.sources:
         pb = s3.PinnedBuffer(N * L, s3.device_numa(0)["node"])
@@ -57,27 +67,39 @@ def main():
     torch.cuda.empty_cache()
     t0 = time.perf_counter()
     model = s3.route_model()
-    out = {"model": model, "model_measure_s": round(time.perf_counter() - t0, 3),
+    rates = s3.route_rates()
+    out = {"model": model, "rates": rates, "digests": "sha256+md5" if a.dual else "sha256",
+           "model_measure_s": round(time.perf_counter() - t0, 3),
            "part_bytes": L, "reps": a.reps, "cpu_backend": s3.cpu_backend(),
            "host_threads": s3.host_threads(1), "rows": [], "mismatches": 0}
     worst = 0.0
     for src, (_, arr) in bufs.items():
         for n in ns:
             parts = s3.BufferParts(arr, offs[:n], lens[:n])
-            est_route, g_est, c_est = s3.route_estimate(lens[:n], model, pinned=src == "pinned")
-            k_est, tg_est, s_est = s3.route_split_estimate(lens[:n], model, source=src)
+            if a.dual:
+                ch = s3.route_choose(lens[:n], s3.route_rates(), "both", source=src)
+                est_route, g_est, c_est = ch["route"], ch["gpu_s"], ch["cpu_s"]
+                k_est, tg_est, s_est = ch["cpu_parts"], ch["stage_threads"], ch["split_s"]
+            else:
+                est_route, g_est, c_est = s3.route_estimate(lens[:n], model, pinned=src == "pinned")
+                k_est, tg_est, s_est = s3.route_split_estimate(lens[:n], model, source=src)
             times = {r: [] for r in ("gpu", "cpu", "split", "auto")}
             taken = None
             for k in range(a.reps + 1):
                 for r in times:
                     t1 = time.perf_counter()
-                    d, tk = s3.sha256_batch_routed(parts, ndevices=1, route=r)
+                    if a.dual:
+                        ds, dm, tk = s3.sha256_md5_batch_routed(parts, ndevices=1, route=r)
+                    else:
+                        d, tk = s3.sha256_batch_routed(parts, ndevices=1, route=r)
                     dt = time.perf_counter() - t1
                     if k:
                         times[r].append(dt)
                     if r == "auto":
                         taken = tk
-                    out["mismatches"] += int(not np.array_equal(d, ref[:n]))
+                    ok = (np.array_equal(ds, ref[0][:n]) and np.array_equal(dm, ref[1][:n])) if a.dual \
+                        else np.array_equal(d, ref[:n])
+                    out["mismatches"] += int(not ok)
             med = {r: float(np.median(v)) for r, v in times.items()}
             ratio = med["auto"] / min(med["gpu"], med["cpu"], med["split"])
             worst = max(worst, ratio)
@@ -95,6 +117,7 @@ def main():
                   f"auto {med['auto']:.4f} ({taken}) model gpu {g_est:.4f} cpu {c_est:.4f} split {s_est:.4f} ({k_est})",
                   file=sys.stderr, flush=True)
     out["worst_auto_over_best"] = round(worst, 4)
+    out["rates_after"] = s3.route_rates()
     print(json.dumps(out))
     return 0 if out["mismatches"] == 0 else 3
 
