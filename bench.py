@@ -990,7 +990,11 @@ def single_gpu_config(s3, torch, dev, cfg: str, ident: dict, steps: int = 2) -> 
     algo = part_bytes + 32 * len(lens)
     kernels = {}
     gd = info = None
-    for kern in (("auto",) if cfg == "c3" else ("auto", "skewp")):
+    # C4 times both kernels AUTO chooses between (by s3h_kernel_policy) explicitly, so the line
+    # carries skews and skewp whichever the default policy picks on this board
+    with s3.Plan(offs, lens, device=dev.index) as p:
+        info = p.info()
+    for kern in (("auto",) if cfg == "c3" else ("skews", "skewp")):
         plan = s3.Plan(offs, lens, device=dev.index, kernel=kern)
         kinfo = plan.info()
         out = torch.zeros((len(lens), 8), dtype=torch.int32, device=dev)
@@ -1027,10 +1031,15 @@ def single_gpu_config(s3, torch, dev, cfg: str, ident: dict, steps: int = 2) -> 
             "parity": {"fixtures_checked": len(checked), "mismatches": int(bad)}}
         kernels[kinfo["kernel"]].update(energy(kernels[kinfo["kernel"]]["power"],
                                                part_bytes / 2**30 / wall))
-        if kern == "auto":
-            gd, info = kd, kinfo
+        if gd is None:
+            gd = kd
+            if kern == "auto":
+                info = kinfo
         elif not np.array_equal(kd, gd):
-            kernels[kinfo["kernel"]]["digests_match_auto"] = False
+            kernels[kinfo["kernel"]]["digests_match_other_kernel"] = False
+        if kinfo["kernel"] == info["kernel"]:
+            auto_digests = kd
+    gd = auto_digests
     dual = _dual_on(s3, torch, dev, data, ids, lens, offs, cfg, stream, gd, info) if cfg == "c3" else None
     del data
     torch.cuda.empty_cache()
@@ -1045,21 +1054,23 @@ def single_gpu_config(s3, torch, dev, cfg: str, ident: dict, steps: int = 2) -> 
     if len(kernels) > 1:
         res["kernels"] = kernels
         # s3h_kernel_policy: AUTO under "throughput" = the faster kernel, under "efficiency"
-        # = the lower energy-delay product (J/GiB x s/GiB)
+        # = the lower energy-delay product (J/GiB x s/GiB), under "power" (the default) skews
+        # only when the board's power cap lets it hold its clock
         ok = {k: v for k, v in kernels.items() if v.get("energy_delay_J_s_per_GiB2")}
-        prev = s3.kernel_policy("efficiency")
-        try:
-            with s3.Plan(offs, lens, device=dev.index) as p:
-                eff_kernel = p.info()["kernel"]
-        finally:
-            s3.kernel_policy(prev)
-        if ok:
-            res["policy_choice"] = {
-                "measured_faster": max(kernels, key=lambda k: kernels[k]["GiBps"]),
-                "measured_lower_energy_delay": min(
-                    ok, key=lambda k: ok[k]["energy_delay_J_s_per_GiB2"]),
-                "auto_throughput_policy": info["kernel"],
-                "auto_efficiency_policy": eff_kernel}
+        chosen = {}
+        for pol in ("throughput", "efficiency", "power"):
+            prev = s3.kernel_policy(pol)
+            try:
+                with s3.Plan(offs, lens, device=dev.index) as p:
+                    chosen[pol] = p.info()["kernel"]
+            finally:
+                s3.kernel_policy(prev)
+        res["policy_choice"] = {
+            "measured_faster": max(kernels, key=lambda k: kernels[k]["GiBps"]),
+            "measured_lower_energy_delay": min(
+                ok, key=lambda k: ok[k]["energy_delay_J_s_per_GiB2"]) if ok else None,
+            "board_power_cap_W": s3.device_power_cap(dev.index),
+            **{f"auto_{pol}_policy": k for pol, k in chosen.items()}}
     if dual:
         res["sha256_md5"] = dual
     return res
@@ -1208,10 +1219,12 @@ def c4_shard(args, s3, torch, dist, dev, rank, world, local, ident, ph, steps: i
     fx = golden_fixtures("c4", "sha256")
     gib_gpu = per * L * steps / 2**30
     algo = per * (L + 32)  # bytes read once + digests written, per GPU per launch
+    with s3.Plan(offs, lens, device=local) as p:  # AUTO under the current (default) policy
+        auto_kernel = p.info()["kernel"]
     res = {"workload": f"C4: {per} x 8 MiB per GPU, {per * world} parts over {world} GPUs "
-                       "(part p on rank p % N)", "steps": steps, "kernels": {}}
+                       "(part p on rank p % N)", "steps": steps, "kernels": {}, "kernel": auto_kernel}
     ph.mark("c4 generate")
-    for kern in ("auto", "skewp"):
+    for kern in ("skews", "skewp"):  # both C4 kernels whatever AUTO's policy picks
         plan = s3.Plan(offs, lens, device=local, kernel=kern)
         info = plan.info()
         out = torch.zeros((per, 8), dtype=torch.int32, device=dev)
@@ -1253,8 +1266,6 @@ def c4_shard(args, s3, torch, dist, dev, rank, world, local, ident, ph, steps: i
             "board_W_max_per_gpu": [p.get("max_W") for p in pws],
             "parity": {"fixtures_checked": sum(x[2] for x in r), "mismatches": sum(x[3] for x in r),
                        "fixtures_checked_per_rank": [x[2] for x in r]}}
-        if kern == "auto":
-            res["kernel"] = info["kernel"]
         ph.mark(f"c4 {info['kernel']}")
     del data
     torch.cuda.empty_cache()
@@ -1262,6 +1273,7 @@ def c4_shard(args, s3, torch, dist, dev, rank, world, local, ident, ph, steps: i
     res.update({k: auto[k] for k in ("per_gpu_GiBps", "aggregate_GiBps", "ms_per_step_max_rank",
                                      "hbm_roofline_frac_per_gpu", "parity")})
     res["faster_kernel"] = max(res["kernels"], key=lambda k: res["kernels"][k]["aggregate_GiBps"])
+    res["board_power_cap_W"] = s3.device_power_cap(local)
     return res
 
 

@@ -58,12 +58,16 @@ enum s3h_algo {
   S3H_ALGO_MD5 = 1     /* MD5 (Content-MD5, multipart ETags), digests n x 4 words */
 };
 
-/* What AUTO optimises when several kernels fit a batch (s3h_kernel_policy):
- * S3H_POLICY_THROUGHPUT (default) -- the fastest kernel; S3H_POLICY_EFFICIENCY -- the lowest
- * energy-delay product.  They differ only for 4,097 - 32 x CUs parts (8,192 on MI355X: the C4
- * shard), where the shared-SIMD SKEWS kernel is 8.6 % faster than SKEWP but draws 1.2-1.4 kW
- * against 0.8 kW (2.44 vs 1.66 J/GiB): EFFICIENCY runs SKEWP there. */
-enum s3h_policy { S3H_POLICY_THROUGHPUT = 0, S3H_POLICY_EFFICIENCY = 1 };
+/* What AUTO optimises when several kernels fit a batch (s3h_kernel_policy).  They differ only
+ * for 4,097 - 32 x CUs parts (8,192 on MI355X: the C4 shard), where the shared-SIMD SKEWS
+ * kernel is ~5 % faster than SKEWP but draws 1.26-1.34 kW against 0.77 kW (2.57 vs 1.65 J/GiB):
+ * S3H_POLICY_THROUGHPUT -- SKEWS; S3H_POLICY_EFFICIENCY -- SKEWP (the lower energy-delay
+ * product); S3H_POLICY_POWER (default since API 2) -- SKEWS only when the device's board power
+ * cap (sysfs hwmon power1_cap, s3h_device_power_cap) lets it hold its full clock (>= 1,450 W:
+ * consumers and producers together need more than MI355X's 1,400 W cap), SKEWP
+ * otherwise.  Initial value from the environment: S3H_KERNEL_POLICY=throughput|efficiency|power
+ * (S3H_PREFER_EFFICIENCY=1 = efficiency). */
+enum s3h_policy { S3H_POLICY_THROUGHPUT = 0, S3H_POLICY_EFFICIENCY = 1, S3H_POLICY_POWER = 2 };
 
 /* Last error message of the calling thread ("" if none). */
 const char *s3h_last_error(void);
@@ -76,9 +80,11 @@ int s3h_api_version(void);
  * into one batch (their digests are the same as from separate calls).  s3h_trim releases the
  * contexts of idle devices. */
 int s3h_trim(void);
-/* Set AUTO's kernel policy for plans created afterwards (initially S3H_POLICY_EFFICIENCY when
- * the environment has S3H_PREFER_EFFICIENCY=1); *previous receives the old one.  No GPU. */
+/* Set AUTO's kernel policy for plans created afterwards (initially S3H_POLICY_POWER, see
+ * above); *previous receives the old one.  No GPU. */
 int s3h_kernel_policy(int policy, int *previous);
+/* Board power cap of HIP device `device` in watts as the POWER policy reads it (0: unknown). */
+int s3h_device_power_cap(int device, double *watts);
 /* Host threads (the calling thread included) the host path uses per device to stage
  * pageable parts and file ranges when `ndevices` device shards run at once: the CPUs this
  * process may use -- its sched_getaffinity mask, capped by the cgroup CPU quota (cpu.max, or
@@ -395,7 +401,8 @@ typedef struct {
   double h2d_bytes_per_s;         /* pinned host -> device (the slowest device) */
   double staged_bytes_per_s;      /* staging memcpy of all cpu_threads threads */
   double call_s;                  /* fixed cost of one host-path GPU call */
-  double gpu_factor, cpu_factor;  /* observed / predicted wall time of routed calls (EWMA; 1: none) */
+  double gpu_factor[3];           /* observed / predicted wall time of routed calls, per digest */
+  double cpu_factor[3];           /* set (EWMA; 1: none; 0 = 1 in s3h_route_choose) */
   uint64_t measurements;          /* times the model was (re)measured */
   uint64_t routed_calls;          /* AUTO / SPLIT calls observed */
   uint64_t divergences;           /* calls that differed from their prediction by > 25 % */
@@ -403,7 +410,7 @@ typedef struct {
 } s3h_route_rates_t;
 int s3h_route_rates(s3h_route_rates_t *r);
 /* AUTO's decision for digest set `digests` under rates *r (pure host arithmetic; reads at most
- * r->size bytes, missing fields = 0, factors 0 = 1). */
+ * r->size bytes, missing fields = 0, factors 0 = 1; the digest set's own factors apply). */
 typedef struct {
   int route;           /* S3H_ROUTE_GPU, _CPU or _SPLIT */
   int stage_threads;   /* split: staging threads per GPU shard (0: pinned parts / no split) */

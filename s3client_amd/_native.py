@@ -47,9 +47,9 @@ C_ABI_SYMBOLS = (
     "s3h_route_rates", "s3h_route_choose", "s3h_route_device_rates", "s3h_route_refresh_calls",
     "s3h_route_scale", "s3h_md5_batch_routed", "s3h_sha256_md5_batch_routed",
     "s3h_sha256_md5_file_parts_routed", "s3h_md5_file_parts", "s3h_host_plan",
-    "s3h_host_alloc_ex",
+    "s3h_host_alloc_ex", "s3h_device_power_cap",
 )
-POLICY_IDS = {"throughput": 0, "efficiency": 1}
+POLICY_IDS = {"throughput": 0, "efficiency": 1, "power": 2}
 POLICY_NAMES = {v: k for k, v in POLICY_IDS.items()}
 SOURCE_IDS = {"pinned": 0, "pageable": 1, "file": 2}
 NUMA_LOCAL, NUMA_OFF = -1, -2
@@ -80,8 +80,8 @@ class RouteRates(ctypes.Structure):
                 ("cpu_all_bytes_per_s", ctypes.c_double * 3),
                 ("chain_bytes_per_s", ctypes.c_double * 3),
                 ("h2d_bytes_per_s", ctypes.c_double), ("staged_bytes_per_s", ctypes.c_double),
-                ("call_s", ctypes.c_double), ("gpu_factor", ctypes.c_double),
-                ("cpu_factor", ctypes.c_double), ("measurements", ctypes.c_uint64),
+                ("call_s", ctypes.c_double), ("gpu_factor", ctypes.c_double * 3),
+                ("cpu_factor", ctypes.c_double * 3), ("measurements", ctypes.c_uint64),
                 ("routed_calls", ctypes.c_uint64), ("divergences", ctypes.c_uint64),
                 ("age_s", ctypes.c_double)]
 
@@ -173,6 +173,7 @@ def lib() -> ctypes.CDLL:
                                          ctypes.POINTER(ctypes.c_void_p)]
             L.s3h_host_free.argtypes = [ctypes.c_void_p]
             L.s3h_kernel_policy.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+            L.s3h_device_power_cap.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
             L.s3h_stream_stats.argtypes = [ctypes.c_void_p, u64p, u64p]
             L.s3h_plan_dual_layout.argtypes = [ctypes.c_void_p, u32p, ctypes.POINTER(ctypes.c_int)]
             L.s3h_dual_layout.argtypes = [u64p, ctypes.c_uint64, ctypes.c_int, u32p,

@@ -75,6 +75,7 @@ struct DeviceGuard {  // restores the calling thread's current device
 // ------------------------------------------------------------------ plans (plan.cpp)
 constexpr uint64_t kMaxParts = 1ull << 31;
 int device_cus(int device);  // cached CU count (0 if unknown)
+double device_power_cap_w(int device);  // cached board power cap in W (0 if unknown)
 uint64_t sort_slots(const uint64_t* offsets, const uint64_t* lengths, uint64_t n, bool nopad,
                     s3h::Slot* slots, uint32_t* order);
 uint32_t dual_mixed_solo(const s3h::Slot* slots, uint64_t n, uint64_t cus, bool* apart);

@@ -142,11 +142,24 @@ bool all_pinned(const uint8_t* const* parts, const uint64_t* lengths, const uint
 bool pinned_range(const void* p, uint64_t bytes) {
   if (!p || bytes == 0) return bytes == 0;
   const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + bytes;  // [lo, hi)
+  // The runtime's record of the allocation holding `a`: HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR /
+  // _RANGE_SIZE answer for hipHostMalloc'd and hipHostRegister'd memory alike;
+  // hipMemGetAddressRange only for the former (it returns base 0 for registered pages;
+  // profiles/r06_pinned_range_probe.jsonl).
   auto range_of = [](uintptr_t a, uintptr_t* base, size_t* size) {
-    hipDeviceptr_t b = nullptr;
+    void* b = nullptr;
     size_t s = 0;
-    if (hipMemGetAddressRange(&b, &s, reinterpret_cast<hipDeviceptr_t>(a)) == hipSuccess && b && s) {
+    void* const p = reinterpret_cast<void*>(a);
+    if (hipPointerGetAttribute(&b, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, p) == hipSuccess &&
+        hipPointerGetAttribute(&s, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, p) == hipSuccess && b && s) {
       *base = reinterpret_cast<uintptr_t>(b);
+      *size = s;
+      return true;
+    }
+    (void)hipGetLastError();
+    hipDeviceptr_t d = nullptr;
+    if (hipMemGetAddressRange(&d, &s, reinterpret_cast<hipDeviceptr_t>(a)) == hipSuccess && d && s) {
+      *base = reinterpret_cast<uintptr_t>(d);
       *size = s;
       return true;
     }

@@ -96,23 +96,39 @@ uint32_t plan_solo(const s3h::Slot* slots, uint64_t n, uint64_t cus) {
 
 // `cus`: the device's CUs.  Above 4,096 parts, while one 32-chain workgroup per CU holds the
 // batch (8,192 parts on MI355X: the C4 shard), the shared-SIMD skew kernel runs every chain
-// at the skew kernel's 8 VALU per round with its producer on the same SIMD: C4 shard 500 vs
-// 469 GiB/s for skewp on one box (profiles/r02_bench_c4_skews_mulf.jsonl), at about twice the
-// board power (r02_smi_c4_power.txt; INTEGRATION.md: pass S3H_KERNEL_SKEWP to trade it back).
-// Under S3H_POLICY_EFFICIENCY (s3h_kernel_policy; env S3H_PREFER_EFFICIENCY=1) AUTO keeps
-// skewp in that range: the C4 shard runs 8.6 % slower (464 vs 504 GiB/s) but at 1.66 instead
-// of 2.44 J/GiB (board 0.77 vs 1.23 kW, BENCH_r04 configs.c4.kernels) --
-// the lower energy-delay product (J/GiB x s/GiB: 3.6e-3 vs 4.9e-3).  Outside 4,097 - 32 x CUs
-// parts both policies choose the same kernel.
+// at the skew kernel's 8 VALU per round with its producer on the same SIMD: C4 shard 492.8 vs
+// 468.9 GiB/s for skewp (BENCH_r05 configs.c4.kernels), at 1.26 kW against 0.77 kW
+// (2.57 vs 1.65 J/GiB): skewp has the lower energy-delay product (J/GiB x s/GiB: 3.5e-3 vs
+// 5.2e-3).  The policy (s3h_kernel_policy) decides in that range:
+//   S3H_POLICY_THROUGHPUT  skews, always;
+//   S3H_POLICY_EFFICIENCY  skewp, always (env S3H_PREFER_EFFICIENCY=1);
+//   S3H_POLICY_POWER       (default) skews only where the board may draw what skews needs to
+//                          hold its full clock, else skewp.  Round 6's attribution
+//                          (profiles/r06_power_attribution.json, one lease): the consumers
+//                          alone on stale W+K draw 1.10 kW at 2.38 GHz, the producers alone
+//                          0.98 kW, together 1.34 kW against the 1.4 kW cap at 2.28 GHz -- the
+//                          consumers' round stream owns most of the power, and skews at full
+//                          clock would need ~1.45 kW.  So under a cap below kSkewsFullClockW
+//                          (MI355X: 1,400 W) skews only runs ~5 % faster than skewp for ~1.6x
+//                          its energy, and POWER picks skewp.
+// Outside 4,097 - 32 x CUs parts every policy chooses the same kernel.
+constexpr double kSkewsFullClockW = 1450.0;
 std::atomic<int> g_kernel_policy{[] {
   const char* e = std::getenv("S3H_PREFER_EFFICIENCY");
-  return e && std::atoi(e) == 1 ? S3H_POLICY_EFFICIENCY : S3H_POLICY_THROUGHPUT;
+  if (e && std::atoi(e) == 1) return int(S3H_POLICY_EFFICIENCY);
+  const char* k = std::getenv("S3H_KERNEL_POLICY");
+  if (k && std::strcmp(k, "throughput") == 0) return int(S3H_POLICY_THROUGHPUT);
+  if (k && std::strcmp(k, "efficiency") == 0) return int(S3H_POLICY_EFFICIENCY);
+  return int(S3H_POLICY_POWER);
 }()};
 
-int resolve_kernel(int algo, uint64_t n, int kernel, uint64_t cus) {
+int resolve_kernel(int algo, uint64_t n, int kernel, uint64_t cus, int device) {
   if (algo == S3H_ALGO_MD5) return S3H_KERNEL_PC;  // MD5 has one kernel (4 VALU per step)
   if (kernel != S3H_KERNEL_AUTO) return kernel;
-  const bool efficient = g_kernel_policy.load() == S3H_POLICY_EFFICIENCY;
+  const int policy = g_kernel_policy.load();
+  const bool efficient = policy == S3H_POLICY_EFFICIENCY ||
+                         (policy == S3H_POLICY_POWER && n > kQuadMaxParts && n <= 32 * cus &&
+                          device_power_cap_w(device) > 0 && device_power_cap_w(device) < kSkewsFullClockW);
   return n <= kQuadMaxParts    ? S3H_KERNEL_SKEW
          : n <= 32 * cus       ? (efficient ? S3H_KERNEL_SKEWP : S3H_KERNEL_SKEWS)
          : n <= kSkewpMaxParts ? S3H_KERNEL_SKEWP
@@ -162,6 +178,22 @@ const char* kernel_name(const s3h_plan_s* P) {
 }
 
 }  // namespace
+
+double device_power_cap_w(int device) {  // cached per device (sysfs hwmon power1_cap)
+  constexpr int kMaxDev = 64;
+  static std::atomic<double> cap[kMaxDev];
+  static std::atomic<bool> have[kMaxDev];
+  if (device < 0 || device >= kMaxDev) return 0;
+  if (!have[device].load(std::memory_order_acquire)) {
+    char bdf[32] = {0};
+    double w = 0;
+    if (hipDeviceGetPCIBusId(bdf, sizeof bdf, device) == hipSuccess) w = pci_power_cap_w(bdf);
+    else (void)hipGetLastError();
+    cap[device].store(w, std::memory_order_relaxed);
+    have[device].store(true, std::memory_order_release);
+  }
+  return cap[device].load(std::memory_order_relaxed);
+}
 
 int device_cus(int device) {  // cached: the host pipeline asks once per slice
   constexpr int kMaxDev = 64;
@@ -266,7 +298,7 @@ int plan_geometry(s3h_plan_s* P, const uint64_t* offsets, const uint64_t* length
   if (n > P->cap) return fail(S3H_EINVAL, "plan: %llu parts exceed capacity %llu",
                               (unsigned long long)n, (unsigned long long)P->cap);
   P->n = n;
-  P->kernel = resolve_kernel(P->algo, n, kernel, uint64_t(device_cus(P->device)));
+  P->kernel = resolve_kernel(P->algo, n, kernel, uint64_t(device_cus(P->device)), P->device);
   P->total_blocks = sort_slots(offsets, lengths, n, false, h_slots, h_order);
   P->max_blocks = s3h::nblocks(h_slots[0].len);
   P->quad_waves = quad_waves(n);
@@ -459,10 +491,18 @@ int batch_device(int device, int algo, const void* d_base, const uint64_t* offse
 extern "C" {
 
 int s3h_kernel_policy(int policy, int* previous) {
-  if (policy != S3H_POLICY_THROUGHPUT && policy != S3H_POLICY_EFFICIENCY)
+  if (policy != S3H_POLICY_THROUGHPUT && policy != S3H_POLICY_EFFICIENCY && policy != S3H_POLICY_POWER)
     return fail(S3H_EINVAL, "kernel policy: unknown policy %d", policy);
   const int prev = g_kernel_policy.exchange(policy);
   if (previous) *previous = prev;
+  return S3H_OK;
+}
+
+int s3h_device_power_cap(int device, double* watts) {
+  if (!watts) return fail(S3H_EINVAL, "device power cap: null argument");
+  *watts = 0;
+  if (int rc = check_device(device)) return rc;
+  *watts = device_power_cap_w(device);
   return S3H_OK;
 }
 

@@ -7,12 +7,17 @@
 // first call that shards onto it).  A measurement is a snapshot taken under whatever load the
 // host and the GPUs carry at that moment, so the model is not trusted forever:
 //   * every AUTO / SPLIT call times the route it ran -- both sides of a split separately --
-//     and keeps, per side (GPU, CPU), the ratio observed / predicted as an EWMA (weight 1/2,
-//     each observation clamped to [1/4, 8]); decisions scale that side's estimate by it, and
-//     the factor of a side a call did not use relaxes 10 % toward 1 per call;
+//     and keeps, per side (GPU, CPU) and digest set, the ratio observed / predicted as an
+//     EWMA (weight 1/2, each observation clamped to [1/4, 8]); decisions scale that side's
+//     estimate by it, and the factor of a side a call did not use relaxes 10 % toward 1;
 //   * when a call's time differs from its corrected prediction by more than 25 %, the model is
-//     marked stale and re-measured (rates of every digest set and device again, factors reset)
-//     at the next routed call at least 0.5 s after the previous measurement;
+//     marked stale and re-measured (rates of every digest set and device again) at the next
+//     routed call once the back-off allows (0.5 s after the previous measurement at first);
+//     a side's factors are reset when its re-measured rates moved by more than 15 % from the
+//     ones the decisions used (the load changed: the factor described the old one), and kept
+//     when they did not (a bias the probes cannot see -- e.g. the CPU route on DRAM-resident
+//     parts against the probes' cache-resident buffers), the back-off then doubling (to 60 s)
+//     so a steady bias does not re-measure on every call;
 //   * every s3h_route_refresh_calls routed calls (default 64) it is re-measured anyway, so a
 //     route that looked slow when measured -- and was therefore never taken again, leaving
 //     nothing to observe -- is re-priced within a bounded number of calls.
@@ -44,7 +49,9 @@ using namespace s3h::host;
 namespace {
 
 constexpr double kDiverge = 0.25;         // |observed / predicted - 1| that marks the model stale
-constexpr double kRemeasureMinS = 0.5;    // at most one divergence-triggered measurement per 0.5 s
+constexpr double kRemeasureMinS = 0.5;    // divergence-triggered re-measurement back-off: first
+constexpr double kRemeasureMaxS = 60.0;   // ... and longest (doubling while the rates hold)
+constexpr double kMoved = 0.15;           // re-measured rates this far from the used ones: reset
 constexpr double kRelax = 0.9;            // an unused side's factor: f <- 1 + (f - 1) x 0.9
 constexpr int kRefreshCallsDefault = 64;  // re-measure after this many routed calls
 
@@ -63,9 +70,15 @@ struct RouteState {
   double staged = 0, call_s = 0;
   int cpu_threads = 0;
   std::vector<DevRates> dev;
-  double f_gpu = 1, f_cpu = 1;
+  double f_gpu[3] = {1, 1, 1}, f_cpu[3] = {1, 1, 1};  // observed / predicted, per digest set
   double scale[4] = {1, 1, 1, 1};  // s3h_route_scale: chain, h2d, cpu, staged
   double t_measured = -1e9;
+  double backoff = kRemeasureMinS;
+  // the effective rates (scale applied) decisions used before the last invalidation, and
+  // whether a re-measurement moved them (per side): compared in ensure()
+  bool have_prev = false;
+  double prev_cpu1[3] = {0, 0, 0}, prev_chain[3] = {0, 0, 0}, prev_h2d = 0;
+  bool moved_gpu = false, moved_cpu = false;
   uint64_t measurements = 0, calls = 0, divergences = 0, calls_since = 0;
   bool stale = false;
   int refresh_calls = [] {
@@ -85,13 +98,24 @@ bool trace_route() {
 }
 
 void invalidate(RouteState& S) {
+  // remember what the decisions used (device 0's GPU rates, every digest set's CPU rate)
+  S.have_prev = true;
+  for (int a = 0; a < 3; ++a) {
+    S.prev_cpu1[a] = S.have_cpu[a] ? S.cpu1[a] * S.scale[2] : 0;
+    S.prev_chain[a] = !S.dev.empty() && S.dev[0].have_chain[a] ? S.dev[0].chain[a] * S.scale[0] : 0;
+  }
+  S.prev_h2d = !S.dev.empty() && S.dev[0].have_h2d ? S.dev[0].h2d * S.scale[1] : 0;
   for (bool& h : S.have_cpu) h = false;
   S.have_staged = S.have_call = false;
   for (DevRates& d : S.dev) d = DevRates{};
-  S.f_gpu = S.f_cpu = 1;
   for (double& x : S.scale) x = 1;
   S.stale = false;
   S.calls_since = 0;
+  S.moved_gpu = S.moved_cpu = false;
+}
+
+bool moved(double before, double now) {
+  return before > 0 && now > 0 && std::fabs(now / before - 1.0) > kMoved;
 }
 
 // One device's lone-chain rate of digest set `dig` and/or its pinned H2D rate.
@@ -184,9 +208,9 @@ int measure_device(int device, unsigned dig, bool chain, bool h2d, DevRates* out
 // (and everything again when the model is stale or due for its refresh); S.mu held.
 int ensure(RouteState& S, unsigned dig, int devs) {
   const double now = wall_s();
-  if ((S.stale && now - S.t_measured >= kRemeasureMinS) ||
-      (S.refresh_calls > 0 && S.calls_since >= uint64_t(S.refresh_calls)))
-    invalidate(S);
+  const bool remeasure = (S.stale && now - S.t_measured >= S.backoff) ||
+                         (S.refresh_calls > 0 && S.calls_since >= uint64_t(S.refresh_calls));
+  if (remeasure) invalidate(S);
   const int a = dig_index(dig);
   bool measured = false;
   if (!S.cpu_threads) S.cpu_threads = int(host_cpus());
@@ -194,6 +218,7 @@ int ensure(RouteState& S, unsigned dig, int devs) {
     S.cpu1[a] = one_thread_rate(dig);
     S.cpu_all[a] = team_rate(unsigned(S.cpu_threads), dig);
     S.have_cpu[a] = measured = true;
+    S.moved_cpu = S.moved_cpu || moved(S.prev_cpu1[a], S.cpu1[a]);
   }
   if (!S.have_staged) {
     S.staged = team_rate(unsigned(S.cpu_threads), 0);
@@ -213,6 +238,7 @@ int ensure(RouteState& S, unsigned dig, int devs) {
     if (D.have_chain[a] && D.have_h2d) continue;
     if (int rc = measure_device(d, dig, !D.have_chain[a], !D.have_h2d, &D)) return rc;
     measured = true;
+    if (d == 0) S.moved_gpu = S.moved_gpu || moved(S.prev_chain[a], D.chain[a]) || moved(S.prev_h2d, D.h2d);
   }
   if (!S.have_call) {
     // fixed cost of one host-path call: a one-block part, timed on its second call (the first
@@ -234,11 +260,17 @@ int ensure(RouteState& S, unsigned dig, int devs) {
     S.t_measured = now;
     ++S.measurements;
   }
+  if (remeasure && S.have_prev) {
+    // the rates moved: the factors described the old conditions; else keep them and back off
+    if (S.moved_gpu) for (double& f : S.f_gpu) f = 1;
+    if (S.moved_cpu) for (double& f : S.f_cpu) f = 1;
+    S.backoff = S.moved_gpu || S.moved_cpu ? kRemeasureMinS : std::min(kRemeasureMaxS, 2 * S.backoff);
+  }
   return S3H_OK;
 }
 
 // The decision inputs for devices [0, devs): the slowest device's chain and H2D rates.
-Rates snapshot(const RouteState& S, int devs) {
+Rates snapshot(const RouteState& S, int devs, unsigned dig) {
   Rates R;
   R.cpu_threads = std::max(1, S.cpu_threads);
   R.devices = std::max(1, int(S.dev.size()));
@@ -257,8 +289,8 @@ Rates snapshot(const RouteState& S, int devs) {
   R.h2d = h * S.scale[1];
   R.staged = S.staged * S.scale[3];
   R.call_s = S.call_s;
-  R.f_gpu = S.f_gpu;
-  R.f_cpu = S.f_cpu;
+  R.f_gpu = S.f_gpu[dig_index(dig)];
+  R.f_cpu = S.f_cpu[dig_index(dig)];
   return R;
 }
 
@@ -266,10 +298,11 @@ int devices_for(int ndevices, int count) {
   return ndevices > 0 ? std::min(ndevices, count) : count;
 }
 
-// One observation of a side (0 GPU, 1 CPU): raw prediction `raw` seconds, observed `t`.
-void observe_side(RouteState& S, int side, double raw, double t) {
+// One observation of a side (0 GPU, 1 CPU) for digest set index a: raw prediction `raw`
+// seconds, observed `t`.
+void observe_side(RouteState& S, int side, int a, double raw, double t) {
   if (!(raw > 0) || !(t > 0)) return;
-  double& f = side == 0 ? S.f_gpu : S.f_cpu;
+  double& f = side == 0 ? S.f_gpu[a] : S.f_cpu[a];
   const double ratio = std::min(8.0, std::max(0.25, t / raw));
   if (std::fabs(t / (raw * f) - 1.0) > kDiverge) {
     ++S.divergences;
@@ -278,20 +311,21 @@ void observe_side(RouteState& S, int side, double raw, double t) {
   f = 0.5 * f + 0.5 * ratio;
 }
 
-void observe(const Decision& D, double t, double t_gpu, double t_cpu) {
+void observe(const Decision& D, unsigned dig, double t, double t_gpu, double t_cpu) {
   RouteState& S = route_state();
   std::lock_guard<std::mutex> l(S.mu);
+  const int a = dig_index(dig);
   ++S.calls;
   ++S.calls_since;
   if (D.route == S3H_ROUTE_GPU) {
-    observe_side(S, 0, D.g, t);
-    S.f_cpu = 1 + (S.f_cpu - 1) * kRelax;
+    observe_side(S, 0, a, D.g, t);
+    S.f_cpu[a] = 1 + (S.f_cpu[a] - 1) * kRelax;
   } else if (D.route == S3H_ROUTE_CPU) {
-    observe_side(S, 1, D.c, t);
-    S.f_gpu = 1 + (S.f_gpu - 1) * kRelax;
+    observe_side(S, 1, a, D.c, t);
+    S.f_gpu[a] = 1 + (S.f_gpu[a] - 1) * kRelax;
   } else {
-    observe_side(S, 0, D.sp.g, t_gpu);
-    observe_side(S, 1, D.sp.c, t_cpu);
+    observe_side(S, 0, a, D.sp.g, t_gpu);
+    observe_side(S, 1, a, D.sp.c, t_cpu);
   }
 }
 
@@ -362,7 +396,7 @@ int routed(unsigned dig, const uint8_t* const* parts, const char* path, const ui
     {
       std::lock_guard<std::mutex> l(S.mu);
       if (int e = ensure(S, dig, devs)) return e;
-      R = snapshot(S, devs);
+      R = snapshot(S, devs, dig);
     }
     const int source = path ? S3H_SOURCE_FILE
                        : all_pinned(parts, lengths, nullptr, n) ? S3H_SOURCE_PINNED : S3H_SOURCE_PAGEABLE;
@@ -386,7 +420,7 @@ int routed(unsigned dig, const uint8_t* const* parts, const char* path, const ui
     } else {
       rc = cpu_run(dig, parts, path, offsets, lengths, n, sha, md5v);
     }
-    if (rc == S3H_OK) observe(D, wall_s() - t0, tg, tc);
+    if (rc == S3H_OK) observe(D, dig, wall_s() - t0, tg, tc);
     if (rc == S3H_OK && taken) *taken = D.route;
     return rc;
   }
@@ -415,7 +449,7 @@ int s3h_route_model(s3h_route_model_t* m) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
     const int rc = ensure(S, S3H_DIGESTS_SHA256, std::max(1, count));
-    const Rates R = snapshot(S, std::max(1, count));
+    const Rates R = snapshot(S, std::max(1, count), S3H_DIGESTS_SHA256);
     *m = s3h_route_model_t{};
     m->cpu_bytes_per_s = R.cpu1[0];
     m->cpu_all_bytes_per_s = R.cpu_all[0];
@@ -440,7 +474,7 @@ int s3h_route_rates(s3h_route_rates_t* r) {
     if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
     int rc = S3H_OK;
     for (unsigned dig = 1; dig <= 3 && rc == S3H_OK; ++dig) rc = ensure(S, dig, std::max(1, count));
-    const Rates R = snapshot(S, std::max(1, count));
+    const Rates R = snapshot(S, std::max(1, count), S3H_DIGESTS_SHA256);
     s3h_route_rates_t full{};
     full.size = uint32_t(std::min<size_t>(r->size, sizeof full));
     full.version = S3H_API_VERSION;
@@ -454,8 +488,10 @@ int s3h_route_rates(s3h_route_rates_t* r) {
     full.h2d_bytes_per_s = R.h2d;
     full.staged_bytes_per_s = R.staged;
     full.call_s = R.call_s;
-    full.gpu_factor = S.f_gpu;
-    full.cpu_factor = S.f_cpu;
+    for (int a = 0; a < 3; ++a) {
+      full.gpu_factor[a] = S.f_gpu[a];
+      full.cpu_factor[a] = S.f_cpu[a];
+    }
     full.measurements = S.measurements;
     full.routed_calls = S.calls;
     full.divergences = S.divergences;

@@ -514,8 +514,9 @@ int s3h_route_choose(const s3h_route_rates_t* rates, int digests, const uint64_t
   R.h2d = r.h2d_bytes_per_s;
   R.staged = r.staged_bytes_per_s;
   R.call_s = r.call_s;
-  R.f_gpu = r.gpu_factor > 0 ? r.gpu_factor : 1;
-  R.f_cpu = r.cpu_factor > 0 ? r.cpu_factor : 1;
+  const int a = dig_index(unsigned(digests));
+  R.f_gpu = r.gpu_factor[a] > 0 ? r.gpu_factor[a] : 1;
+  R.f_cpu = r.cpu_factor[a] > 0 ? r.cpu_factor[a] : 1;
   const std::string bad = rates_check(R, unsigned(digests));
   if (!bad.empty()) return fail(S3H_EINVAL, "route choose: %s", bad.c_str());
   try {

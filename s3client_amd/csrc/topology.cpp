@@ -2,6 +2,7 @@
 // entry points that need no GPU: s3h_host_threads, s3h_host_plan, s3h_pci_numa, s3h_mem_node.
 #include "topology.hpp"
 
+#include <dirent.h>
 #include <pthread.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -139,6 +140,26 @@ int mem_node(const void* p) {
   int node = -1;
   if (!p || syscall(SYS_get_mempolicy, &node, nullptr, 0, p, kMpolFNode | kMpolFAddr) != 0) return -1;
   return node;
+}
+
+double pci_power_cap_w(const char* bdf) {
+  if (!bdf || !*bdf) return 0;
+  std::string b(bdf);
+  for (char& c : b) c = char(std::tolower(static_cast<unsigned char>(c)));
+  const std::string dir = sysfs_root() + "/bus/pci/devices/" + b + "/hwmon";
+  DIR* d = opendir(dir.c_str());
+  if (!d) return 0;
+  double w = 0;
+  while (dirent* e = readdir(d)) {
+    if (std::strncmp(e->d_name, "hwmon", 5) != 0) continue;
+    std::string v;
+    if (read_line(dir + "/" + e->d_name + "/power1_cap", &v) && std::atof(v.c_str()) > 0) {
+      w = std::atof(v.c_str()) * 1e-6;
+      break;
+    }
+  }
+  closedir(d);
+  return w;
 }
 
 std::atomic<int> g_numa_mode{[] {

@@ -56,6 +56,9 @@ int pci_numa(const char* bdf, int* node, std::string* cpulist);
 bool node_cpulist(int node, std::string* cpulist);
 // Node of the page holding p (get_mempolicy MPOL_F_NODE | MPOL_F_ADDR); -1 if unknown.
 int mem_node(const void* p);
+// Board power cap of the GPU at PCI address `bdf` in watts (<root>/bus/pci/devices/<bdf>/
+// hwmon/hwmon*/power1_cap, microwatts); 0 when the platform does not say.
+double pci_power_cap_w(const char* bdf);
 
 // Placement policy: kNumaLocal (each device's node; default), kNumaOff (no binding), or a
 // forced node (measurements: the remote side of an A/B).  Env S3H_HOST_NUMA = local|off|<node>.

@@ -760,12 +760,21 @@ def dual_layout(lengths, cus: int = 256) -> tuple[int, bool]:
 
 
 def kernel_policy(policy: str) -> str:
-    """AUTO's kernel policy for plans created afterwards -- "throughput" (default) or
-    "efficiency" (skewp instead of the shared-SIMD skews kernel for 4,097 - 32 x CUs parts:
-    8.6 % slower, 32 % fewer joules per GiB) -- returns the previous one (s3h_kernel_policy)."""
+    """AUTO's kernel policy for plans created afterwards -- "throughput" (skews for 4,097 -
+    32 x CUs parts), "efficiency" (skewp there: ~5 % slower, ~36 % fewer joules per GiB) or
+    "power" (the default: skews only when the board's power cap lets it hold its clock) --
+    returns the previous one (s3h_kernel_policy)."""
     prev = ctypes.c_int(0)
     check(lib().s3h_kernel_policy(_native.POLICY_IDS[policy], ctypes.byref(prev)))
     return _native.POLICY_NAMES[prev.value]
+
+
+def device_power_cap(device: int = 0) -> float:
+    """Board power cap of ``device`` in watts as the "power" kernel policy reads it (sysfs hwmon
+    power1_cap; 0.0 when the platform does not say): s3h_device_power_cap."""
+    w = ctypes.c_double(0)
+    check(lib().s3h_device_power_cap(device, ctypes.byref(w)))
+    return w.value
 
 
 def trim() -> None:

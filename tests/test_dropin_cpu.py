@@ -279,7 +279,7 @@ def _rates(**kw):
     r = {"cpu_threads": 16, "devices": 1, "cpu_bytes_per_s": [2.5e9, 0.8e9, 0.6e9],
          "cpu_all_bytes_per_s": [37e9, 12e9, 9e9], "chain_bytes_per_s": [69e6, 120e6, 69e6],
          "h2d_bytes_per_s": 56e9, "staged_bytes_per_s": 60e9, "call_s": 3e-4,
-         "gpu_factor": 1.0, "cpu_factor": 1.0}
+         "gpu_factor": [1.0, 1.0, 1.0], "cpu_factor": [1.0, 1.0, 1.0]}
     r.update(kw)
     return r
 
@@ -312,11 +312,13 @@ def test_route_choose_applies_observed_factors():
     lens = [P] * 128
     base = s3.route_choose(lens, _rates(), "sha256")
     assert base["route"] == "cpu"
-    slow_cpu = s3.route_choose(lens, _rates(cpu_factor=3.0), "sha256")
+    slow_cpu = s3.route_choose(lens, _rates(cpu_factor=[3.0, 1.0, 1.0]), "sha256")
     assert abs(slow_cpu["cpu_s"] / base["cpu_s"] - 3.0) < 1e-9
     fast_gpu = s3.route_choose(lens, _rates(chain_bytes_per_s=[690e6, 1.2e9, 690e6]), "sha256")
     assert fast_gpu["route"] in ("gpu", "split")
-    back = s3.route_choose(lens, _rates(chain_bytes_per_s=[690e6, 1.2e9, 690e6], gpu_factor=10.0), "sha256")
+    back = s3.route_choose(lens, _rates(chain_bytes_per_s=[690e6, 1.2e9, 690e6], gpu_factor=[10.0, 1.0, 1.0]), "sha256")
+    # the factors are per digest set: SHA-256's do not price both digests
+    assert s3.route_choose(lens, _rates(cpu_factor=[1.0, 1.0, 5.0]), "sha256")["cpu_s"] == base["cpu_s"]
     assert back["route"] == "cpu"
     with pytest.raises(s3.S3HashError):
         s3.route_choose(lens, _rates(chain_bytes_per_s=[0, 0, 0]), "sha256")
@@ -337,7 +339,7 @@ def test_route_choose_reads_only_the_callers_struct_size():
     for f in ("cpu_bytes_per_s", "cpu_all_bytes_per_s", "chain_bytes_per_s"):
         for i, x in enumerate(R[f]):
             getattr(r, f)[i] = x
-    r.gpu_factor = 100.0  # beyond the caller's size: must be ignored
+    r.gpu_factor[0] = 100.0  # beyond the caller's size: must be ignored
     r.size = _native.RouteRates.gpu_factor.offset
     lens = (ctypes.c_uint64 * 4)(*([8 << 20] * 4))
     c = _native.RouteChoice()

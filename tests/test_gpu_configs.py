@@ -12,6 +12,8 @@ import pytest
 
 import s3client_amd as s3
 
+from .kernel_choice import shared_range_kernel
+
 pytestmark = pytest.mark.gpu
 SEED = 20241008
 MIB = 1 << 20
@@ -151,7 +153,8 @@ def test_c4_rank0_shard(torch_cuda, oracle, golden):
     try:
         s3.generate_parts(data, offs, lens, ids, SEED)
         with s3.Plan(offs, lens) as plan:  # AUTO: shared-SIMD producers, one workgroup per CU
-            assert plan.info()["kernel"] == "skews" and plan.info()["grid"] == per // 32
+            assert plan.info()["kernel"] == shared_range_kernel()
+            assert plan.info()["grid"] == per // 32
             out = torch.empty((per, 8), dtype=torch.int32, device="cuda")
             plan.launch(data, out)
             torch.cuda.synchronize()
@@ -201,7 +204,7 @@ def test_other_rank_shards(torch_cuda, oracle, golden, cfg, world, rank):
     try:
         s3.generate_parts(data, offs, lens, ids, SEED)
         with s3.Plan(offs, lens) as plan:
-            assert plan.info()["kernel"] == ("skews" if cfg == "c4" else "skew")
+            assert plan.info()["kernel"] == (shared_range_kernel() if cfg == "c4" else "skew")
             out = torch.empty((per, 8), dtype=torch.int32, device="cuda")
             plan.launch(data, out)
             plan.status()  # device error word clear

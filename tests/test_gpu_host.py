@@ -379,8 +379,17 @@ def test_sharded_host_batch_on_repeated_device(torch_cuda, oracle):
 def test_host_batch_shared_simd_kernel_range(torch_cuda, oracle):
     """4,097-8,192 parts (AUTO = the shared-SIMD skew kernel, one 32-part workgroup per CU)
     from pinned memory at a constant stride (2-D copies, 256 KiB slices) and from pageable
-    parts (staged slices): every slice is a resumable launch of that kernel."""
+    parts (staged slices): every slice is a resumable launch of that kernel (the "throughput"
+    policy: the default "power" policy may pick skewp on a power-capped board)."""
     torch = torch_cuda
+    prev = s3.kernel_policy("throughput")
+    try:
+        _host_shared_simd_range(torch, oracle)
+    finally:
+        s3.kernel_policy(prev)
+
+
+def _host_shared_simd_range(torch, oracle):
     assert s3.Plan([0] * 4500, [1] * 4500).info()["kernel"] == "skews"
     rng = np.random.default_rng(53)
     n, stride = 4500, 600_000  # 3 slices per part
@@ -773,8 +782,9 @@ lens = rng.integers(1, 60000, n)
 bufs = [s3.PinnedBuffer(int(L) + 4096) for L in lens]
 order = sorted(range(n), key=lambda i: bufs[i].ptr)
 apart = [bufs[i].array[:int(lens[i])] for i in order]
-one = torch.empty(int(lens.sum()) + 64 * n, dtype=torch.uint8, pin_memory=True)
-offs = np.concatenate([[0], np.cumsum(lens + 64)[:-1]])
+pad = (lens + 63) // 64 * 64  # packed at 64-B boundaries: the range spans the group's bytes
+one = torch.empty(int(pad.sum()) + 64, dtype=torch.uint8, pin_memory=True)
+offs = np.concatenate([[0], np.cumsum(pad)[:-1]])
 s3.sha256_batch_host(apart)
 s3.sha256_batch_host(s3.BufferParts(one, offs, lens))
 print("ok")

@@ -9,6 +9,8 @@ import pytest
 
 import s3client_amd as s3
 
+from .kernel_choice import shared_range_kernel
+
 pytestmark = pytest.mark.gpu
 SEED = 20241008
 KERNELS = ["skew", "skewp", "skews", "quad", "pair", "pc", "lane"]
@@ -93,8 +95,8 @@ def test_kernels_agree_on_many_small_parts(torch_cuda, oracle):
     assert s3.Plan([0] * 40000, [1] * 40000).info()["kernel"] == "pc"
     assert s3.Plan([0] * 1024, [1] * 1024).info()["kernel"] == "skew"
     assert s3.Plan([0] * 10000, [1] * 10000).info()["kernel"] == "skewp"
-    assert s3.Plan([0] * 8192, [1] * 8192).info()["kernel"] == "skews"
-    assert s3.Plan([0] * 4097, [1] * 4097).info()["kernel"] == "skews"
+    assert s3.Plan([0] * 8192, [1] * 8192).info()["kernel"] == shared_range_kernel()
+    assert s3.Plan([0] * 4097, [1] * 4097).info()["kernel"] == shared_range_kernel()
     assert s3.Plan([0] * 30000, [1] * 30000).info()["kernel"] == "pair"
     rng = np.random.default_rng(7)
     n = 70000
@@ -491,7 +493,8 @@ def test_dual_digest_group_kernel_device_and_host(torch_cuda, oracle):
     rl[:4] = [0, 55, 56, 64]
     ro = np.cumsum(rng.integers(0, 40, n) + np.concatenate([[0], rl[:-1]]))
     host = rng.integers(0, 256, int(ro[-1] + rl[-1]) + 8, dtype=np.uint8)
-    assert s3.Plan(ro, rl).info()["kernel"] == "skews"  # SHA-256 alone; both digests: group kernel
+    # SHA-256 alone: the shared-range kernel; both digests: the group kernel
+    assert s3.Plan(ro, rl).info()["kernel"] == shared_range_kernel()
     sha, m5 = s3.sha256_md5_batch_device(_dev_buffer(torch_cuda, host), ro, rl)
     assert np.array_equal(sha.cpu().numpy().view(np.uint32), oracle.batch(host, ro, rl))
     assert np.array_equal(m5.cpu().numpy().view(np.uint32), oracle.md5_batch(host, ro, rl))
@@ -533,7 +536,7 @@ AUTO_EDGES = [(1, "skew"), (2048, "skew"), (2049, "skew"), (4096, "skew"), (4097
 
 
 def test_auto_kernel_edges(torch_cuda, oracle):
-    """Every AUTO switch point of capi.hip resolve_kernel, one part below and above: the plan
+    """Every AUTO switch point of plan.cpp resolve_kernel, one part below and above: the plan
     picks the documented kernel and every digest of ragged small parts (0-300 B,
     all byte alignments) matches the oracle; SHA-256 + MD5 from the dual path at the dual
     kernel's switch points (split grid / skew group / skewp group / two streams) vs the oracle
@@ -544,7 +547,8 @@ def test_auto_kernel_edges(torch_cuda, oracle):
     for n, kernel in AUTO_EDGES:
         lens = rng.integers(0, 300, n)
         offs = rng.integers(0, 1 << 20, n)
-        assert s3.Plan(offs, lens).info()["kernel"] == kernel, n
+        want = shared_range_kernel() if kernel == "skews" else kernel  # default "power" policy
+        assert s3.Plan(offs, lens).info()["kernel"] == want, n
         got = s3.sha256_batch_device(data, offs, lens).cpu().numpy().view(np.uint32)
         assert np.array_equal(got, oracle.batch(host, offs, lens, threads=16)), n
     for n in (1820, 1821, 2048, 2049, 4096, 4097, 8192, 8193):
