@@ -45,7 +45,9 @@ inline uint32_t load_be32(const uint8_t *p) {
   return __builtin_bswap32(v);
 }
 
-void compress_scalar(uint32_t st[8], const uint8_t *p, uint64_t nblk) {
+void compress_scalar(uint32_t st_out[8], const uint8_t *p, uint64_t nblk) {
+  uint32_t st[8];  // local across blocks: st_out shares cache lines with other parts' digests
+  std::memcpy(st, st_out, sizeof st);
   for (; nblk; --nblk, p += 64) {
     uint32_t w[16];
     for (int i = 0; i < 16; ++i) w[i] = load_be32(p + 4 * i);
@@ -69,6 +71,7 @@ void compress_scalar(uint32_t st[8], const uint8_t *p, uint64_t nblk) {
     }
     for (int i = 0; i < 8; ++i) st[i] += v[i];
   }
+  std::memcpy(st_out, st, sizeof st);
 }
 
 __attribute__((target("sha,sse4.1,ssse3")))

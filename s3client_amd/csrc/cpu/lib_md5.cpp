@@ -68,14 +68,20 @@ inline void all_groups(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, const
   (group<G>(a, b, c, d, m), ...);
 }
 
+// The chaining state stays in locals for the whole run: `st` usually points into the caller's
+// digest array, where neighbouring parts' states share a cache line, and a store per block
+// (the compiler must assume `p` may alias `st`) made threads hashing adjacent parts fight over
+// that line -- the CPU route ran at half its single-thread rate x threads.
 void compress(uint32_t st[4], const uint8_t *p, uint64_t nblk) {
+  uint32_t s0 = st[0], s1 = st[1], s2 = st[2], s3 = st[3];
   for (; nblk; --nblk, p += 64) {
     uint32_t m[16];
     std::memcpy(m, p, 64);  // little-endian words on x86
-    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+    uint32_t a = s0, b = s1, c = s2, d = s3;
     all_groups(a, b, c, d, m, std::make_integer_sequence<int, 16>());
-    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+    s0 += a; s1 += b; s2 += c; s3 += d;
   }
+  st[0] = s0; st[1] = s1; st[2] = s2; st[3] = s3;
 }
 
 void finish(uint32_t st[4], const uint8_t *data, uint64_t len, uint64_t total) {
