@@ -130,8 +130,10 @@ def split_ref_tg(lengths, m, tg, ndevices=0, source="pinned"):
 
 
 def split_ref(lengths, m, ndevices=0, source="pinned"):
-    """The whole plan: tg = 0 for pinned parts, else the best of T x {1, 4, 6, 8, 9} / 12; many
-    small pinned parts (the group pipeline packs them) are planned as staged."""
+    """The whole plan: tg = 0 for pinned parts, else the best of each device's share T / N of
+    the host threads x {1, 4, 6, 8, 9} / 12 that leave the CPU side a thread (topology.cpp
+    split_stage_candidates); many small pinned parts (the group pipeline packs them) are
+    planned as staged."""
     if source == "pinned" and len(lengths) > 64 and (
             max(lengths) <= MIB or (len(lengths) > 256 and max(lengths) != min(lengths))):
         source = "pageable"
@@ -139,8 +141,10 @@ def split_ref(lengths, m, ndevices=0, source="pinned"):
         s_, k = split_ref_tg(lengths, m, 0, ndevices, source)
         return s_, k, 0
     T = m["cpu_threads"]
+    cap = max(1, min(ndevices, m["devices"]) if ndevices > 0 else m["devices"])
     best = None
-    for t in dict.fromkeys(max(1, T * num // 12) for num in (1, 4, 6, 8, 9)):
+    cands = dict.fromkeys(max(1, max(1, T // cap) * num // 12) for num in (1, 4, 6, 8, 9))
+    for t in (t for t in cands if t * cap < T):
         r = split_ref_tg(lengths, m, t, ndevices, source)
         if r and (best is None or r[0] < best[0]):
             best = (r[0], r[1], t)
