@@ -159,6 +159,17 @@ def lib() -> ctypes.CDLL:
             if not os.path.exists(LIB_PATH):
                 raise S3HashError(S3H_EINVAL, f"{LIB_PATH} missing: run `make` (or "
                                   "__graft_entry__.build()) -- there is no fallback path")
+            # One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64 and
+            # libhsa-runtime64 (SONAME libamdhip64.so.7, like /opt/rocm's), but torch's own
+            # libraries NEED the unversioned names: loaded AFTER this library, torch maps a
+            # second HIP + ROCr instance and this library's runtime loses the device ("no HIP
+            # device visible" on its first GPU call after torch.cuda.init(); tools/
+            # cpu_route_context_probe.py on the box).  With torch loaded first this library's
+            # NEEDED libamdhip64.so.7 resolves to torch's runtime by SONAME.
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
             L = ctypes.CDLL(LIB_PATH)
             L.s3h_last_error.restype = ctypes.c_char_p
             L.s3h_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]

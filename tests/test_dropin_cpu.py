@@ -351,3 +351,17 @@ def test_route_choose_reads_only_the_callers_struct_size():
     r.size = 8  # too small to hold the rates
     assert _native.lib().s3h_route_choose(ctypes.byref(r), 1, lens, 4, 0, 0, ctypes.byref(c)) == -1
     assert s3._native.lib().s3h_api_version() == 2
+
+
+def test_one_hip_runtime_per_process():
+    """Loading the library first must not leave two HIP runtimes in the process (torch's own
+    libamdhip64 + /opt/rocm's): _native.lib() loads torch before libs3hash.so, so the
+    library's libamdhip64.so.7 binds to torch's by SONAME (the box lost the device when the
+    library's runtime came first)."""
+    code = ("import s3client_amd as s3; s3._native.lib(); import torch\n"
+            "maps = {l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}\n"
+            "print(len(maps))")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "1"

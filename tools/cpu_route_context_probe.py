@@ -3,7 +3,7 @@
 tools/cpu_dual_probe (same cpu_batch, same 8 MiB parts) on the GPU box.
 
 Times s3h_sha256_md5_batch_routed(route="cpu") over 64 x 8 MiB parts in successive process
-states -- bare (no torch, no HIP), torch + HIP initialised, after GPU-route calls, from a
+states -- before any HIP initialisation, torch + HIP initialised, after GPU-route calls, from a
 pinned buffer -- and beside each the process's CPU time (user+sys over wall = the parallelism
 the threads actually got) and the cgroup's throttling counters (cpu.stat nr_throttled /
 throttled_usec).  One JSON object on stdout.
@@ -89,7 +89,7 @@ def main():
               f"(par {d['runs'][-1]['parallelism']}), sha256 {gib / s['best_wall_s']:.2f} GiB/s",
               file=sys.stderr, flush=True)
 
-    phase("bare")
+    phase("before_hip_init")
     import torch
     torch.cuda.init()
     dev_buf = torch.empty(64 * MIB, dtype=torch.uint8, device="cuda")
