@@ -63,8 +63,8 @@ enum s3h_algo {
  * kernel is ~5 % faster than SKEWP but draws 1.26-1.34 kW against 0.77 kW (2.57 vs 1.65 J/GiB):
  * S3H_POLICY_THROUGHPUT -- SKEWS; S3H_POLICY_EFFICIENCY -- SKEWP (the lower energy-delay
  * product); S3H_POLICY_POWER (default since API 2) -- SKEWS only when the device's board power
- * cap (sysfs hwmon power1_cap, s3h_device_power_cap) lets it hold its full clock (>= 1,450 W:
- * consumers and producers together need more than MI355X's 1,400 W cap), SKEWP
+ * cap (sysfs hwmon power1_cap, s3h_device_power_cap) lets it hold its full clock (>= 1,500 W:
+ * consumers and producers together need ~1.52 kW, more than MI355X's 1,400 W cap), SKEWP
  * otherwise.  Initial value from the environment: S3H_KERNEL_POLICY=throughput|efficiency|power
  * (S3H_PREFER_EFFICIENCY=1 = efficiency). */
 enum s3h_policy { S3H_POLICY_THROUGHPUT = 0, S3H_POLICY_EFFICIENCY = 1, S3H_POLICY_POWER = 2 };
@@ -150,6 +150,9 @@ int s3h_device_pci_bus_id(int device, char *out, int len);
 int s3h_pci_numa(const char *pci_bus_id, int *node, char *cpulist, int len, int *usable_cpus);
 /* The same for HIP device `device` (needs the device: its PCI address). */
 int s3h_device_numa_node(int device, int *node, char *cpulist, int len);
+/* Board power cap of the PCI function in watts (sysfs hwmon<k>/power1_cap; 0 when the platform
+ * does not report one): what S3H_POLICY_POWER reads for a device.  No GPU needed. */
+int s3h_pci_power_cap(const char *pci_bus_id, double *watts);
 /* Placement policy of the host path: S3H_NUMA_LOCAL (default: each device's own node),
  * S3H_NUMA_OFF (no binding: the runtime's placement, unbound threads) or a node >= 0 (every
  * device's staging and threads on that node -- for local/remote measurements).  Initial value

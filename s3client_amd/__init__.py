@@ -15,7 +15,7 @@ from .hashing import (Plan, device_count, digests_to_text, generate_parts, hash_
                       kernel_policy, dual_layout, md5_batch_routed, sha256_md5_batch_routed,
                       sha256_md5_file_parts_routed, md5_file_parts, route_rates, route_choose,
                       route_device_rates, route_refresh_calls, route_scale, host_plan,
-                      device_power_cap)
+                      device_power_cap, pci_power_cap)
 from .upload import upload_parts_geometry, UploadPart
 from ._native import S3HashError, LIB_PATH
 
@@ -30,5 +30,5 @@ __all__ = ["BufferParts", "Plan", "device_count", "digests_to_text", "generate_p
            "mem_node", "PinnedBuffer", "kernel_policy", "dual_layout", "md5_batch_routed",
            "sha256_md5_batch_routed", "sha256_md5_file_parts_routed", "md5_file_parts",
            "route_rates", "route_choose", "route_device_rates", "route_refresh_calls",
-           "route_scale", "host_plan", "device_power_cap",
+           "route_scale", "host_plan", "device_power_cap", "pci_power_cap",
            "upload_parts_geometry", "UploadPart", "S3HashError", "LIB_PATH"]

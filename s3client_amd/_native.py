@@ -47,7 +47,7 @@ C_ABI_SYMBOLS = (
     "s3h_route_rates", "s3h_route_choose", "s3h_route_device_rates", "s3h_route_refresh_calls",
     "s3h_route_scale", "s3h_md5_batch_routed", "s3h_sha256_md5_batch_routed",
     "s3h_sha256_md5_file_parts_routed", "s3h_md5_file_parts", "s3h_host_plan",
-    "s3h_host_alloc_ex", "s3h_device_power_cap",
+    "s3h_host_alloc_ex", "s3h_device_power_cap", "s3h_pci_power_cap",
 )
 POLICY_IDS = {"throughput": 0, "efficiency": 1, "power": 2}
 POLICY_NAMES = {v: k for k, v in POLICY_IDS.items()}
@@ -185,6 +185,7 @@ def lib() -> ctypes.CDLL:
             L.s3h_host_free.argtypes = [ctypes.c_void_p]
             L.s3h_kernel_policy.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
             L.s3h_device_power_cap.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+            L.s3h_pci_power_cap.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]
             L.s3h_stream_stats.argtypes = [ctypes.c_void_p, u64p, u64p]
             L.s3h_plan_dual_layout.argtypes = [ctypes.c_void_p, u32p, ctypes.POINTER(ctypes.c_int)]
             L.s3h_dual_layout.argtypes = [u64p, ctypes.c_uint64, ctypes.c_int, u32p,

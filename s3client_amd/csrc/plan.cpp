@@ -104,15 +104,18 @@ uint32_t plan_solo(const s3h::Slot* slots, uint64_t n, uint64_t cus) {
 //   S3H_POLICY_EFFICIENCY  skewp, always (env S3H_PREFER_EFFICIENCY=1);
 //   S3H_POLICY_POWER       (default) skews only where the board may draw what skews needs to
 //                          hold its full clock, else skewp.  Round 6's attribution
-//                          (profiles/r06_power_attribution.json, one lease): the consumers
-//                          alone on stale W+K draw 1.10 kW at 2.38 GHz, the producers alone
-//                          0.98 kW, together 1.34 kW against the 1.4 kW cap at 2.28 GHz -- the
-//                          consumers' round stream owns most of the power, and skews at full
-//                          clock would need ~1.45 kW.  So under a cap below kSkewsFullClockW
-//                          (MI355X: 1,400 W) skews only runs ~5 % faster than skewp for ~1.6x
-//                          its energy, and POWER picks skewp.
+//                          (profiles/r06_power_attribution.json, one lease, two rounds): idle
+//                          board 245 W; the consumers alone on stale W+K 1,098 W at 2.38 GHz
+//                          (+853 W); the producers alone 977 W at 2.32 GHz running 1.66x the
+//                          product's block rate (+732 W, ~441 W at the product's rate); the
+//                          product 1,344 W at 2.28 GHz against the 1.4 kW cap.  The consumers'
+//                          round stream owns two thirds of the dynamic power, and skews at
+//                          2.35 GHz would need ~245 + 1,294 x 2.35 / 2.38 = ~1.52 kW.  Under
+//                          a cap below kSkewsFullClockW skews runs ~5 % faster than skewp for
+//                          ~1.5x its energy (the higher energy-delay product), so POWER picks
+//                          skewp; a board allowed 1.5 kW or more keeps skews.
 // Outside 4,097 - 32 x CUs parts every policy chooses the same kernel.
-constexpr double kSkewsFullClockW = 1450.0;
+constexpr double kSkewsFullClockW = 1500.0;
 std::atomic<int> g_kernel_policy{[] {
   const char* e = std::getenv("S3H_PREFER_EFFICIENCY");
   if (e && std::atoi(e) == 1) return int(S3H_POLICY_EFFICIENCY);

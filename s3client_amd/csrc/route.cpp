@@ -15,8 +15,8 @@
 //     routed call once the back-off allows (0.5 s after the previous measurement at first);
 //     a side's factors are reset when its re-measured rates moved by more than 15 % from the
 //     ones the decisions used (the load changed: the factor described the old one), and kept
-//     when they did not (a bias the probes cannot see -- e.g. the CPU route on DRAM-resident
-//     parts against the probes' cache-resident buffers), the back-off then doubling (to 60 s)
+//     when they did not (a bias the probes cannot see -- e.g. a co-tenant holding some of the
+//     host CPUs only while batches run), the back-off then doubling (to 60 s)
 //     so a steady bias does not re-measure on every call;
 //   * every s3h_route_refresh_calls routed calls (default 64) it is re-measured anyway, so a
 //     route that looked slow when measured -- and was therefore never taken again, leaving

@@ -278,6 +278,12 @@ int s3h_host_plan(const char* const* pci_bus_ids, int ndevices, const char* affi
   return S3H_OK;
 }
 
+int s3h_pci_power_cap(const char* pci_bus_id, double* watts) {
+  if (!pci_bus_id || !watts) return fail(S3H_EINVAL, "pci power cap: null argument");
+  *watts = pci_power_cap_w(pci_bus_id);
+  return S3H_OK;
+}
+
 int s3h_pci_numa(const char* pci_bus_id, int* node, char* cpulist, int len, int* usable_cpus) {
   if (!node) return fail(S3H_EINVAL, "pci numa: null node");
   *node = -1;

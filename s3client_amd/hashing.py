@@ -777,6 +777,14 @@ def device_power_cap(device: int = 0) -> float:
     return w.value
 
 
+def pci_power_cap(pci_bus_id: str) -> float:
+    """Board power cap in watts of the PCI function (sysfs hwmon power1_cap; 0.0 when absent;
+    no GPU needed): s3h_pci_power_cap."""
+    w = ctypes.c_double(0)
+    check(lib().s3h_pci_power_cap(pci_bus_id.encode(), ctypes.byref(w)))
+    return w.value
+
+
 def trim() -> None:
     """Free the host path's cached per-device buffers (HBM ring, pinned staging, plans):
     s3h_trim.  A process that shares the GPU with other work calls this when it is done."""

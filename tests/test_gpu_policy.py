@@ -1,7 +1,7 @@
 """AUTO's kernel policy: "efficiency" runs skewp where
 "throughput" runs the shared-SIMD skews kernel (4,097 - 32 x CUs parts), "power" (the default)
 runs skews there only when the board's power cap (sysfs hwmon power1_cap) is at least the
-1,450 W skews needs to hold its clock; same digests; elsewhere every policy agrees."""
+1,500 W skews needs to hold its clock; same digests; elsewhere every policy agrees."""
 import os
 import subprocess
 import sys
@@ -41,7 +41,7 @@ def test_efficiency_policy_picks_skewp_same_digests(torch_cuda, oracle):
     rng = np.random.default_rng(61)
     cap = s3.device_power_cap(0)
     print("board power cap", cap, "W")
-    k_pow = "skewp" if 0 < cap < 1450 else "skews"
+    k_pow = "skewp" if 0 < cap < 1500 else "skews"
     cases = {8192: ("skews", "skewp", k_pow), 1024: ("skew", "skew", "skew"),
              30000: ("pair", "pair", "pair")}
     for n, (k_thr, k_eff, k_pw) in cases.items():

@@ -126,3 +126,17 @@ def test_plan_matches_this_process():
         per, cpus = s3.host_threads(n)
         assert p["cpus"] == cpus and p["staging_threads_per_device"] == per
         assert p["affinity_cpus"] == len(os.sched_getaffinity(0))
+
+
+def test_pci_power_cap_from_sysfs(tmp_path, monkeypatch):
+    """The POWER kernel policy's input (plan.cpp resolve_kernel): hwmon power1_cap in microwatts
+    under the device's PCI function, 0 when the platform has none."""
+    root = fake_node(tmp_path)
+    hw = tmp_path / "sys" / "bus" / "pci" / "devices" / BDFS[5] / "hwmon" / "hwmon7"
+    hw.mkdir(parents=True)
+    (hw / "power1_cap").write_text("1400000000\n")
+    monkeypatch.setenv("S3H_SYSFS_ROOT", root)
+    assert s3.pci_power_cap(BDFS[5]) == 1400.0
+    assert s3.pci_power_cap(BDFS[5].upper()) == 1400.0
+    assert s3.pci_power_cap(BDFS[0]) == 0.0          # no hwmon directory
+    assert s3.pci_power_cap("0000:ff:00.0") == 0.0   # no such function
