@@ -420,7 +420,13 @@ int routed(unsigned dig, const uint8_t* const* parts, const char* path, const ui
     } else {
       rc = cpu_run(dig, parts, path, offsets, lengths, n, sha, md5v);
     }
-    if (rc == S3H_OK) observe(D, dig, wall_s() - t0, tg, tc);
+    const double t = wall_s() - t0;
+    if (rc == S3H_OK) observe(D, dig, t, tg, tc);
+    if (rc == S3H_OK && trace_route())
+      std::fprintf(stderr, "[s3h route]   observed %.4f s (gpu side %.4f s vs %.4f raw, cpu side %.4f s vs "
+                   "%.4f raw)\n", t, D.route == S3H_ROUTE_SPLIT ? tg : D.route == S3H_ROUTE_GPU ? t : 0.0,
+                   D.route == S3H_ROUTE_SPLIT ? D.sp.g : D.g, D.route == S3H_ROUTE_SPLIT ? tc : D.route == S3H_ROUTE_CPU ? t : 0.0,
+                   D.route == S3H_ROUTE_SPLIT ? D.sp.c : D.c);
     if (rc == S3H_OK && taken) *taken = D.route;
     return rc;
   }

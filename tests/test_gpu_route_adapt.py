@@ -101,8 +101,9 @@ def test_both_digests_ragged_c3_like(torch_cuda, oracle, tmp_path):
 
 def test_auto_prices_both_digests(torch_cuda, oracle):
     """AUTO's pick for both digests is s3h_route_choose's under the live rates for the dual
-    digest set -- and for a batch the CPU wins on SHA-256 alone, the dual pick is no longer the
-    CPU (a CPU MD5 is several times slower per thread than SHA-NI SHA-256)."""
+    digest set -- and, priced on the measured rates alone (corrections left by earlier calls
+    reset to 1), for a batch the CPU wins on SHA-256 alone the dual pick is no longer the CPU
+    (CPU MD5 + SHA-256 is ~3.5x slower per thread than SHA-NI SHA-256 alone)."""
     torch = torch_cuda
     host, offs, lens = _gen(torch, 256, 8 * MIB)
     buf = torch.empty(host.size, dtype=torch.uint8, pin_memory=True)
@@ -111,17 +112,20 @@ def test_auto_prices_both_digests(torch_cuda, oracle):
     want_s = oracle.batch(host, offs, lens, threads=16)
     want_m = oracle.md5_batch(host, offs, lens, threads=16)
     R = s3.route_rates()
-    c_sha = s3.route_choose(lens, R, "sha256")
     c_both = s3.route_choose(lens, R, "both")
-    print("rates", R, "\nchoices sha256", c_sha, "both", c_both)
-    assert c_both["cpu_s"] > 2.0 * c_sha["cpu_s"]  # MD5 + SHA-256 per CPU thread
+    R0 = dict(R, gpu_factor=[1.0] * 3, cpu_factor=[1.0] * 3)
+    c_sha0 = s3.route_choose(lens, R0, "sha256")
+    c_both0 = s3.route_choose(lens, R0, "both")
+    print("rates", R, "\nlive choice both", c_both, "\nmeasured-rate choices sha256", c_sha0,
+          "both", c_both0)
+    assert c_both0["cpu_s"] > 2.0 * c_sha0["cpu_s"]  # MD5 + SHA-256 per CPU thread
     sha, m5, taken = s3.sha256_md5_batch_routed(parts, route="auto")
     assert taken == c_both["route"]
     assert np.array_equal(sha, want_s) and np.array_equal(m5, want_m)
     got, taken_sha = s3.sha256_batch_routed(parts, route="auto")
     assert np.array_equal(got, want_s)
-    if c_sha["route"] == "cpu":
-        assert c_both["route"] != "cpu"
+    if c_sha0["route"] == "cpu":
+        assert c_both0["route"] != "cpu"
 
 
 def test_device_rates_and_state():
