@@ -31,9 +31,13 @@ KERNEL_OBJ := $(OBJDIR)/launch.o
 # error-word check are read from the gfx950 code object the linked library ships
 # (tools/isa_counts.py -> s3client_amd/kernel_isa_counts.json; disassembly in build/isa).
 ISA_DIS := build/isa/libs3hash_gfx950.dis
-$(KERNEL_OBJ): $(CSRC)/launch.hip
+# (explicit prerequisites: the -MMD file is written from build/isa, so its relative paths do not
+# resolve from the repo root)
+KERNEL_SRCS := $(CSRC)/launch.hip $(CSRC)/sha256_kernels.hip $(wildcard $(CSRC)/*.inc) \
+               $(CSRC)/sha256_device.hpp $(CSRC)/kernel_abi.hpp $(CSRC)/exp_config.hpp $(CSRC)/internal.hpp
+$(KERNEL_OBJ): $(KERNEL_SRCS)
 	@mkdir -p $(OBJDIR) build/isa
-	cd build/isa && $(HIPCC) $(HIPFLAGS) -MF ../../$(@:.o=.d) -save-temps -c -o ../../$@ ../../$<
+	cd build/isa && $(HIPCC) $(HIPFLAGS) -MF ../../$(@:.o=.d) -save-temps -c -o ../../$@ ../../$(CSRC)/launch.hip
 
 $(OBJDIR)/%.o: $(CSRC)/%.cpp
 	@mkdir -p $(OBJDIR)

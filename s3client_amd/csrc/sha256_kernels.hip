@@ -1530,7 +1530,8 @@ __device__ __forceinline__ void md5_step_vmem(uint32_t& s0, uint32_t& s1, uint32
 }
 #endif
 
-// Decoded message words of MD5 block `blk` (zeros past the launch's range, padding at the end).
+// Decoded message words of MD5 block `blk` (zeros at or past `limit` -- the launch's range or
+// the lane's last block -- padding at the end).
 __device__ __forceinline__ void md5_decode(const RawBlock& r, uint32_t sel, const uint8_t* bp,
                                            uint64_t len, uint64_t bits, uint64_t blk,
                                            uint64_t limit, uint32_t w[16]) {
@@ -1648,7 +1649,8 @@ __device__ __forceinline__ void md5_self_body(const LaunchArgs& A, const uint32_
       if (J >= iters) goto md5_done;
       fetch_full(p + 64 * (J + kDepth), b0 + J + kDepth < fend, A.zero, ring[(u + kDepth) % kRing]);
       uint32_t w[16];
-      md5_decode(ring[u], sel, p + 64 * J, decode_len(valid, s.len), bits, b0 + J, A.blk_end, w);
+      md5_decode(ring[u], sel, p + 64 * J, decode_len(valid, s.len), bits, b0 + J,
+                 nb < A.blk_end ? nb : A.blk_end, w);  // past the lane's last block: zeros
       hash_words(w, J);
     }
   }
@@ -1713,6 +1715,12 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
     const uint64_t fend = fetch_end(s.len, A.blk_end);
     const uint64_t bits = valid ? msg_bits(A, slot, s.len) : 0;
     const uint64_t dl = decode_len(valid, s.len);
+    // Blocks past this lane's last one (its padding included) are never consumed (the consumer
+    // keeps only live chains' sums): decoded as zeros, like blocks past the launch's range.
+    // Without this a ragged group's lanes that had finished took md5_decode's tail branch --
+    // 64 predicated byte loads -- for every block after the shortest part's end, and the whole
+    // wave ran it (MD5 of 300 parts of U[1, 16] MiB: 1.85x the longest chain's time).
+    const uint64_t lim = nb < A.blk_end ? nb : A.blk_end;
     RawBlock ra[kBps], rb[kBps];
 #define S3H_MD5_FETCH(R, K)                                                                  \
     _Pragma("unroll") for (int h = 0; h < kBps; ++h)                                        \
@@ -1720,7 +1728,7 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
 #define S3H_MD5_MAKE_T(R, K, FULL)                                                           \
     _Pragma("unroll") for (int h = 0; h < kBps; ++h)                                        \
       md5_produce<FULL>(R[h], sel, p + 64 * ((K) * kBps + h), dl, bits, b0 + (K) * kBps + h, \
-                        A.blk_end, lds_km[(K) & 1][h], lane);
+                        lim, lds_km[(K) & 1][h], lane);
 #define S3H_MD5_MAKE(R, K) S3H_MD5_MAKE_T(R, K, false)
     // Steps below `full_steps` hold whole data blocks of every lane's part (slots are sorted
     // by length; the group's last valid slot is the shortest; lanes past n decode_len past
