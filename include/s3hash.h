@@ -341,7 +341,8 @@ int s3h_sha256_md5_batch_device(int device, const void *d_base, const uint64_t *
  * visible GPU (S3H_ENODEV otherwise): it chooses between paths with identical digests and is
  * never a fallback for a missing device.  *taken (if non-null) receives the route that ran.
  *   gpu_s = call_s + max(longest part / chain rate, bytes per device / feed rate)
- *           feed = h2d (pinned parts) or min(h2d, staged) (pageable parts, file ranges)
+ *           feed = h2d (pinned parts), min(h2d, staged memcpy) (pageable parts) or
+ *                  min(h2d, staged pread) (file ranges)
  *   cpu_s = (longest-first schedule of the parts on k = min(n, threads) threads) / (rate(k) / k)
  *           rate(k) = min(k x one-thread rate, all-threads rate)
  * each for the digest set the call computes (SHA-256, MD5, or both), times the observed /
@@ -410,6 +411,8 @@ typedef struct {
   uint64_t routed_calls;          /* AUTO / SPLIT calls observed */
   uint64_t divergences;           /* calls that differed from their prediction by > 25 % */
   double age_s;                   /* seconds since the last measurement */
+  double staged_file_bytes_per_s; /* file ranges: cpu_threads threads' pread from the page cache
+                                   * (0: price them at staged_bytes_per_s) */
 } s3h_route_rates_t;
 int s3h_route_rates(s3h_route_rates_t *r);
 /* AUTO's decision for digest set `digests` under rates *r (pure host arithmetic; reads at most
@@ -444,8 +447,8 @@ int s3h_md5_batch_routed(const uint8_t *const *parts, const uint64_t *lengths, u
 /* Both upload headers on a route: the GPU side is s3h_sha256_md5_batch_host /
  * _file_parts (one grid, one PCIe pass), the CPU side hashes each part with SHA-256 and MD5 in
  * one pass over memory (64 KiB chunks while they sit in cache); the model prices both digests
- * (a CPU MD5 runs at ~0.8 GB/s per thread: the dual CPU route is ~4x slower per thread than
- * SHA-256 alone, so the GPU wins at far fewer parts). */
+ * (a CPU MD5 runs at ~1.0 GB/s per thread, both digests at ~0.7: the dual CPU route is ~3.5x
+ * slower per thread than SHA-256 alone, so the GPU wins at far fewer parts). */
 int s3h_sha256_md5_batch_routed(const uint8_t *const *parts, const uint64_t *lengths, uint64_t n,
                                 uint32_t *sha256_digests, uint32_t *md5_digests, int ndevices,
                                 int route, int *taken);

@@ -83,7 +83,7 @@ class RouteRates(ctypes.Structure):
                 ("call_s", ctypes.c_double), ("gpu_factor", ctypes.c_double * 3),
                 ("cpu_factor", ctypes.c_double * 3), ("measurements", ctypes.c_uint64),
                 ("routed_calls", ctypes.c_uint64), ("divergences", ctypes.c_uint64),
-                ("age_s", ctypes.c_double)]
+                ("age_s", ctypes.c_double), ("staged_file_bytes_per_s", ctypes.c_double)]
 
 
 class RouteChoice(ctypes.Structure):

@@ -67,7 +67,7 @@ struct RouteState {
   bool have_cpu[3] = {false, false, false};
   double cpu1[3] = {0, 0, 0}, cpu_all[3] = {0, 0, 0};
   bool have_staged = false, have_call = false;
-  double staged = 0, call_s = 0;
+  double staged = 0, staged_file = 0, call_s = 0;
   int cpu_threads = 0;
   std::vector<DevRates> dev;
   double f_gpu[3] = {1, 1, 1}, f_cpu[3] = {1, 1, 1};  // observed / predicted, per digest set
@@ -222,6 +222,7 @@ int ensure(RouteState& S, unsigned dig, int devs) {
   }
   if (!S.have_staged) {
     S.staged = team_rate(unsigned(S.cpu_threads), 0);
+    S.staged_file = pread_team_rate(unsigned(S.cpu_threads));
     S.have_staged = measured = true;
   }
   int count = 0;
@@ -288,6 +289,7 @@ Rates snapshot(const RouteState& S, int devs, unsigned dig) {
     if (S.dev[size_t(d)].have_h2d) h = h > 0 ? std::min(h, S.dev[size_t(d)].h2d) : S.dev[size_t(d)].h2d;
   R.h2d = h * S.scale[1];
   R.staged = S.staged * S.scale[3];
+  R.staged_file = S.staged_file * S.scale[3];
   R.call_s = S.call_s;
   R.f_gpu = S.f_gpu[dig_index(dig)];
   R.f_cpu = S.f_cpu[dig_index(dig)];
@@ -502,6 +504,7 @@ int s3h_route_rates(s3h_route_rates_t* r) {
     full.routed_calls = S.calls;
     full.divergences = S.divergences;
     full.age_s = wall_s() - S.t_measured;
+    full.staged_file_bytes_per_s = R.staged_file;
     std::memcpy(r, &full, full.size);
     return rc;
   });

@@ -5,6 +5,7 @@
 
 #include <fcntl.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -143,8 +144,9 @@ Split split_choose(const Rates& R, unsigned dig, const uint64_t* sorted, uint64_
 
 }  // namespace
 
-void route_times(const Rates& R, unsigned dig, const uint64_t* lengths, uint64_t n, int ndevices,
+void route_times(const Rates& R0, unsigned dig, const uint64_t* lengths, uint64_t n, int ndevices,
                  int source, double* gpu_s, double* cpu_s) {
+  const Rates R = for_source(R0, source);
   const int a = dig_index(dig);
   uint64_t total = 0, longest = 0;
   for (uint64_t i = 0; i < n; ++i) {
@@ -185,8 +187,9 @@ std::vector<uint64_t> longest_first(const uint64_t* lengths, uint64_t n) {
 // try each device's share of the host threads times 1, 4, 6, 8, 9 twelfths as staging threads
 // per GPU shard (topology.cpp split_stage_candidates; S3H_SPLIT_STAGE_THREADS fixes it, for
 // measurements) and keep the fastest estimate.
-Split split_plan(const Rates& R, unsigned dig, const uint64_t* lengths, uint64_t n, int ndevices,
+Split split_plan(const Rates& R0, unsigned dig, const uint64_t* lengths, uint64_t n, int ndevices,
                  int source, const std::vector<uint64_t>& order) {
+  const Rates R = for_source(R0, source);
   std::vector<double> ws[4];
   std::vector<uint64_t> sorted(n);  // the lengths in `order`
   for (uint64_t k = 0; k < n; ++k) sorted[k] = lengths[order[k]];
@@ -354,6 +357,45 @@ double team_rate(unsigned threads, unsigned dig) {
   return double(threads) * kBuf * kReps / best;
 }
 
+double pread_team_rate(unsigned threads) {
+  constexpr uint64_t kBuf = 2ull << 20;
+  constexpr int kReps = 3;
+  threads = std::max(1u, threads);
+  FdGuard fd{int(syscall(SYS_memfd_create, "s3h_pread_probe", 0u))};
+  if (fd.fd < 0) return 0;
+  std::vector<uint8_t> fill(kBuf, 0x5a);
+  for (unsigned t = 0; t < threads; ++t)
+    if (pwrite(fd.fd, fill.data(), kBuf, off_t(uint64_t(t) * kBuf)) != ssize_t(kBuf)) return 0;
+  std::vector<std::vector<uint8_t>> dst(threads, std::vector<uint8_t>(kBuf, 0));
+  std::atomic<bool> bad{false};
+  double best = 1e30;
+  for (int round = 0; round < 2; ++round) {
+    std::atomic<unsigned> ready{0};
+    std::atomic<bool> go{false};
+    auto work = [&](unsigned t) {
+      ready.fetch_add(1);
+      while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+      for (int r = 0; r < kReps; ++r)
+        if (pread(fd.fd, dst[t].data(), kBuf, off_t(uint64_t(t) * kBuf)) != ssize_t(kBuf)) bad = true;
+    };
+    std::vector<std::thread> pool;
+    for (unsigned t = 1; t < threads; ++t) pool.emplace_back(work, t);
+    while (ready.load() + 1 < threads) std::this_thread::yield();
+    const auto t0 = std::chrono::steady_clock::now();
+    go.store(true, std::memory_order_release);
+    work(0);
+    for (auto& th : pool) th.join();
+    best = std::min(best, seconds_since(t0));
+  }
+  return bad ? 0.0 : double(threads) * kBuf * kReps / best;
+}
+
+Rates for_source(const Rates& R, int source) {
+  Rates r = R;
+  if (source == S3H_SOURCE_FILE && R.staged_file > 0) r.staged = R.staged_file;
+  return r;
+}
+
 void FdGuard::close_now() {
   if (fd >= 0) ::close(fd);
   fd = -1;
@@ -513,6 +555,7 @@ int s3h_route_choose(const s3h_route_rates_t* rates, int digests, const uint64_t
   }
   R.h2d = r.h2d_bytes_per_s;
   R.staged = r.staged_bytes_per_s;
+  R.staged_file = r.staged_file_bytes_per_s;  // 0 when the caller's struct predates it
   R.call_s = r.call_s;
   const int a = dig_index(unsigned(digests));
   R.f_gpu = r.gpu_factor[a] > 0 ? r.gpu_factor[a] : 1;

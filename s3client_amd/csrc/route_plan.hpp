@@ -6,7 +6,8 @@
 // are per-job batches of a few parts (lib/src/upload.cpp:89-110, 136-140), exactly the shape
 // where it loses.  A routed call (route.cpp) prices each route from measured rates:
 //   gpu_s = call_s + max(longest part / chain rate, bytes per device / feed rate)
-//           feed = pinned H2D rate, or min(H2D, staging memcpy rate) for pageable parts / files
+//           feed = pinned H2D rate, or min(H2D, staging rate) for pageable parts (the threads'
+//           memcpy) and file ranges (their pread from the page cache)
 //   cpu_s = longest-first makespan of the parts on k = min(n, threads) threads
 //           / (rate(k) / k),  rate(k) = min(k x one-thread rate, all-threads rate)
 //   split_s(m) = max(gpu_s(the n - m shorter parts), cpu_s(the m longest))
@@ -41,6 +42,7 @@ struct Rates {
   double chain[3] = {0, 0, 0};    // one GPU chain (the slowest device in use)
   double h2d = 0;                 // pinned host -> device, the slowest device in use
   double staged = 0;              // pageable sources: the threads' memcpy into pinned staging
+  double staged_file = 0;         // file ranges: the threads' pread from the page cache (0: staged)
   double call_s = 0;              // fixed cost of one host-path GPU call
   double f_gpu = 1, f_cpu = 1;    // observed / predicted wall time of earlier routed calls
 };
@@ -90,6 +92,12 @@ int cpu_batch(unsigned dig, const uint8_t* const* parts, int fd, const uint64_t*
 // 2 MiB buffer, 3 passes, best of 2) of digest set `dig`; dig == 0: memcpy (staging fill).
 double one_thread_rate(unsigned dig);
 double team_rate(unsigned threads, unsigned dig);
+// `threads` threads' aggregate pread rate from the page cache (each its own 2 MiB of a memfd,
+// read in 2 MiB calls, 3 passes, best of 2): how fast the host path stages file ranges, ~0.6x
+// the memcpy rate on the GPU box (profiles/r06_route_gpu_side_probe.json).  0 if unavailable.
+double pread_team_rate(unsigned threads);
+// The rates a decision over `source` uses: file ranges stage at the pread rate.
+Rates for_source(const Rates& R, int source);
 // Opens `path` and checks that every range lies inside it (CPU route); the descriptor in *fd.
 int open_ranges(const char* path, const uint64_t* offsets, const uint64_t* lengths, uint64_t n, int* fd);
 

@@ -326,6 +326,28 @@ def test_route_choose_applies_observed_factors():
         s3.route_choose(lens, _rates(), "sha1")
 
 
+def test_route_choose_prices_file_staging_at_the_pread_rate():
+    """File ranges stage through pread from the page cache, slower than the memcpy that stages
+    pageable parts (GPU box: C2 from a file on 5 staging threads 0.28 s against 0.16 s on 16,
+    profiles/r06_route_gpu_side_probe.json): with staged_file_bytes_per_s set the model feeds
+    the GPU side of a file batch at min(H2D, that rate); with it 0 (a caller's older struct)
+    file ranges are priced like pageable parts."""
+    P = 8 << 20
+    lens = [P] * 1024
+    R = _rates(staged_bytes_per_s=60e9, staged_file_bytes_per_s=20e9)
+    page = s3.route_choose(lens, R, "sha256", source="pageable")
+    file = s3.route_choose(lens, R, "sha256", source="file")
+    assert abs(page["gpu_s"] - (3e-4 + 1024 * P / 56e9)) < 1e-9
+    assert abs(file["gpu_s"] - (3e-4 + 1024 * P / 20e9)) < 1e-9
+    old = s3.route_choose(lens, _rates(staged_bytes_per_s=60e9), "sha256", source="file")
+    assert abs(old["gpu_s"] - page["gpu_s"]) < 1e-12
+    # the split's GPU side too: fewer bytes fit its feed, so more parts go to the CPU
+    sp_page = s3.route_choose(lens, R, "sha256", source="pageable")
+    sp_file = s3.route_choose(lens, R, "sha256", source="file")
+    if sp_page["route"] == "split" and sp_file["route"] == "split":
+        assert sp_file["cpu_parts"] >= sp_page["cpu_parts"]
+
+
 def test_route_choose_reads_only_the_callers_struct_size():
     """A caller compiled against a shorter s3h_route_rates_t (no factors, no counters) passes a
     smaller `size`: the library reads that many bytes and treats the rest as absent (advisor

@@ -36,7 +36,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--ns", default="8,32,64,128,256,512,1024")
-    ap.add_argument("--sources", default="pinned,pageable")
+    ap.add_argument("--sources", default="pinned,pageable", help="of pinned,pageable,file")
     ap.add_argument("--dual", action="store_true", help="both digests (SHA-256 + MD5)")
     a = ap.parse_args()
     import torch
@@ -63,6 +63,15 @@ def main():
         pg = np.empty(N * L, dtype=np.uint8)
         torch.from_numpy(pg).copy_(data)
         bufs["pageable"] = (None, pg)
+    if "file" in a.sources:  # file ranges (page cache): one file of the N parts
+        import tempfile
+        tmpd = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
+        fpath = os.path.join(tmpd, "route_sweep.bin")
+        fa = np.empty(N * L, dtype=np.uint8)
+        torch.from_numpy(fa).copy_(data)
+        fa.tofile(fpath)
+        del fa
+        bufs["file"] = (fpath, None)
     del data
     torch.cuda.empty_cache()
     t0 = time.perf_counter()
@@ -73,22 +82,27 @@ def main():
            "part_bytes": L, "reps": a.reps, "cpu_backend": s3.cpu_backend(),
            "host_threads": s3.host_threads(1), "rows": [], "mismatches": 0}
     worst = 0.0
-    for src, (_, arr) in bufs.items():
+    for src, (handle, arr) in bufs.items():
         for n in ns:
-            parts = s3.BufferParts(arr, offs[:n], lens[:n])
+            parts = s3.BufferParts(arr, offs[:n], lens[:n]) if arr is not None else None
             if a.dual:
                 ch = s3.route_choose(lens[:n], s3.route_rates(), "both", source=src)
                 est_route, g_est, c_est = ch["route"], ch["gpu_s"], ch["cpu_s"]
                 k_est, tg_est, s_est = ch["cpu_parts"], ch["stage_threads"], ch["split_s"]
             else:
-                est_route, g_est, c_est = s3.route_estimate(lens[:n], model, pinned=src == "pinned")
-                k_est, tg_est, s_est = s3.route_split_estimate(lens[:n], model, source=src)
+                ch = s3.route_choose(lens[:n], s3.route_rates(), "sha256", source=src)
+                est_route, g_est, c_est = ch["route"], ch["gpu_s"], ch["cpu_s"]
+                k_est, tg_est, s_est = ch["cpu_parts"], ch["stage_threads"], ch["split_s"]
             times = {r: [] for r in ("gpu", "cpu", "split", "auto")}
             taken = None
             for k in range(a.reps + 1):
                 for r in times:
                     t1 = time.perf_counter()
-                    if a.dual:
+                    if src == "file" and a.dual:
+                        ds, dm, tk = s3.sha256_md5_file_parts_routed(handle, offs[:n], lens[:n], ndevices=1, route=r)
+                    elif src == "file":
+                        d, tk = s3.sha256_file_parts_routed(handle, offs[:n], lens[:n], ndevices=1, route=r)
+                    elif a.dual:
                         ds, dm, tk = s3.sha256_md5_batch_routed(parts, ndevices=1, route=r)
                     else:
                         d, tk = s3.sha256_batch_routed(parts, ndevices=1, route=r)
@@ -116,6 +130,8 @@ def main():
             print(f"[route_sweep] {src} n={n}: gpu {med['gpu']:.4f} cpu {med['cpu']:.4f} split {med['split']:.4f} "
                   f"auto {med['auto']:.4f} ({taken}) model gpu {g_est:.4f} cpu {c_est:.4f} split {s_est:.4f} ({k_est})",
                   file=sys.stderr, flush=True)
+    if "file" in bufs:
+        os.remove(bufs["file"][0])
     out["worst_auto_over_best"] = round(worst, 4)
     out["rates_after"] = s3.route_rates()
     print(json.dumps(out))
