@@ -78,7 +78,7 @@ static_assert(S3H_EXP_STALL_PRODUCER == 0, "product build: producers publish eve
     defined(S3H_EXP_GROUP_ONLY) || defined(S3H_EXP_NONTEMPORAL_FETCH) ||                    \
     defined(S3H_EXP_GROUP_ANY) || defined(S3H_EXP_NO_TAIL_RAMP) ||                        \
     defined(S3H_EXP_PAGEABLE_DIRECT) || defined(S3H_EXP_PRODUCER_IDLE) ||                   \
-    defined(S3H_EXP_CONSUMER_IDLE)
+    defined(S3H_EXP_CONSUMER_IDLE) || defined(S3H_EXP_MD5_UNPACED)
 #error "an experiment switch is defined in a product build (define S3H_EXPERIMENT_BUILD: make exp)"
 #endif
 #endif  // S3H_EXPERIMENT_BUILD

@@ -1584,8 +1584,20 @@ __device__ __forceinline__ void md5_produce(const RawBlock& r, uint32_t sel, con
 // i.e. well under a SHA-256 skew/skewp chain's 544-609, so it keeps pace with the SHA-256
 // group it shares a workgroup with (sha256_md5_group_kernel).  Loads run kDepth blocks ahead
 // (an MD5 block is ~0.6 us of chain time; HBM latency under a full-chip load is several).
-template <uint32_t kChains>
-__device__ __forceinline__ void md5_self_body(const LaunchArgs& A, const uint32_t group) {
+//
+// Paced (kPaceBps > 0, `pace` = the workgroup's SHA-256 producer step counter flags[0]): the
+// SHA-256 group beside this wave reads the same parts, kPaceBps blocks per producer step, and
+// issues a step's loads before it publishes the step.  Unpaced, the MD5 chain (~1.8x faster)
+// ran ahead and both chains read every byte from HBM (C3 dual: 2.0017x the algorithmic bytes,
+// profiles/r04_c3_dual_mixed_counters.json).  Paced, block B is fetched only once the producer
+// has published step B / kPaceBps, i.e. after its own load of B was issued, microseconds
+// earlier on the same CU: the MD5 read hits L2.  Pacing is a cache policy, not a dependency --
+// the MD5 digests never read the producer's output -- so a wait that runs past kPaceSpinLimit
+// polls (~1.7 ms; a producer step is ~10 us) just stops pacing for the rest of the launch.
+constexpr uint32_t kPaceSpinLimit = 1u << 16;
+template <uint32_t kChains, uint32_t kPaceBps = 0>
+__device__ __forceinline__ void md5_self_body(const LaunchArgs& A, const uint32_t group,
+                                              const uint32_t* pace = nullptr) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t slot0 = group * kChains;
   if (slot0 >= A.n) return;
@@ -1620,8 +1632,31 @@ __device__ __forceinline__ void md5_self_body(const LaunchArgs& A, const uint32_
   const uint64_t full_end = (A.slots[last].len >> 6) < A.blk_end ? (A.slots[last].len >> 6) : A.blk_end;
   const uint64_t nfast = full_end > b0 ? (full_end - b0) / kRing * kRing : 0;  // whole rings
   RawBlock ring[kRing];
+  // Paced: the producer step count last read (wave-uniform) and whether pacing is still on.
+  uint32_t seen = 0;
+  bool pacing = kPaceBps != 0;
+  auto pace_to = [&](uint64_t B) {  // before fetching block b0 + B
+    if constexpr (kPaceBps != 0) {
+      if (!pacing || B >= iters) return;  // past the range: the zero page, nothing to share
+      const uint32_t need = B < 2 * kPaceBps ? 1u : uint32_t(B / kPaceBps);
+      uint32_t spin = 0;
+      while (seen < need) {
+        seen = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(pace, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (seen >= need) break;
+        if (++spin >= kPaceSpinLimit) {
+          pacing = false;
+          return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+  };
 #pragma unroll
-  for (uint32_t k = 0; k < kDepth; ++k) fetch_full(p + 64 * k, b0 + k < fend, A.zero, ring[k]);
+  for (uint32_t k = 0; k < kDepth; ++k) {
+    pace_to(k);
+    fetch_full(p + 64 * k, b0 + k < fend, A.zero, ring[k]);
+  }
   auto hash_words = [&](const uint32_t w[16], uint64_t J) {
     uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
     md5_steps_w<0>(a, b, c, d, w);
@@ -1635,6 +1670,7 @@ __device__ __forceinline__ void md5_self_body(const LaunchArgs& A, const uint32_
 #pragma unroll
     for (uint32_t u = 0; u < kRing; ++u) {
       const uint64_t J = j + u;
+      pace_to(J + kDepth);
       fetch_full(p + 64 * (J + kDepth), b0 + J + kDepth < fend, A.zero, ring[(u + kDepth) % kRing]);
       uint32_t w[16];
 #pragma unroll
@@ -1647,6 +1683,7 @@ __device__ __forceinline__ void md5_self_body(const LaunchArgs& A, const uint32_
     for (uint32_t u = 0; u < kRing; ++u) {
       const uint64_t J = j + u;
       if (J >= iters) goto md5_done;
+      pace_to(J + kDepth);
       fetch_full(p + 64 * (J + kDepth), b0 + J + kDepth < fend, A.zero, ring[(u + kDepth) % kRing]);
       uint32_t w[16];
       md5_decode(ring[u], sel, p + 64 * J, decode_len(valid, s.len), bits, b0 + J,
@@ -1953,6 +1990,13 @@ __global__ __launch_bounds__(128) void sha256_md5_dual_kernel(LaunchArgs S, Laun
 // beside the SHA-256 chain, so a grid of <= 256 workgroups (skewp: <= 8,192 parts, BASELINE
 // C4's per-GPU shard) gets both digests in about the SHA-256 time.  The MD5 plan must hold
 // the same parts in the same order (plans of the same geometry do: stable sort).
+// The self-fed MD5 wave of a group is paced by its SHA-256 producer (md5_self_body): it
+// fetches each block after the producer has, so the part is read from HBM once.
+#ifdef S3H_EXP_MD5_UNPACED  // experiment: round 3-5's unpaced MD5 wave (every byte read twice)
+template <bool PAIR> constexpr uint32_t kMd5PaceBps = 0;
+#else
+template <bool PAIR> constexpr uint32_t kMd5PaceBps = SkewGeom<1, PAIR>::kBps;
+#endif
 template <bool PAIR>
 __global__ __launch_bounds__(192) void sha256_md5_group_kernel(LaunchArgs S, LaunchArgs M) {
   __shared__ SkewLds<1, PAIR> LS;
@@ -1964,7 +2008,7 @@ __global__ __launch_bounds__(192) void sha256_md5_group_kernel(LaunchArgs S, Lau
   if ((S3H_EXP_GROUP_ONLY == 1 && wave == 1) || (S3H_EXP_GROUP_ONLY == 2 && wave != 1)) return;
 #endif
   if (wave == 1)
-    md5_self_body<SkewGeom<1, PAIR>::kParts>(M, blockIdx.x);
+    md5_self_body<SkewGeom<1, PAIR>::kParts, kMd5PaceBps<PAIR>>(M, blockIdx.x, &flags[0]);
   else
     skew_body<1, PAIR, true>(S, blockIdx.x, wave >> 1, LS, flags);
 }
@@ -1998,7 +2042,7 @@ __global__ __launch_bounds__(192) void sha256_md5_group_mixed_kernel(LaunchArgs 
     if (wave != 1)
       skew_body<1, false, true>(S, blockIdx.x, wave >> 1, L.skew, flags);
     else if (!lead_md5)
-      md5_self_body<kSolo>(M, blockIdx.x);
+      md5_self_body<kSolo, kMd5PaceBps<false>>(M, blockIdx.x, &flags[0]);
     return;
   }
   if (lead_md5 && blockIdx.x >= F + G) {  // MD5 of slots 0 .. 8F-1, 64 chains per workgroup
@@ -2012,7 +2056,7 @@ __global__ __launch_bounds__(192) void sha256_md5_group_mixed_kernel(LaunchArgs 
   S.slots += shift; S.out_idx += shift; S.n -= shift;
   M.slots += shift; M.out_idx += shift; M.n -= shift;
   if (wave == 1)
-    md5_self_body<SkewGeom<1, true>::kParts>(M, blockIdx.x - F);
+    md5_self_body<SkewGeom<1, true>::kParts, kMd5PaceBps<true>>(M, blockIdx.x - F, &flags[0]);
   else
     skew_body<1, true, true>(S, blockIdx.x - F, wave >> 1, L.skewp, flags);
 }

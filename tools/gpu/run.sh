@@ -20,6 +20,8 @@
 #   py:SCRIPT[:ARGS]     python SCRIPT ARGS                                  (600 s)
 #   trace:SCRIPT         rocprofv3 --kernel-trace --memory-copy-trace of python3 SCRIPT (300 s)
 #   exe:PROGRAM ARGS     a built tool, e.g. tools/ubench_dep                  (300 s)
+#   make:ARGS            make ARGS on the box, e.g. an experiment build (tools/exp is
+#                        gpurun-ignored: experiment libraries are built where they run) (600 s)
 set -o pipefail
 TAG=${1:?usage: run.sh TAG STEP...}; shift
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
@@ -63,6 +65,9 @@ for step in "$@"; do
       nr=${rest%%:*}; args=""; [ "$rest" != "$nr" ] && args=${rest#*:}
       S3H_BENCH_SHARE_GPU=1 timeout -k 10 600 python bench.py --gpus $nr $args > $out.jsonl 2> $out.err; rc=$?
       [ $rc -eq 0 ] && python3 tools/gpu/summary.py $out.jsonl ;;
+    make)
+      eval "timeout -k 10 600 make -j16 $rest" > $out.log 2>&1; rc=$?
+      tail -1 $out.log ;;
     exe)  # exe:PROGRAM [ARGS] -- a built tool (e.g. tools/ubench_dep), output to .log
       timeout -k 10 300 $rest > $out.log 2>&1; rc=$?
       tail -12 $out.log ;;
