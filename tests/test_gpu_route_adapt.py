@@ -229,11 +229,23 @@ def test_route_recovers_when_the_route_not_taken_is_mispriced(torch_cuda, oracle
         buf.numpy()[:] = host
         parts = s3.BufferParts(buf, offs, lens)
         want = oracle.batch(host, offs, lens, threads=16)
-        s3.route_rates()  # start the period right after a measurement
+        m0 = s3.route_rates()["measurements"]  # start the period right after a measurement
         s3.route_scale(which, 1 / 3)
         routes = _run_until(parts, want, base, 8)
-        print(f"{n} x {L >> 20} MiB: {base} -> scaled {which} /3 -> routes {routes}")
+        st = s3.route_rates()
+        now = s3.route_choose([L] * n, st, "sha256")["route"]
+        print(f"{n} x {L >> 20} MiB: {base} -> scaled {which} /3 -> routes {routes}; "
+              f"re-priced model chooses {now}; state {st}")
         assert routes[0] == after, routes
-        assert routes[-1] == base and len(routes) <= 6, routes
+        # the periodic re-measurement (every 4 calls) happened and dropped the 1/3 scale
+        assert st["measurements"] > m0, st
+        key = {"chain": "chain_bytes_per_s", "h2d": "h2d_bytes_per_s"}[which]
+        v, v0 = st[key], R[key]
+        assert (v[0] if isinstance(v, list) else v) > 0.6 * (v0[0] if isinstance(v0, list) else v0), st
+        # ... and from then on AUTO follows the re-priced model: back to the GPU side, unless the
+        # re-measured rates and the observed CPU factor (a shared box's CPUs ran faster than
+        # first measured) now put the CPU ahead of it -- the model's own choice, not the scale
+        assert routes[-1] == now, (routes, now)
+        assert now != base or len(routes) <= 6, routes
     finally:
         s3.route_refresh_calls(prev)

@@ -13,6 +13,7 @@
 #   benchlib:LIB[:ARGS]  the same with S3H_LIBRARY=LIB (a `make exp` build)    (400 s)
 #   stats[:ARGS]         rocprofv3 --kernel-trace --stats of bench.py ARGS    (400 s)
 #   pmc[:CTRS[:ARGS]]    rocprofv3 --pmc CTRS (one pass, e.g. FETCH_SIZE) of bench.py ARGS (240 s)
+#   pmclib:LIB:CTRS[:ARGS] the same on an experiment build (S3H_LIBRARY=LIB)     (240 s)
 #   n2[:ARGS]            2-rank torch.distributed.run rehearsal of bench.py on the one GPU
 #                        (S3H_BENCH_SHARE_GPU=1, gloo collectives, as the driver's N>1 runs) (600 s)
 #   selfn:N[:ARGS]       `python bench.py --gpus N ARGS` with NO launcher (bench.py starts the N
@@ -56,6 +57,10 @@ for step in "$@"; do
     pmc)
       ctrs=${rest%%:*}; args=""; [ "$rest" != "$ctrs" ] && args=${rest#*:}
       timeout -s KILL 240 rocprofv3 --pmc $ctrs --kernel-trace -d ${out}_prof -o run --output-format csv -- python3 bench.py $args > $out.jsonl 2> $out.err; rc=$?
+      [ $rc -eq 0 ] && ls ${out}_prof ;;
+    pmclib)  # pmclib:LIB:CTRS:ARGS -- one --pmc pass of bench.py on an experiment build
+      lib=${rest%%:*}; r2=${rest#*:}; ctrs=${r2%%:*}; args=""; [ "$r2" != "$ctrs" ] && args=${r2#*:}
+      S3H_LIBRARY=$lib timeout -s KILL 240 rocprofv3 --pmc $ctrs --kernel-trace -d ${out}_prof -o run --output-format csv -- python3 bench.py $args > $out.jsonl 2> $out.err; rc=$?
       [ $rc -eq 0 ] && ls ${out}_prof ;;
     n2)
       S3H_BENCH_SHARE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
