@@ -53,6 +53,10 @@ struct s3h_plan_s {
   bool dual_apart = false;      // ... whose MD5 chains run on workgroups of their own
   uint64_t* d_clocks = nullptr; // clock probe buffer (caller-owned), see s3h_plan_set_clock_probe
   uint32_t* d_err = nullptr;    // device error word (s3h::kErr* bits), read by plan_check
+  // mixed dual grid, apart form: per skew group the producer's step count tagged with the
+  // launch epoch (pacing of the MD5 waves on other workgroups); allocated on first use
+  uint64_t* d_progress = nullptr;
+  uint32_t progress_epoch = 0;
 };
 
 namespace s3h::host {
@@ -109,8 +113,11 @@ int dual_launch(s3h_plan_s* S, s3h_plan_s* M, const void* d_base, uint32_t* d_sh
 // Each returns the launch's hipGetLastError (the caller cleared the thread's error before).
 hipError_t launch_plan_kernel(const s3h_plan_s* P, int cus, uint64_t range_blocks,
                               const s3h::LaunchArgs& A, hipStream_t s);
+// `progress` / `epoch`: the mixed grid's apart form (F step counts, tagged with this launch's
+// epoch; plan.cpp dual_launch); unused by the other forms.
 hipError_t launch_dual_kernel(DualMode mode, const s3h_plan_s* S, const s3h_plan_s* M,
-                              const s3h::LaunchArgs& A, const s3h::LaunchArgs& B, hipStream_t s);
+                              const s3h::LaunchArgs& A, const s3h::LaunchArgs& B, uint64_t* progress,
+                              uint32_t epoch, hipStream_t s);
 hipError_t launch_stream_init(uint32_t* state, uint64_t n, int md5, hipStream_t s);
 hipError_t launch_stream_splice(const uint8_t* base, const s3h::SpliceJob* jobs, uint8_t* carry,
                                 uint8_t* head, uint64_t n, hipStream_t s);

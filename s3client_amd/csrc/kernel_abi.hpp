@@ -55,6 +55,27 @@ struct LaunchArgs {
   uint32_t* err;
 };
 
+// Cross-workgroup MD5 pacing (experiment S3H_EXP_MD5_XCD_PACE, sha256_kernels.hip ShaPacer /
+// XcdChains): the MD5 workgroups of the split dual grid and the mixed grid's apart form take
+// the chains of the skew groups on their own XCD and follow those groups' producers through
+// step counts in global memory.  Measured: C2 dual traffic 2x -> 1.04-1.22x at -0.3 %, C3 dual
+// 1.25x -> 1.18x at -3 to -4 % (profiles/r06_dual_xcd_pace_ab.json); the product keeps the
+// in-workgroup (LDS) pacing only.
+constexpr bool kMd5XcdPace = S3H_EXP_MD5_XCD_PACE != 0;
+
+// sha256_md5_group_mixed_kernel, apart form: the MD5 workgroups of the F skew groups' chains,
+// 64 chains each -- by XCD class under kMd5XcdPace (workgroups b and b + 8 share an XCD:
+// ceil(F / 8) skew groups per class -> ceil(F / 64) workgroups per class, 8 classes).
+S3H_HOST_DEVICE uint32_t mixed_lead_wgs(uint64_t F) {
+  return kMd5XcdPace ? uint32_t(8 * ((F + 63) / 64)) : uint32_t((8 * F + 63) / 64);
+}
+
+// sha256_md5_dual_kernel (the split dual grid): MD5 workgroups after the `sha_groups` skew
+// workgroups -- one per 64 parts, or by XCD class (8 x ceil(sha_groups / 64)) under kMd5XcdPace.
+S3H_HOST_DEVICE uint32_t split_md5_wgs(uint64_t sha_groups, uint64_t n) {
+  return kMd5XcdPace ? uint32_t(8 * ((sha_groups + 63) / 64)) : uint32_t((n + 63) / 64);
+}
+
 // Workgroup shapes (sha256_kernels.hip).
 constexpr int kPcThreads = 128;          // producer/consumer: wave 0 consumer, wave 1 producer; 64 parts
 constexpr int kPairThreads = 128;        // lane-pair kernel: 32 parts per workgroup

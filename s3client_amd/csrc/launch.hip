@@ -55,21 +55,23 @@ hipError_t launch_plan_kernel(const s3h_plan_s* P, int cus, uint64_t range, cons
 }
 
 hipError_t launch_dual_kernel(DualMode mode, const s3h_plan_s* S, const s3h_plan_s* M,
-                              const s3h::LaunchArgs& A, const s3h::LaunchArgs& B, hipStream_t stream) {
+                              const s3h::LaunchArgs& A, const s3h::LaunchArgs& B, uint64_t* progress,
+                              uint32_t epoch, hipStream_t stream) {
   if (mode == kDualGroup) {
     hipLaunchKernelGGL(s3h::sha256_md5_group_kernel<true>, dim3(uint32_t((S->n + 31) / 32)),
                        dim3(192), 0, stream, A, B);
   } else if (mode == kDualGroupMixed) {  // the LDS pad keeps one workgroup per CU
     const uint32_t F = S->dual_solo, G = uint32_t((S->n - 8ull * F + 31) / 32);
-    const uint32_t lead = S->dual_apart ? (8 * F + 63) / 64 : 0;
+    const uint32_t lead = S->dual_apart ? s3h::mixed_lead_wgs(F) : 0;
     hipLaunchKernelGGL(s3h::sha256_md5_group_mixed_kernel, dim3(F + G + lead), dim3(192),
-                       kMixedLdsPad, stream, A, B, F, G, lead);
+                       kMixedLdsPad, stream, A, B, F, G, lead, progress, epoch);
   } else if (mode == kDualGroupSkew) {
     hipLaunchKernelGGL(s3h::sha256_md5_group_kernel<false>, dim3(uint32_t((S->n + 7) / 8)),
                        dim3(192), 0, stream, A, B);
   } else {
-    hipLaunchKernelGGL(s3h::sha256_md5_dual_kernel<false>, dim3(S->grid + M->grid), dim3(128), 0,
-                       stream, A, B, uint32_t(S->grid));
+    hipLaunchKernelGGL(s3h::sha256_md5_dual_kernel<false>,
+                       dim3(S->grid + s3h::split_md5_wgs(S->grid, S->n)), dim3(128), 0, stream, A, B,
+                       uint32_t(S->grid), progress, epoch);
   }
   return hipGetLastError();
 }

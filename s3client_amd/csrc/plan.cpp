@@ -240,7 +240,7 @@ uint32_t dual_mixed_solo(const s3h::Slot* slots, uint64_t n, uint64_t cus, bool*
     // every part would need a skew group at the apart form's ratio: round 3's ratio may
     // still leave some to the skewp groups (advisor r4)
     if (F * kSkew >= n) continue;
-    const uint64_t wgs = F + (n - F * kSkew + kSkewp - 1) / kSkewp + (a ? (8 * F + 63) / 64 : 0);
+    const uint64_t wgs = F + (n - F * kSkew + kSkewp - 1) / kSkewp + (a ? s3h::mixed_lead_wgs(F) : 0);
     if (wgs <= cus) {
       *apart = a != 0;
       return uint32_t(F);
@@ -416,10 +416,11 @@ DualMode dual_mode(const s3h_plan_s* S, const s3h_plan_s* M, uint64_t b0, uint64
   if (S->kernel == S3H_KERNEL_SKEW && S->quad_waves == 1 && S->grid <= cus) return kDualGroupSkew;
 #endif
 #ifndef S3H_EXP_NO_SPLIT  // tools/ experiment builds only: never the split grid
-  if (S->kernel == S3H_KERNEL_SKEW && S->quad_waves == 1 && S->grid + M->grid <= cus)
+  if (S->kernel == S3H_KERNEL_SKEW && S->quad_waves == 1 &&
+      S->grid + s3h::split_md5_wgs(S->grid, S->n) <= cus)
     return kDualSplit;
 #endif
-  // skew plans whose split grid does not fit (1,821-2,048 parts on 256 CUs): each skew group
+  // skew plans whose split grid does not fit (1,817-2,048 parts on 256 CUs): each skew group
   // with a self-fed MD5 wave over the same 8 parts, one workgroup per CU -- both digests in
   // ~125 ms for 8 MiB parts vs 140 on the skewp group kernel (profiles/r02_exp_dual_group_skew.jsonl)
   if (S->kernel == S3H_KERNEL_SKEW && S->quad_waves == 1 && S->grid <= cus) return kDualGroupSkew;
@@ -454,8 +455,26 @@ int dual_launch(s3h_plan_s* S, s3h_plan_s* M, const void* d_base, uint32_t* d_sh
                                       origin, 0, nullptr);
   const s3h::LaunchArgs B = make_args(M, d_base, d_md5, ranged ? M->d_state : nullptr, b0, b1,
                                       origin, 0, nullptr);
+  uint64_t* progress = nullptr;
+  uint32_t epoch = 0;
+  if (s3h::kMd5XcdPace && ((mode == kDualGroupMixed && S->dual_apart) || mode == kDualSplit)) {
+    // the skew groups' producer step counts (F <= CUs groups in the mixed grid, sha_grid <= CUs
+    // in the split grid; slot (g % 8) * 128 + g / 8); zeroed once, then every launch tags its
+    // counts with a new epoch
+    constexpr uint64_t kProgressSlots = 1024;
+    const uint64_t groups = mode == kDualSplit ? S->grid : S->dual_solo;
+    if (groups > kProgressSlots)
+      return fail(S3H_EINVAL, "dual grid: %llu skew groups", (unsigned long long)groups);
+    if (!S->d_progress) {
+      HIP_TRY(hipMalloc(&S->d_progress, kProgressSlots * sizeof(uint64_t)));
+      HIP_TRY(hipMemsetAsync(S->d_progress, 0, kProgressSlots * sizeof(uint64_t), stream));
+    }
+    if (++S->progress_epoch == 0) S->progress_epoch = 1;
+    progress = S->d_progress;
+    epoch = S->progress_epoch;
+  }
   (void)hipGetLastError();
-  HIP_TRY(launch_dual_kernel(mode, S, M, A, B, stream));
+  HIP_TRY(launch_dual_kernel(mode, S, M, A, B, progress, epoch, stream));
   return S3H_OK;
 }
 
@@ -549,6 +568,7 @@ int s3h_plan_destroy(s3h_plan_t P) {
   (void)hipFree(P->d_state);
   (void)hipFree(P->d_zero);
   (void)hipFree(P->d_err);
+  (void)hipFree(P->d_progress);
   delete P;
   return S3H_OK;
 }

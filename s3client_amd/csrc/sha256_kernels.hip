@@ -846,11 +846,17 @@ __device__ __forceinline__ void produce_block_simple(const RawBlock& r,
 }
 
 // SIMPLE: the producer is written in the co-issuable instruction classes (it shares its
-// consumer's SIMD: sha256_skew_shared_kernel).
-template <int NC, bool PAIR, bool FLAGS, bool SIMPLE = false>
+// consumer's SIMD: sha256_skew_shared_kernel).  GPROG: the producer also stores each published
+// step count, tagged (epoch << 32 | steps), to `gprog` when it is non-null -- the pacing hint
+// of MD5 waves on other workgroups of the same XCD (ShaPacer): a plain store, which stays in
+// this XCD's L2 where those waves' L2-served polls read it (an agent-scope store would write
+// through to memory and drop the line, and every poll would then cross the fabric); one 8-byte
+// store per step, never read back by this group.
+template <int NC, bool PAIR, bool FLAGS, bool SIMPLE = false, bool GPROG = false>
 __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t group,
                                           const uint32_t role, SkewLds<NC, PAIR>& L,
-                                          uint32_t* flags) {
+                                          uint32_t* flags, uint64_t* gprog = nullptr,
+                                          uint32_t epoch = 0) {
   static_assert(!FLAGS || NC == 1, "flag-synchronised groups have one consumer wave");
   using G = SkewGeom<NC, PAIR>;
   constexpr uint32_t kCpw = G::kCpw, kParts = G::kParts, kBps = G::kBps, kCols = G::kCols;
@@ -867,6 +873,11 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
       if (!S3H_EXP_STALL_PRODUCER || (m) <= 1u) flag_publish(&flags[0], (m)); \
     } else {                                                                  \
       __syncthreads();                                                        \
+    }                                                                         \
+    if constexpr (GPROG && !S3H_EXP_GPROG_OFF) {                              \
+      if (gprog)                                                              \
+        __hip_atomic_store(gprog, (uint64_t(epoch) << 32) | uint64_t(m),      \
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);   \
     }                                                                         \
   } while (0)
 
@@ -1592,17 +1603,123 @@ __device__ __forceinline__ void md5_produce(const RawBlock& r, uint32_t sel, con
 // profiles/r04_c3_dual_mixed_counters.json).  Paced, block B is fetched only once the producer
 // has published step B / kPaceBps, i.e. after its own load of B was issued, microseconds
 // earlier on the same CU: the MD5 read hits L2.  Pacing is a cache policy, not a dependency --
-// the MD5 digests never read the producer's output -- so a wait that runs past kPaceSpinLimit
-// polls (~1.7 ms; a producer step is ~10 us) just stops pacing for the rest of the launch.
-constexpr uint32_t kPaceSpinLimit = 1u << 16;
-template <uint32_t kChains, uint32_t kPaceBps = 0>
+// the MD5 digests never read the producer's output -- so a wait that runs past
+// (kPaceWaitTicks, 200 us; a producer step is ~10 us) just stops pacing for the rest of the launch.
+//
+// kXcd (MD5 chains of skew groups that run on OTHER workgroups: the mixed grid's apart MD5
+// workgroups, the split grid's MD5 workgroups): workgroups b and b + 8 share an XCD (and its
+// L2; MI355X_MICROARCH.md "Workgroup dispatch"), so an MD5 workgroup takes the skew groups of
+// its own class blockIdx.x (mod 8) -- XcdChains -- and follows their producers' step counts in
+// global memory (ShaPacer, skew_body GPROG).
+// A wait longer than this (s_memrealtime ticks, 100 MHz: 200 us, ~20-30 producer steps) turns
+// pacing off for the rest of the launch (a producer that is not running, e.g. a shared device).
+constexpr uint64_t kPaceWaitTicks = 20000;
+
+// Where skew group g's producer step count lives in the progress array: the groups of one
+// XCD class side by side, so the eight an MD5 wave follows share one 64-byte line (one L2
+// read per poll).  < kProgressSlots (plan.cpp) for g < 1,024.
+__device__ __forceinline__ uint32_t xcd_progress_slot(uint32_t g) { return (g & 7u) * 128u + (g >> 3); }
+
+// Chains of an MD5 wave in XCD-class order: chain c = c0 + i (c0 = 64 x the wave's index among
+// its class's waves) is part c % 8 of skew group g = xcls + 8 (c / 8), slot 8g + c % 8, over
+// `ngroups` skew groups of 8 slots and `n` slots.  Slots ascend with i, so lane 0 holds the
+// wave's longest part and its last valid lane the shortest, as in a contiguous group.
+struct XcdChains {
+  uint32_t xcls, c0, ngroups, n;
+  __device__ uint32_t slot_of(uint32_t i) const {
+    const uint32_t c = c0 + i;
+    return 8u * (xcls + 8u * (c >> 3)) + (c & 7u);
+  }
+  __device__ uint32_t count() const {  // valid chains (a prefix of the lanes)
+    const uint32_t in_cls = ngroups > xcls ? (ngroups - xcls + 7u) / 8u : 0u;
+    const uint32_t first = c0 >> 3;
+    if (in_cls <= first) return 0;
+    const uint32_t k = in_cls - first < 8u ? in_cls - first : 8u;  // this wave's skew groups
+    const uint32_t end = slot_of(8u * k - 1u) + 1u;                 // the last group may be partial
+    return end <= n ? 8u * k : 8u * k - (end - n);
+  }
+};
+
+// Waits, before the MD5 wave fetches block b0 + B, until the SHA-256 producer(s) of the same
+// parts have published step B / kPaceBps (their loads of B are then issued).  LDS form: the
+// workgroup's own producer counter; global form (kGlobal): the minimum over the wave's skew
+// groups of gprog[group] = (epoch << 32 | steps), another launch's epoch reading as 0, over
+// the lanes that still fetch data of their own part (B < `data_end`, blocks past b0): a lane
+// whose part has ended -- or whose group has nothing in this launch's range -- waits for no
+// producer (its group's producer stops publishing once the group's longest part ends).
+template <uint32_t kPaceBps, bool kGlobal>
+struct ShaPacer {
+  const uint32_t* lds;
+  const uint64_t* gprog;
+  uint32_t epoch, group;  // global form: this lane's skew group (ignored where !valid)
+  bool valid;
+  uint64_t data_end;  // global form: this lane's part's blocks of data past b0
+  uint32_t seen = 0;  // wave-uniform: the last step count read
+  bool on = kPaceBps != 0;
+  __device__ __forceinline__ void wait_for(uint64_t B) {
+    if constexpr (kPaceBps != 0) {
+      if (!on) return;
+      const uint32_t need = (B < 2 * kPaceBps ? 1u : uint32_t(B / kPaceBps)) + S3H_EXP_PACE_LAG;
+      uint64_t t0 = 0;
+      while (seen < need) {
+        if constexpr (kGlobal) {
+          // the slowest of this wave's skew groups (a poll only happens when the wave has
+          // caught up with them; its wait for the wave's own loads is then no extra stall)
+          uint32_t m = 0xffffffffu;
+          if (valid && B < data_end) {
+            // agent scope: L2-served (no stale L1 line); the producer is on this XCD
+            const uint64_t v = __hip_atomic_load(gprog + xcd_progress_slot(group), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            m = uint32_t(v >> 32) == epoch ? uint32_t(v) : 0u;
+          }
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t t = __shfl_xor(m, o);
+            m = t < m ? t : m;
+          }
+          seen = __builtin_amdgcn_readfirstlane(m);
+        } else {
+          seen = __builtin_amdgcn_readfirstlane(
+              __hip_atomic_load(lds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        }
+        if (seen >= need) break;
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (t0 == 0) {
+          t0 = now;
+        } else if (now - t0 > kPaceWaitTicks) {
+          on = false;
+          return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+  }
+};
+
+template <uint32_t kChains, uint32_t kPaceBps = 0, bool kXcd = false>
 __device__ __forceinline__ void md5_self_body(const LaunchArgs& A, const uint32_t group,
-                                              const uint32_t* pace = nullptr) {
+                                              const uint32_t* pace = nullptr,
+                                              const uint64_t* gprog = nullptr, uint32_t epoch = 0,
+                                              uint32_t nskew = 0) {
+  static_assert(!kXcd || (kChains == 64 && kPaceBps != 0), "XCD-class MD5 waves: 64 paced chains");
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t slot0 = group * kChains;
-  if (slot0 >= A.n) return;
-  const uint32_t slot = slot0 + lane;
-  const bool valid = lane < kChains && slot < A.n;
+  // chains of this wave: slot_of(i) for i < nvalid, ascending in i
+  const XcdChains xc = {blockIdx.x & 7u, 64u * (group >> 3), nskew, A.n};
+  auto slot_of = [&](uint32_t i) -> uint32_t {
+    if constexpr (kXcd) return xc.slot_of(i);
+    else return group * kChains + i;
+  };
+  uint32_t nvalid;
+  if constexpr (kXcd) {
+    nvalid = xc.count();
+  } else {
+    const uint32_t slot0 = group * kChains;
+    nvalid = slot0 >= A.n ? 0u : (A.n - slot0 < kChains ? A.n - slot0 : kChains);
+  }
+  if (nvalid == 0) return;
+  const uint32_t slot0 = slot_of(0);
+  const bool valid = lane < nvalid;
+  const uint32_t slot = valid ? slot_of(lane) : slot0;
   Slot s = {0, 0};
   if (valid) s = A.slots[slot];
   const uint64_t nb = valid ? slot_blocks(A, s.len) : 0;
@@ -1628,29 +1745,13 @@ __device__ __forceinline__ void md5_self_body(const LaunchArgs& A, const uint32_
   // word -- so the compiler keeps counted vmcnt waits; the padding blocks at the end run the
   // general decode (its byte loads would otherwise force a full vmcnt drain every block).
   constexpr uint32_t kDepth = S3H_EXP_MD5_SELF_DEPTH, kRing = kDepth + 1;
-  const uint32_t last = (slot0 + kChains <= A.n ? slot0 + kChains : A.n) - 1;
+  const uint32_t last = slot_of(nvalid - 1);
   const uint64_t full_end = (A.slots[last].len >> 6) < A.blk_end ? (A.slots[last].len >> 6) : A.blk_end;
   const uint64_t nfast = full_end > b0 ? (full_end - b0) / kRing * kRing : 0;  // whole rings
   RawBlock ring[kRing];
-  // Paced: the producer step count last read (wave-uniform) and whether pacing is still on.
-  uint32_t seen = 0;
-  bool pacing = kPaceBps != 0;
+  ShaPacer<kPaceBps, kXcd> pacer = {pace, gprog, epoch, slot >> 3, valid, fend > b0 ? fend - b0 : 0};
   auto pace_to = [&](uint64_t B) {  // before fetching block b0 + B
-    if constexpr (kPaceBps != 0) {
-      if (!pacing || B >= iters) return;  // past the range: the zero page, nothing to share
-      const uint32_t need = B < 2 * kPaceBps ? 1u : uint32_t(B / kPaceBps);
-      uint32_t spin = 0;
-      while (seen < need) {
-        seen = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(pace, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (seen >= need) break;
-        if (++spin >= kPaceSpinLimit) {
-          pacing = false;
-          return;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
+    if (B < iters) pacer.wait_for(B);  // past the range: the zero page, nothing to share
   };
 #pragma unroll
   for (uint32_t k = 0; k < kDepth; ++k) {
@@ -1723,14 +1824,35 @@ struct Md5Lds {
 #else
 #define S3H_MD5_SYNC() __syncthreads()
 #endif
-template <int kBps>
+// kXcd (the split dual grid, sha256_md5_dual_kernel): the workgroup's 64 chains are those of
+// the skew groups on its own XCD (XcdChains over `ngroups` groups), and the producer fetches a
+// step only once those groups' producers have fetched it (ShaPacer, global form) -- one HBM
+// read of every part for both digests.
+template <int kBps, bool kXcd = false>
 __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t group,
-                                            const uint32_t role, Md5Lds<kBps>& L) {
+                                            const uint32_t role, Md5Lds<kBps>& L,
+                                            const uint64_t* gprog = nullptr, uint32_t epoch = 0,
+                                            uint32_t ngroups = 0) {
   auto& lds_km = L.km;
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t slot0 = group * 64u;
-  const uint32_t slot = slot0 + lane;
-  const bool valid = slot < A.n;
+  const XcdChains xc = {blockIdx.x & 7u, 64u * (group >> 3), ngroups, A.n};
+  uint32_t slot0, slot;  // the first chain's and this lane's slot
+  bool valid;
+  if constexpr (kXcd) {
+    const uint32_t nvalid = xc.count();
+    if (nvalid == 0) return;  // uniform across the workgroup: both waves leave before any barrier
+    slot0 = xc.slot_of(0);
+    valid = lane < nvalid;
+    slot = valid ? xc.slot_of(lane) : slot0;
+  } else {
+    slot0 = group * 64u;
+    slot = slot0 + lane;
+    valid = slot < A.n;
+  }
+  auto last_slot = [&]() -> uint32_t {  // the last valid chain's slot (the shortest part)
+    if constexpr (kXcd) return xc.slot_of(xc.count() - 1);
+    else return (slot0 + 64u <= A.n ? slot0 + 64u : A.n) - 1;
+  };
   Slot s = {0, 0};
   if (valid) s = A.slots[slot];
   const uint64_t nb = valid ? slot_blocks(A, s.len) : 0;
@@ -1759,7 +1881,15 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
     // wave ran it (MD5 of 300 parts of U[1, 16] MiB: 1.85x the longest chain's time).
     const uint64_t lim = nb < A.blk_end ? nb : A.blk_end;
     RawBlock ra[kBps], rb[kBps];
+    ShaPacer<kXcd ? SkewGeom<1, false>::kBps : 0, true> pacer = {nullptr, gprog, epoch, slot >> 3, valid,
+                                                                 fend > b0 ? fend - b0 : 0};
+    // kXcd: step K's last block, once the skew producers have fetched it
 #define S3H_MD5_FETCH(R, K)                                                                  \
+    if constexpr (kXcd) {                                                                    \
+      if (uint64_t(K) * kBps < iters)                                                        \
+        pacer.wait_for(uint64_t(K) * kBps + kBps - 1 < iters ? uint64_t(K) * kBps + kBps - 1 \
+                                                             : iters - 1);                   \
+    }                                                                                        \
     _Pragma("unroll") for (int h = 0; h < kBps; ++h)                                        \
       fetch_full(p + 64 * ((K) * kBps + h), b0 + (K) * kBps + h < fend, A.zero, R[h]);
 #define S3H_MD5_MAKE_T(R, K, FULL)                                                           \
@@ -1770,7 +1900,7 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
     // Steps below `full_steps` hold whole data blocks of every lane's part (slots are sorted
     // by length; the group's last valid slot is the shortest; lanes past n decode_len past
     // everything): a compact loop with the perm-only decode runs them in pairs.
-    const uint32_t lastv = (slot0 + 64u <= A.n ? slot0 + 64u : A.n) - 1;
+    const uint32_t lastv = last_slot();
     const uint64_t fabs = A.slots[lastv].len >> 6 < A.blk_end ? A.slots[lastv].len >> 6 : A.blk_end;
     const uint64_t full_steps = fabs > b0 ? (fabs - b0) / kBps : 0;
     // Register sets of raw blocks in flight: with 4-block steps (md5_pc_kernel<4>) two sets --
@@ -1863,7 +1993,7 @@ __device__ __forceinline__ void md5_pc_body(const LaunchArgs& A, const uint32_t 
     }
     S3H_MD5_SYNC();
     // slots are sorted by length: every chain of the group is live below the last one's end
-    const uint32_t last = (slot0 + 64u <= A.n ? slot0 + 64u : A.n) - 1;
+    const uint32_t last = last_slot();
     const uint64_t live_end = slot_blocks(A, A.slots[last].len);
     uint64_t clk0 = 0, rt0 = 0;  // clock probe (s3h_plan_set_clock_probe), as in skew_body
     if (A.clocks) {
@@ -1972,16 +2102,25 @@ __global__ __launch_bounds__(kPcThreads) void md5_pc_kernel(LaunchArgs A) {
 // profiles/r01_dual_kernel_trace.txt); one grid of <= 256 workgroups is placed one per CU
 // (profiles/r01_placement.txt).  Used while sha_grid + md5_grid <= #CUs (skew, <= 2,048 parts).
 static_assert(kPcThreads == 128, "dual kernel assumes 128-thread MD5 workgroups");
+// Experiment S3H_EXP_MD5_XCD_PACE (kernel_abi.hpp kMd5XcdPace): the MD5 workgroups take the
+// chains of the skew groups on their own XCD and fetch each step after those groups' producers
+// have (md5_pc_body kXcd; the producers store their step counts to `progress`, tagged with
+// `epoch`), so C2's parts are read from HBM about once for both digests -- measured 0.3 %
+// slower, not the product.  Product: MD5 slots 64w.. per workgroup, unpaced.
 template <bool PAIR>
 __global__ __launch_bounds__(128) void sha256_md5_dual_kernel(LaunchArgs S, LaunchArgs M,
-                                                              uint32_t sha_grid) {
+                                                              uint32_t sha_grid, uint64_t* progress,
+                                                              uint32_t epoch) {
   __shared__ SkewLds<1, PAIR> LS;
   __shared__ Md5Lds<2> LM;  // 64 KiB beside the skew group's 36 KiB
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr bool kPaced = kMd5XcdPace && !PAIR;  // XcdChains assumes 8-part skew groups
   if (blockIdx.x < sha_grid)
-    skew_body<1, PAIR, false>(S, blockIdx.x, wave, LS, nullptr);
+    skew_body<1, PAIR, false, false, kPaced>(S, blockIdx.x, wave, LS, nullptr,
+                                             progress ? progress + xcd_progress_slot(blockIdx.x) : nullptr,
+                                             epoch);
   else
-    md5_pc_body<2>(M, blockIdx.x - sha_grid, wave, LM);
+    md5_pc_body<2, kPaced>(M, blockIdx.x - sha_grid, wave, LM, progress, epoch, sha_grid);
 }
 
 // sha256_md5_group_kernel: every workgroup holds BOTH digests of the same kParts parts -- a
@@ -2024,10 +2163,17 @@ __global__ __launch_bounds__(192) void sha256_md5_group_kernel(LaunchArgs S, Lau
 // whose slot / out_idx arrays start at slot 8F; the clock probe is off (two group numberings).
 // With `lead_md5` > 0 the 8F longest slots' MD5 chains run apart, on `lead_md5` workgroups
 // after the G skewp ones (one self-fed MD5 wave of 64 chains each), so those skew groups run
-// their SHA-256 alone on their CUs (capi.hip dual_mixed_solo: when that grid fits).
+// their SHA-256 alone on their CUs (plan.cpp dual_mixed_solo: when that grid fits).  The skewp
+// groups' MD5 waves follow their own producer through LDS (one HBM read of those parts for both
+// digests); the apart MD5 waves run unpaced -- pacing them across workgroups
+// (S3H_EXP_MD5_XCD_PACE: each takes the skew groups of its own XCD and follows their
+// producers' step counts in `progress`, tagged with this launch's `epoch`) cut C3's traffic
+// 1.25x -> 1.18x but cost 3-4 % of its rate.
 __global__ __launch_bounds__(192) void sha256_md5_group_mixed_kernel(LaunchArgs S, LaunchArgs M,
                                                                     uint32_t F, uint32_t G,
-                                                                    uint32_t lead_md5) {
+                                                                    uint32_t lead_md5,
+                                                                    uint64_t* progress,
+                                                                    uint32_t epoch) {
   __shared__ union {
     SkewLds<1, false> skew;
     SkewLds<1, true> skewp;
@@ -2040,7 +2186,9 @@ __global__ __launch_bounds__(192) void sha256_md5_group_mixed_kernel(LaunchArgs 
   constexpr uint32_t kSolo = SkewGeom<1, false>::kParts;
   if (blockIdx.x < F) {
     if (wave != 1)
-      skew_body<1, false, true>(S, blockIdx.x, wave >> 1, L.skew, flags);
+      skew_body<1, false, true, false, kMd5XcdPace && kMd5PaceBps<false> != 0>(
+          S, blockIdx.x, wave >> 1, L.skew, flags,
+          lead_md5 ? progress + xcd_progress_slot(blockIdx.x) : nullptr, epoch);
     else if (!lead_md5)
       md5_self_body<kSolo, kMd5PaceBps<false>>(M, blockIdx.x, &flags[0]);
     return;
@@ -2048,7 +2196,12 @@ __global__ __launch_bounds__(192) void sha256_md5_group_mixed_kernel(LaunchArgs 
   if (lead_md5 && blockIdx.x >= F + G) {  // MD5 of slots 0 .. 8F-1, 64 chains per workgroup
     if (wave != 1) return;
     M.n = M.n < kSolo * F ? M.n : kSolo * F;
-    md5_self_body<64>(M, blockIdx.x - F - G);
+    if constexpr (kMd5XcdPace && kMd5PaceBps<false> != 0)
+      // lead_md5 = mixed_lead_wgs(F): 8 XCD classes x ceil(F / 64) workgroups, each over the
+      // skew groups that share its XCD, paced by their producers' global step counts
+      md5_self_body<64, kMd5PaceBps<false>, true>(M, blockIdx.x - F - G, nullptr, progress, epoch, F);
+    else
+      md5_self_body<64>(M, blockIdx.x - F - G);  // slots 64w.., unpaced (the product)
     return;
   }
   const uint32_t shift = kSolo * F;

@@ -45,10 +45,10 @@ ALL_KERNELS = {
     "skewp": KERNELS["skewp"][0], "skews": KERNELS["skews"][0],
     "md5-pc": "_ZN3s3h13md5_pc_kernelILi4EEEvNS_10LaunchArgsE",
     "md5-pc1": "_ZN3s3h13md5_pc_kernelILi1EEEvNS_10LaunchArgsE",
-    "dual_split": "_ZN3s3h22sha256_md5_dual_kernelILb0EEEvNS_10LaunchArgsES1_j",
+    "dual_split": "_ZN3s3h22sha256_md5_dual_kernelILb0EEEvNS_10LaunchArgsES1_jPmj",
     "dual_group": "_ZN3s3h23sha256_md5_group_kernelILb1EEEvNS_10LaunchArgsES1_",
     "dual_group_skew": "_ZN3s3h23sha256_md5_group_kernelILb0EEEvNS_10LaunchArgsES1_",
-    "dual_group_mixed": "_ZN3s3h29sha256_md5_group_mixed_kernelENS_10LaunchArgsES0_jjj",
+    "dual_group_mixed": "_ZN3s3h29sha256_md5_group_mixed_kernelENS_10LaunchArgsES0_jjjPmj",
 }
 FLAG_KERNELS = ("skew_nc2", "skews", "dual_group", "dual_group_skew", "dual_group_mixed")
 ERR_STORE = re.compile(r"^\t(global|flat|buffer)_atomic_or\b")
