@@ -1602,17 +1602,19 @@ __device__ __forceinline__ void md5_produce(const RawBlock& r, uint32_t sel, con
 // ran ahead and both chains read every byte from HBM (C3 dual: 2.0017x the algorithmic bytes,
 // profiles/r04_c3_dual_mixed_counters.json).  Paced, block B is fetched only once the producer
 // has published step B / kPaceBps, i.e. after its own load of B was issued, microseconds
-// earlier on the same CU: the MD5 read hits L2.  Pacing is a cache policy, not a dependency --
-// the MD5 digests never read the producer's output -- so a wait that runs past
-// (kPaceWaitTicks, 200 us; a producer step is ~10 us) just stops pacing for the rest of the launch.
+// earlier on the same CU: the MD5 read hits the CU's L1 or L2.  Pacing is a cache policy, not
+// a dependency -- the MD5 digests never read the producer's output -- so a wait longer than
+// kPaceWaitTicks just stops pacing for the rest of the launch.
 //
-// kXcd (MD5 chains of skew groups that run on OTHER workgroups: the mixed grid's apart MD5
-// workgroups, the split grid's MD5 workgroups): workgroups b and b + 8 share an XCD (and its
-// L2; MI355X_MICROARCH.md "Workgroup dispatch"), so an MD5 workgroup takes the skew groups of
-// its own class blockIdx.x (mod 8) -- XcdChains -- and follows their producers' step counts in
-// global memory (ShaPacer, skew_body GPROG).
-// A wait longer than this (s_memrealtime ticks, 100 MHz: 200 us, ~20-30 producer steps) turns
-// pacing off for the rest of the launch (a producer that is not running, e.g. a shared device).
+// kXcd (experiment S3H_EXP_MD5_XCD_PACE; MD5 chains of skew groups that run on OTHER
+// workgroups: the mixed grid's apart MD5 workgroups, the split grid's MD5 workgroups):
+// workgroups b and b + 8 share an XCD (and its L2; MI355X_MICROARCH.md "Workgroup dispatch",
+// tools/xcd_probe.hip), so an MD5 workgroup takes the skew groups of its own class
+// blockIdx.x (mod 8) -- XcdChains -- and follows their producers' step counts in global
+// memory (ShaPacer, skew_body GPROG).
+
+// s_memrealtime ticks (100 MHz): 200 us, ~20-30 producer steps -- a producer that is not
+// running (a shared device, the forced-stall build) turns pacing off instead of stalling MD5.
 constexpr uint64_t kPaceWaitTicks = 20000;
 
 // Where skew group g's producer step count lives in the progress array: the groups of one
