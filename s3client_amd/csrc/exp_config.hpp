@@ -49,9 +49,10 @@
 #define S3H_EXP_PACE_LAG 0  // MD5 pacing: extra producer steps to wait for beyond the block's own
 #endif
 #ifndef S3H_EXP_SKEW_MERGE_NEXT
-// 1: skew / skewp consumers read the next block's rows before rounds 0-15 and end a block with
-// one statement (rounds 16-63 + NEXT): one LDS wait per block instead of two
-#define S3H_EXP_SKEW_MERGE_NEXT 0
+// skew consumers read the next block's rows before rounds 0-15 and end a block with one
+// statement (rounds 16-63 + NEXT): one LDS wait per block instead of two.  1: the quad layout
+// (skew / skews), 0: never (rounds 1-6), 2: also the lane-pair layout (skewp)
+#define S3H_EXP_SKEW_MERGE_NEXT 1
 #endif
 #ifndef S3H_EXP_MD5_XCD_PACE
 // 1: MD5 workgroups of the split / mixed dual grids paced by the skew groups on their XCD
@@ -82,7 +83,7 @@ static_assert(S3H_EXP_MD5_PSETS1 == 3, "product build: three sets for 1-block MD
 static_assert(S3H_EXP_MIXED_MD5_APART == 1, "product build: skew groups' MD5 apart when it fits");
 static_assert(S3H_EXP_TAIL_RAMP_DIV == 8, "product build: host tail slices shrink by 7/8");
 static_assert(S3H_EXP_SPIN_LIMIT == (1u << 24), "product build: flag waits give up after 2^24 polls");
-static_assert(S3H_EXP_SKEW_MERGE_NEXT == 0, "product build: three statements per skew block");
+static_assert(S3H_EXP_SKEW_MERGE_NEXT == 1, "product build: quad-layout blocks end in one statement");
 static_assert(S3H_EXP_MD5_XCD_PACE == 0, "product build: MD5 paced within a workgroup only");
 static_assert(S3H_EXP_GPROG_OFF == 0, "product build: skew producers publish their step counts");
 static_assert(S3H_EXP_PACE_LAG == 0, "product build: MD5 waits for its block's own producer step");

@@ -646,7 +646,7 @@ __global__ __launch_bounds__(64 * (NC + 1)) void sha256_quad_kernel(LaunchArgs A
       [w57] "v"(W[57]), [w58] "v"(W[58]), [w59] "v"(W[59]), [w60] "v"(W[60]), [w61] "v"(W[61]),   \
       [w62] "v"(W[62]), [w63] "v"(W[63]), [am] "v"(am), [mk] "v"(mk), [am2] "v"(am2), [am3] "v"(am3)
 
-// The next block's rows as inputs of the statement that ends a block (S3H_EXP_SKEW_MERGE_NEXT):
+// The next block's rows as inputs of the statement that ends a block (skew_body kMergeNext):
 // w0 is NEXT's operand, the rest only make the compiler wait for every row there.
 #define S3H_SKEW_WNEXT(W) [w0] "v"(W[0]), [nw1] "v"(W[1]), [nw2] "v"(W[2]), [nw3] "v"(W[3]), [nw4] "v"(W[4]), [nw5] "v"(W[5]), [nw6] "v"(W[6]), [nw7] "v"(W[7]), [nw8] "v"(W[8]), [nw9] "v"(W[9]), [nw10] "v"(W[10]), [nw11] "v"(W[11]), [nw12] "v"(W[12]), [nw13] "v"(W[13]), [nw14] "v"(W[14]), [nw15] "v"(W[15]), [nw16] "v"(W[16]), [nw17] "v"(W[17]), [nw18] "v"(W[18]), [nw19] "v"(W[19]), [nw20] "v"(W[20]), [nw21] "v"(W[21]), [nw22] "v"(W[22]), [nw23] "v"(W[23]), [nw24] "v"(W[24]), [nw25] "v"(W[25]), [nw26] "v"(W[26]), [nw27] "v"(W[27]), [nw28] "v"(W[28]), [nw29] "v"(W[29]), [nw30] "v"(W[30]), [nw31] "v"(W[31]), [nw32] "v"(W[32]), [nw33] "v"(W[33]), [nw34] "v"(W[34]), [nw35] "v"(W[35]), [nw36] "v"(W[36]), [nw37] "v"(W[37]), [nw38] "v"(W[38]), [nw39] "v"(W[39]), [nw40] "v"(W[40]), [nw41] "v"(W[41]), [nw42] "v"(W[42]), [nw43] "v"(W[43]), [nw44] "v"(W[44]), [nw45] "v"(W[45]), [nw46] "v"(W[46]), [nw47] "v"(W[47]), [nw48] "v"(W[48]), [nw49] "v"(W[49]), [nw50] "v"(W[50]), [nw51] "v"(W[51]), [nw52] "v"(W[52]), [nw53] "v"(W[53]), [nw54] "v"(W[54]), [nw55] "v"(W[55]), [nw56] "v"(W[56]), [nw57] "v"(W[57]), [nw58] "v"(W[58]), [nw59] "v"(W[59]), [nw60] "v"(W[60]), [nw61] "v"(W[61]), [nw62] "v"(W[62]), [nw63] "v"(W[63])
 
@@ -1102,34 +1102,37 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
   // Fast steps -- none of whose blocks can end the launch or a chain -- run fully unrolled
   // with no per-block test; the remaining blocks (the ragged tail and the launch's last
   // block) run one at a time with the step barrier, capture and exit checks.
-#if S3H_EXP_SKEW_MERGE_NEXT
-  // Experiment: the next block's rows are read before this block's rounds 0-15 (the step
-  // barrier moves with them), and rounds 16-63 + NEXT are one statement that takes every one of
-  // them as an input, so the compiler drains LDS once per block (the rows arrived long before)
-  // and the block is two statements instead of three.
+  // The next block's rows are read before this block's rounds 0-15 (the step barrier moves
+  // with them), and rounds 16-63 + NEXT are one statement that takes every one of them as an
+  // input: the compiler drains LDS once per block (the rows arrived ~500 cycles before) and a
+  // block is two statements instead of three -- 543.88 -> 542.38 instructions per block, C2
+  // 2,207.1 -> 2,202.8 cycles per block and C4 skews 2,238.3 -> 2,232.4 in one lease; the lane
+  // pair layout (skewp) measured 2,476.1 -> 2,485.5 that way and keeps the three statements
+  // (profiles/r06_skew_merge_next_ab.json).  S3H_EXP_SKEW_MERGE_NEXT: 0 never, 2 also skewp.
+  constexpr bool kMergeNext = PAIR ? S3H_EXP_SKEW_MERGE_NEXT == 2 : S3H_EXP_SKEW_MERGE_NEXT >= 1;
 #define S3H_SKEW_FAST(L, P, CUR, NXT)                                                           \
-  if (i == kBps - 1) {                                                                          \
-    S3H_SYNC_STEP(j + 1, j + 2);                                                                \
-    load(NXT, nbuf);                                                                            \
+  if constexpr (kMergeNext) {                                                                   \
+    if (i == kBps - 1) {                                                                        \
+      S3H_SYNC_STEP(j + 1, j + 2);                                                              \
+      load(NXT, nbuf);                                                                          \
+    } else {                                                                                    \
+      load(NXT, buf + (i + 1) * kBlkStride);                                                    \
+    }                                                                                           \
+    asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_A_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));         \
+    asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_B_##P S3H_##L##_NEXT_##P                           \
+                 : S3H_SKEW_STATE : S3H_SKEW_W(CUR), S3H_SKEW_WNEXT(NXT));                      \
   } else {                                                                                      \
-    load(NXT, buf + (i + 1) * kBlkStride);                                                      \
-  }                                                                                             \
-  asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_A_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));           \
-  asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_B_##P S3H_##L##_NEXT_##P                             \
-               : S3H_SKEW_STATE : S3H_SKEW_W(CUR), S3H_SKEW_WNEXT(NXT));
-#else
-#define S3H_SKEW_FAST(L, P, CUR, NXT)                                                           \
-  asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_A_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));           \
-  if (i == kBps - 1) {                                                                          \
-    S3H_SYNC_STEP(j + 1, j + 2);                                                                \
-    load(NXT, nbuf);                                                                            \
-  } else {                                                                                      \
-    load(NXT, buf + (i + 1) * kBlkStride);                                                      \
-  }                                                                                             \
-  asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_B_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));           \
-  asm volatile(S3H_ALIGN8 S3H_##L##_NEXT_##P                                                    \
-               : S3H_SKEW_STATE : [w0] "v"(NXT[0]), [am] "v"(am), [mk] "v"(mk));
-#endif
+    asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_A_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));         \
+    if (i == kBps - 1) {                                                                        \
+      S3H_SYNC_STEP(j + 1, j + 2);                                                              \
+      load(NXT, nbuf);                                                                          \
+    } else {                                                                                    \
+      load(NXT, buf + (i + 1) * kBlkStride);                                                    \
+    }                                                                                           \
+    asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_B_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));         \
+    asm volatile(S3H_ALIGN8 S3H_##L##_NEXT_##P                                                  \
+                 : S3H_SKEW_STATE : [w0] "v"(NXT[0]), [am] "v"(am), [mk] "v"(mk));              \
+  }
 #define S3H_SKEW_SLOW(L, P, CUR, NXT)                                                           \
   {                                                                                             \
     asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_A_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));         \
