@@ -62,6 +62,18 @@
 #ifndef S3H_EXP_GPROG_OFF
 #define S3H_EXP_GPROG_OFF 0  // 1: skew producers never store their global step counts (MD5 waits time out)
 #endif
+// ragged dual grid (plan.cpp dual_mixed_solo): cycles per block of a skewp group beside its MD5
+// wave, and of a skew group with its MD5 apart / beside it -- the rates the split into skew
+// and skewp groups is planned with
+#ifndef S3H_EXP_DUAL_SKEWP_CYC
+#define S3H_EXP_DUAL_SKEWP_CYC 2550
+#endif
+#ifndef S3H_EXP_DUAL_SKEW_CYC_APART
+#define S3H_EXP_DUAL_SKEW_CYC_APART 2224
+#endif
+#ifndef S3H_EXP_DUAL_SKEW_CYC_INGROUP
+#define S3H_EXP_DUAL_SKEW_CYC_INGROUP 2280
+#endif
 #ifndef S3H_EXP_SPIN_LIMIT
 #define S3H_EXP_SPIN_LIMIT (1u << 24)  // flag waits: s_sleep 1 polls before a wait times out
 #endif
@@ -82,6 +94,9 @@ static_assert(S3H_EXP_MD5_PSETS == 2, "product build: two MD5 producer register 
 static_assert(S3H_EXP_MD5_PSETS1 == 3, "product build: three sets for 1-block MD5 steps");
 static_assert(S3H_EXP_MIXED_MD5_APART == 1, "product build: skew groups' MD5 apart when it fits");
 static_assert(S3H_EXP_TAIL_RAMP_DIV == 8, "product build: host tail slices shrink by 7/8");
+static_assert(S3H_EXP_DUAL_SKEWP_CYC == 2550 && S3H_EXP_DUAL_SKEW_CYC_APART == 2224 &&
+                  S3H_EXP_DUAL_SKEW_CYC_INGROUP == 2280,
+              "product build: the dual grid's planning rates");
 static_assert(S3H_EXP_SPIN_LIMIT == (1u << 24), "product build: flag waits give up after 2^24 polls");
 static_assert(S3H_EXP_SKEW_MERGE_NEXT == 1, "product build: quad-layout blocks end in one statement");
 static_assert(S3H_EXP_MD5_XCD_PACE == 0, "product build: MD5 paced within a workgroup only");

@@ -228,7 +228,8 @@ uint32_t dual_mixed_solo(const s3h::Slot* slots, uint64_t n, uint64_t cus, bool*
   if (n <= 2048 || cus == 0 || (n + kSkewp - 1) / kSkewp > cus) return 0;
   const double longest = double(s3h::nblocks(slots[0].len));
   for (int a = S3H_EXP_MIXED_MD5_APART; a >= 0; --a) {
-    const double ratio = a ? 2550.0 / 2224.0 : 2550.0 / 2280.0;
+    const double ratio = a ? double(S3H_EXP_DUAL_SKEWP_CYC) / S3H_EXP_DUAL_SKEW_CYC_APART
+                           : double(S3H_EXP_DUAL_SKEWP_CYC) / S3H_EXP_DUAL_SKEW_CYC_INGROUP;
     uint64_t lo = 0, hi = n;  // first slot whose part ends in time at the skewp rate
     while (lo < hi) {
       const uint64_t mid = (lo + hi) / 2;
