@@ -64,9 +64,11 @@
 #endif
 // ragged dual grid (plan.cpp dual_mixed_solo): cycles per block of a skewp group beside its MD5
 // wave, and of a skew group with its MD5 apart / beside it -- the rates the split into skew
-// and skewp groups is planned with
+// and skewp groups is planned with.  2,650 from a sweep on C3 (profiles/
+// r06_dual_mixed_planning_sweep.json: 2,550, calibrated on the C4 shard's equal parts, left
+// C3's ragged skewp groups finishing last)
 #ifndef S3H_EXP_DUAL_SKEWP_CYC
-#define S3H_EXP_DUAL_SKEWP_CYC 2550
+#define S3H_EXP_DUAL_SKEWP_CYC 2650
 #endif
 #ifndef S3H_EXP_DUAL_SKEW_CYC_APART
 #define S3H_EXP_DUAL_SKEW_CYC_APART 2224
@@ -94,7 +96,7 @@ static_assert(S3H_EXP_MD5_PSETS == 2, "product build: two MD5 producer register 
 static_assert(S3H_EXP_MD5_PSETS1 == 3, "product build: three sets for 1-block MD5 steps");
 static_assert(S3H_EXP_MIXED_MD5_APART == 1, "product build: skew groups' MD5 apart when it fits");
 static_assert(S3H_EXP_TAIL_RAMP_DIV == 8, "product build: host tail slices shrink by 7/8");
-static_assert(S3H_EXP_DUAL_SKEWP_CYC == 2550 && S3H_EXP_DUAL_SKEW_CYC_APART == 2224 &&
+static_assert(S3H_EXP_DUAL_SKEWP_CYC == 2650 && S3H_EXP_DUAL_SKEW_CYC_APART == 2224 &&
                   S3H_EXP_DUAL_SKEW_CYC_INGROUP == 2280,
               "product build: the dual grid's planning rates");
 static_assert(S3H_EXP_SPIN_LIMIT == (1u << 24), "product build: flag waits give up after 2^24 polls");

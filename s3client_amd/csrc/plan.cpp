@@ -212,7 +212,8 @@ int device_cus(int device) {  // cached: the host pipeline asks once per slice
 }
 
 // Both digests of 2,049-8,192 parts (sha256_md5_group_kernel) run every chain at skewp's rate
-// beside a self-fed MD5 wave: ~2,550 cycles per block (C4 shard, 457 GiB/s for both).  A
+// beside a self-fed MD5 wave: ~2,550 cycles per block on the C4 shard's equal parts (457 GiB/s
+// for both), planned at 2,650 for ragged groups (exp_config.hpp S3H_EXP_DUAL_SKEWP_CYC).  A
 // ragged batch is timed by its longest parts, so sha256_md5_group_mixed_kernel gives the
 // longest F x 8 slots skew groups and the rest skewp groups: F = the fewest 8-slot groups
 // after which every remaining part, at the skewp rate, ends before the longest part does at

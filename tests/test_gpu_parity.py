@@ -315,20 +315,20 @@ def test_md5_beyond_one_workgroup_per_cu(torch_cuda, oracle):
 
 
 @pytest.mark.parametrize("n,shape,apart", [(2100, "ragged", True), (3000, "ragged", True),
-                                           (6000, "ragged", False), (2100, "between", False)])
+                                           (5500, "ragged", False), (2100, "between", False)])
 def test_dual_mixed_grid_ragged(torch_cuda, oracle, n, shape, apart):
     """SHA-256 + MD5 of a ragged batch in the skewp-group range (C3-like lengths, scaled):
     the one-grid mixed kernel (the longest parts in skew groups, the rest in skewp groups,
     slot arrays offset for the second half) vs the oracle, device- and host-resident, BOTH
     forms of it: the skew groups' MD5 on workgroups of their own (2,100 / 3,000 parts) and,
-    when that grid would exceed one workgroup per CU (6,000 parts), inside each skew group.
-    "between": one longest part and 2,099 at 0.88 of it -- every part needs a skew group at
+    when that grid would exceed one workgroup per CU (5,500 parts), inside each skew group.
+    "between": one longest part and 2,099 at 0.85 of it -- every part needs a skew group at
     the apart form's rate ratio, so only the in-group form's smaller ratio gives a mixed grid
     (F = 1; before the advisor-r4 fix this fell to the plain group kernel).  Equal lengths keep
     the plain group kernel (dual_solo 0)."""
     rng = np.random.default_rng(n)
     if shape == "between":
-        lens = np.full(n, int(64 * 1024 * 0.88), dtype=np.int64)
+        lens = np.full(n, int(64 * 1024 * 0.85), dtype=np.int64)
         lens[0] = 64 * 1024
     else:
         lens = 5 * 1024 + rng.integers(0, 59 * 1024 + 1, n)
