@@ -1110,8 +1110,33 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
   // pair layout (skewp) measured 2,476.1 -> 2,485.5 that way and keeps the three statements
   // (profiles/r06_skew_merge_next_ab.json).  S3H_EXP_SKEW_MERGE_NEXT: 0 never, 2 also skewp.
   constexpr bool kMergeNext = PAIR ? S3H_EXP_SKEW_MERGE_NEXT == 2 : S3H_EXP_SKEW_MERGE_NEXT >= 1;
+  // Flag-synchronised groups (experiment S3H_EXP_FLAG_PREFETCH): the producer's step counter is
+  // read without waiting, just before the next step's rows (LDS executes a wave's reads in
+  // order, and the producer publishes a step only after its rows are written, so rows read
+  // after a counter value that covers the step are that step's rows); it is checked after
+  // rounds 0-15, and only a counter that did not cover the step costs a wait and a second read
+  // of the rows.  Saves the counter read's latency at every step boundary.
+  constexpr bool kFlagPrefetch = FLAGS && S3H_EXP_FLAG_PREFETCH != 0;
 #define S3H_SKEW_FAST(L, P, CUR, NXT)                                                           \
-  if constexpr (kMergeNext) {                                                                   \
+  if constexpr (kMergeNext && kFlagPrefetch) {                                                  \
+    /* the producer's step counter is read with the rows, checked after rounds 0-15 */          \
+    uint32_t seen_prod = 0xffffffffu;                                                           \
+    if (i == kBps - 1) {                                                                        \
+      flag_publish(&flags[1], j + 1);                                                           \
+      seen_prod = __hip_atomic_load(&flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
+      asm volatile("" ::: "memory"); /* the rows are read after the counter */                  \
+      load(NXT, nbuf);                                                                          \
+    } else {                                                                                    \
+      load(NXT, buf + (i + 1) * kBlkStride);                                                    \
+    }                                                                                           \
+    asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_A_##P : S3H_SKEW_STATE : S3H_SKEW_W(CUR));         \
+    if (i == kBps - 1 && __builtin_amdgcn_readfirstlane(seen_prod) < j + 2) {                   \
+      flag_wait_ge(&flags[0], j + 2, alive, A.err); /* not yet produced: wait, read again */    \
+      load(NXT, nbuf);                                                                          \
+    }                                                                                           \
+    asm volatile(S3H_ALIGN8 S3H_##L##_ROUNDS_B_##P S3H_##L##_NEXT_##P                           \
+                 : S3H_SKEW_STATE : S3H_SKEW_W(CUR), S3H_SKEW_WNEXT(NXT));                      \
+  } else if constexpr (kMergeNext) {                                                            \
     if (i == kBps - 1) {                                                                        \
       S3H_SYNC_STEP(j + 1, j + 2);                                                              \
       load(NXT, nbuf);                                                                          \
