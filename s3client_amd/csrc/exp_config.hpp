@@ -55,9 +55,10 @@
 #define S3H_EXP_SKEW_MERGE_NEXT 1
 #endif
 #ifndef S3H_EXP_FLAG_PREFETCH
-// 1: flag-synchronised skew consumers read the producer's step counter with the next step's rows
-// and check it after rounds 0-15 (skew_body kFlagPrefetch)
-#define S3H_EXP_FLAG_PREFETCH 0
+// flag-synchronised skew consumers read the producer's step counter with the next step's rows
+// and check it after rounds 0-15 (skew_body kFlagPrefetch; profiles/r06_flag_prefetch_ab.json:
+// C3 2,217 -> 2,200 cycles per block, C4 skews 2,232 -> 2,220).  0: wait at the step boundary
+#define S3H_EXP_FLAG_PREFETCH 1
 #endif
 #ifndef S3H_EXP_MD5_XCD_PACE
 // 1: MD5 workgroups of the split / mixed dual grids paced by the skew groups on their XCD
@@ -106,7 +107,7 @@ static_assert(S3H_EXP_DUAL_SKEWP_CYC == 2650 && S3H_EXP_DUAL_SKEW_CYC_APART == 2
               "product build: the dual grid's planning rates");
 static_assert(S3H_EXP_SPIN_LIMIT == (1u << 24), "product build: flag waits give up after 2^24 polls");
 static_assert(S3H_EXP_SKEW_MERGE_NEXT == 1, "product build: quad-layout blocks end in one statement");
-static_assert(S3H_EXP_FLAG_PREFETCH == 0, "product build: flag waits at the step boundary");
+static_assert(S3H_EXP_FLAG_PREFETCH == 1, "product build: step counters read with the rows");
 static_assert(S3H_EXP_MD5_XCD_PACE == 0, "product build: MD5 paced within a workgroup only");
 static_assert(S3H_EXP_GPROG_OFF == 0, "product build: skew producers publish their step counts");
 static_assert(S3H_EXP_PACE_LAG == 0, "product build: MD5 waits for its block's own producer step");

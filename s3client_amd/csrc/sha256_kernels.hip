@@ -1110,12 +1110,13 @@ __device__ __forceinline__ void skew_body(const LaunchArgs& A, const uint32_t gr
   // pair layout (skewp) measured 2,476.1 -> 2,485.5 that way and keeps the three statements
   // (profiles/r06_skew_merge_next_ab.json).  S3H_EXP_SKEW_MERGE_NEXT: 0 never, 2 also skewp.
   constexpr bool kMergeNext = PAIR ? S3H_EXP_SKEW_MERGE_NEXT == 2 : S3H_EXP_SKEW_MERGE_NEXT >= 1;
-  // Flag-synchronised groups (experiment S3H_EXP_FLAG_PREFETCH): the producer's step counter is
+  // Flag-synchronised groups (S3H_EXP_FLAG_PREFETCH, on in the product): the producer's step counter is
   // read without waiting, just before the next step's rows (LDS executes a wave's reads in
   // order, and the producer publishes a step only after its rows are written, so rows read
   // after a counter value that covers the step are that step's rows); it is checked after
   // rounds 0-15, and only a counter that did not cover the step costs a wait and a second read
-  // of the rows.  Saves the counter read's latency at every step boundary.
+  // of the rows.  Saves the counter read's latency at every step boundary: C3 2,217 -> 2,200
+  // cycles per block, C4 skews 2,232 -> 2,220 (profiles/r06_flag_prefetch_ab.json).
   constexpr bool kFlagPrefetch = FLAGS && S3H_EXP_FLAG_PREFETCH != 0;
 #define S3H_SKEW_FAST(L, P, CUR, NXT)                                                           \
   if constexpr (kMergeNext && kFlagPrefetch) {                                                  \
